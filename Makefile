@@ -1,0 +1,40 @@
+# Top-level build.  Everything is compiled for gfx950 only.
+#   lib   : dynamic_direct_lidar_odometry_amd/_lib/libddlo_gicp.so (the product: HIP kernels + C-ABI)
+#   oracle: oracle/liboracle.so and oracle/_ref/libref_nanoflann.so (TEST-ONLY checker)
+#   facade: tests/cpp/facade_replay (C++ NanoGICP facade driver, links the product)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := dynamic_direct_lidar_odometry_amd
+CSRC := $(PKG)/csrc
+LIBDIR := $(PKG)/_lib
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/capi.o
+
+all: lib oracle facade
+
+lib: $(LIBDIR)/libddlo_gicp.so
+
+$(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/search.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libddlo_gicp.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle
+
+facade: tests/cpp/facade_replay
+
+tests/cpp/facade_replay: tests/cpp/facade_replay.cpp include/nano_gicp/nano_gicp.hpp include/ddlo_gicp.h $(LIBDIR)/libddlo_gicp.so
+	g++ -std=c++17 -O2 -Iinclude -o $@ tests/cpp/facade_replay.cpp -L$(LIBDIR) -lddlo_gicp -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+clean:
+	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so tests/cpp/facade_replay
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib oracle facade clean

@@ -1,0 +1,372 @@
+"""MI355X-native GICP scan-matching core (drop-in for DDLO's NanoGICP S2S/S2M path).
+
+The product is the C-ABI library ``_lib/libddlo_gicp.so`` (HIP kernels for
+gfx950 + host runtime, declared in ``include/ddlo_gicp.h``).  This module is a
+thin ctypes mirror of the reference's ``nano_gicp::NanoGICP`` surface
+(reference ``include/nano_gicp/nano_gicp.hpp:58-148``) used by the tests and
+``bench.py``; the C++ facade for native callers is ``include/nano_gicp/nano_gicp.hpp``.
+
+There is no CPU fallback: if the HIP library is missing or no device is
+visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = ["GicpParams", "GicpResult", "Context", "NanoGICP", "GicpError", "lib_path", "load",
+           "REG_NONE", "REG_MIN_EIG", "REG_NORMALIZED_MIN_EIG", "REG_PLANE", "REG_FROBENIUS",
+           "GAUSS_NEWTON", "LEVENBERG_MARQUARDT", "SOURCE", "TARGET"]
+
+REG_NONE, REG_MIN_EIG, REG_NORMALIZED_MIN_EIG, REG_PLANE, REG_FROBENIUS = range(5)
+GAUSS_NEWTON, LEVENBERG_MARQUARDT = 0, 1
+SOURCE, TARGET = 0, 1
+COV_MAT4D, COV_SYM6 = 0, 1
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+STATUS = {0: "GICP_OK", 1: "GICP_EINVAL", 2: "GICP_ENOTARGET", 3: "GICP_ENOSOURCE", 4: "GICP_ETOOFEW",
+          5: "GICP_EHIP", 6: "GICP_ENOMEM", 7: "GICP_ESTATE", 8: "GICP_ENONFINITE"}
+
+
+class GicpError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"{STATUS.get(status, status)}: {msg}")
+        self.status = status
+
+
+class GicpParams(C.Structure):
+    _fields_ = [
+        ("k_correspondences", C.c_int32),
+        ("max_iterations", C.c_int32),
+        ("max_correspondence_distance", C.c_double),
+        ("transformation_epsilon", C.c_double),
+        ("rotation_epsilon", C.c_double),
+        ("lm_init_lambda_factor", C.c_double),
+        ("regularization", C.c_int32),
+        ("optimizer", C.c_int32),
+        ("lm_max_iterations", C.c_int32),
+        ("fixed_iterations", C.c_int32),
+    ]
+
+    def replace(self, **kw):
+        p = GicpParams()
+        C.pointer(p)[0] = self
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+
+class GicpResult(C.Structure):
+    _fields_ = [
+        ("converged", C.c_int32),
+        ("nr_iterations", C.c_int32),
+        ("iterations_run", C.c_int32),
+        ("lm_failed", C.c_int32),
+        ("lm_trials", C.c_int32),
+        ("num_correspondences", C.c_int32),
+        ("final_cost", C.c_double),
+        ("final_hessian", C.c_double * 36),
+        ("lm_lambda", C.c_double),
+        ("device_ms", C.c_double),
+        ("linearize_ms", C.c_double),
+    ]
+
+
+def lib_path() -> str:
+    return os.path.join(_HERE, "_lib", "libddlo_gicp.so")
+
+
+def load():
+    """Load the HIP library (raises if it was not built — no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP library not built: {path} (run __graft_entry__.build() or `make lib`)")
+    L = C.CDLL(path)
+    P, S, I, D = C.c_void_p, C.c_size_t, C.c_int, C.c_double
+    sig = {
+        "gicp_abi_version": (C.c_int32, []),
+        "gicp_last_error": (C.c_char_p, []),
+        "gicp_default_params": (I, [C.POINTER(GicpParams)]),
+        "gicp_ctx_create": (I, [I, C.POINTER(P)]),
+        "gicp_ctx_destroy": (I, [P]),
+        "gicp_set_params": (I, [P, C.POINTER(GicpParams)]),
+        "gicp_get_params": (I, [P, C.POINTER(GicpParams)]),
+        "gicp_set_source": (I, [P, P, S, S, I]),
+        "gicp_set_target": (I, [P, P, S, S]),
+        "gicp_clear_source": (I, [P]),
+        "gicp_clear_target": (I, [P]),
+        "gicp_get_size": (I, [P, I, C.POINTER(S)]),
+        "gicp_compute_covariances": (I, [P, I]),
+        "gicp_set_covariances": (I, [P, I, P, S, I]),
+        "gicp_get_covariances": (I, [P, I, P, S, I]),
+        "gicp_has_covariances": (I, [P, I, C.POINTER(I)]),
+        "gicp_swap_source_target": (I, [P]),
+        "gicp_share_source": (I, [P, P]),
+        "gicp_align": (I, [P, P, P, C.POINTER(GicpResult)]),
+        "gicp_get_residuals": (I, [P, P, S]),
+        "gicp_get_correspondences": (I, [P, P, P, S]),
+        "gicp_transform_source": (I, [P, P, S, S]),
+        "gicp_linearize": (I, [P, P, P, P, P, P]),
+        "gicp_knn_target": (I, [P, P, S, S, I, P, P]),
+        "gicp_get_moments": (I, [P, P]),
+        "gicp_set_profiling": (I, [P, I]),
+        "gicp_get_stream": (I, [P, C.POINTER(P)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def default_params(**kw) -> GicpParams:
+    p = GicpParams()
+    load().gicp_default_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _xyz(points):
+    a = np.asarray(points)
+    if a.dtype == np.float32 and a.ndim == 2 and a.shape[1] >= 3 and a.flags.c_contiguous:
+        return a, a.strides[0]
+    a = np.ascontiguousarray(np.asarray(points, dtype=np.float32).reshape(-1, 3))
+    return a, 12
+
+
+class Context:
+    """One gicp_ctx (one NanoGICP instance) on one HIP device."""
+
+    def __init__(self, device: int = 0, params: GicpParams | None = None):
+        self.L = load()
+        h = C.c_void_p()
+        self._check(self.L.gicp_ctx_create(device, C.byref(h)))
+        self.h = h
+        if params is not None:
+            self.set_params(params)
+
+    def _check(self, rc):
+        if rc != 0:
+            raise GicpError(rc, self.L.gicp_last_error().decode())
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gicp_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- params
+    def set_params(self, p: GicpParams):
+        self._check(self.L.gicp_set_params(self.h, C.byref(p)))
+
+    def get_params(self) -> GicpParams:
+        p = GicpParams()
+        self._check(self.L.gicp_get_params(self.h, C.byref(p)))
+        return p
+
+    # ---- clouds
+    def set_source(self, points, build_index=True):
+        a, stride = _xyz(points)
+        self._check(self.L.gicp_set_source(self.h, _ptr(a), len(a), stride, int(build_index)))
+
+    def set_target(self, points):
+        a, stride = _xyz(points)
+        self._check(self.L.gicp_set_target(self.h, _ptr(a), len(a), stride))
+
+    def clear_source(self):
+        self._check(self.L.gicp_clear_source(self.h))
+
+    def clear_target(self):
+        self._check(self.L.gicp_clear_target(self.h))
+
+    def size(self, side) -> int:
+        n = C.c_size_t()
+        self._check(self.L.gicp_get_size(self.h, side, C.byref(n)))
+        return n.value
+
+    def compute_covariances(self, side):
+        self._check(self.L.gicp_compute_covariances(self.h, side))
+
+    def set_covariances(self, side, cov):
+        cov = np.ascontiguousarray(cov, np.float64)
+        layout = COV_MAT4D if cov.shape[-1] == 16 or cov.shape[-2:] == (4, 4) else COV_SYM6
+        n = cov.shape[0]
+        self._check(self.L.gicp_set_covariances(self.h, side, _ptr(cov), n, layout))
+
+    def get_covariances(self, side, layout=COV_SYM6):
+        n = self.size(side)
+        out = np.zeros((n, 16 if layout == COV_MAT4D else 6), np.float64)
+        self._check(self.L.gicp_get_covariances(self.h, side, _ptr(out), n, layout))
+        return out
+
+    def has_covariances(self, side) -> bool:
+        v = C.c_int()
+        self._check(self.L.gicp_has_covariances(self.h, side, C.byref(v)))
+        return bool(v.value)
+
+    def swap_source_target(self):
+        self._check(self.L.gicp_swap_source_target(self.h))
+
+    def share_source_from(self, other: "Context"):
+        self._check(self.L.gicp_share_source(self.h, other.h))
+
+    # ---- registration
+    def align(self, guess=None):
+        out = np.zeros((4, 4), np.float32)
+        res = GicpResult()
+        g = None if guess is None else np.ascontiguousarray(guess, np.float32)
+        self._check(self.L.gicp_align(self.h, None if g is None else _ptr(g), _ptr(out), C.byref(res)))
+        return out, res
+
+    def residuals(self):
+        n = self.size(SOURCE)
+        out = np.zeros(n, np.float64)
+        self._check(self.L.gicp_get_residuals(self.h, _ptr(out), n))
+        return out
+
+    def correspondences(self):
+        n = self.size(SOURCE)
+        corr = np.zeros(n, np.int32)
+        sqd = np.zeros(n, np.float32)
+        self._check(self.L.gicp_get_correspondences(self.h, _ptr(corr), _ptr(sqd), n))
+        return corr, sqd
+
+    def transform_source(self, out=None):
+        n = self.size(SOURCE)
+        if out is None:
+            out = np.zeros((n, 3), np.float32)
+        self._check(self.L.gicp_transform_source(self.h, _ptr(out), n, out.strides[0]))
+        return out
+
+    def linearize(self, pose):
+        pose = np.ascontiguousarray(pose, np.float64)
+        H = np.zeros((6, 6)); b = np.zeros(6); cost = C.c_double(); nc = C.c_int32()
+        self._check(self.L.gicp_linearize(self.h, _ptr(pose), _ptr(H), _ptr(b), C.byref(cost), C.byref(nc)))
+        return H, b, cost.value, nc.value
+
+    def moments(self):
+        out = np.zeros(80)
+        self._check(self.L.gicp_get_moments(self.h, _ptr(out)))
+        return out
+
+    def knn_target(self, queries, k):
+        q, stride = _xyz(queries)
+        idx = np.zeros((len(q), k), np.int32)
+        d = np.zeros((len(q), k), np.float32)
+        self._check(self.L.gicp_knn_target(self.h, _ptr(q), len(q), stride, k, _ptr(idx), _ptr(d)))
+        return idx, d
+
+    def set_profiling(self, on=True):
+        self._check(self.L.gicp_set_profiling(self.h, int(on)))
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        self._check(self.L.gicp_get_stream(self.h, C.byref(s)))
+        return s.value or 0
+
+
+class NanoGICP:
+    """Reference-shaped facade (method names of nano_gicp::NanoGICP + the PCL
+    Registration calls OdomNode makes, odom.cc:92-112,518-532,745-851)."""
+
+    def __init__(self, device=0):
+        self.ctx = Context(device)
+        self.params = self.ctx.get_params()
+        self._src_id = None
+        self._tgt_id = None
+        self._final = np.eye(4, dtype=np.float32)
+        self._converged = False
+        self.last_result = None
+
+    def _push(self):
+        self.ctx.set_params(self.params)
+
+    # PCL Registration setters used by OdomNode
+    def setMaximumIterations(self, n): self.params.max_iterations = int(n); self._push()
+    def setTransformationEpsilon(self, e): self.params.transformation_epsilon = float(e); self._push()
+    def setMaxCorrespondenceDistance(self, d): self.params.max_correspondence_distance = float(d); self._push()
+    def setEuclideanFitnessEpsilon(self, e): pass          # no-op for NanoGICP
+    def setRANSACIterations(self, n): pass                 # no-op
+    def setRANSACOutlierRejectionThreshold(self, t): pass  # no-op
+    def setSearchMethodSource(self, *a): pass              # no-op (force_no_recompute)
+    def setSearchMethodTarget(self, *a): pass
+    def setNumThreads(self, n): pass                       # CPU-only knob
+    # NanoGICP / LsqRegistration setters
+    def setCorrespondenceRandomness(self, k): self.params.k_correspondences = int(k); self._push()
+    def setRegularizationMethod(self, m): self.params.regularization = int(m); self._push()
+    def setRotationEpsilon(self, e): self.params.rotation_epsilon = float(e); self._push()
+    def setInitialLambdaFactor(self, f): self.params.lm_init_lambda_factor = float(f); self._push()
+
+    def setInputSource(self, cloud):
+        if self._src_id is not None and self._src_id == id(cloud):   # pointer identity (:135)
+            return
+        self.ctx.set_source(cloud, True)
+        self._src_id = id(cloud)
+
+    def registerInputSource(self, cloud):
+        if self._src_id is not None and self._src_id == id(cloud):
+            return
+        self.ctx.set_source(cloud, False)
+        self._src_id = id(cloud)
+
+    def setInputTarget(self, cloud):
+        if self._tgt_id is not None and self._tgt_id == id(cloud):
+            return
+        self.ctx.set_target(cloud)
+        self._tgt_id = id(cloud)
+
+    def setSourceCovariances(self, covs): self.ctx.set_covariances(SOURCE, covs)
+    def setTargetCovariances(self, covs): self.ctx.set_covariances(TARGET, covs)
+    def calculateSourceCovariances(self): self.ctx.compute_covariances(SOURCE); return True
+    def calculateTargetCovariances(self): self.ctx.compute_covariances(TARGET); return True
+    def getSourceCovariances(self): return self.ctx.get_covariances(SOURCE, COV_MAT4D).reshape(-1, 4, 4)
+    def getTargetCovariances(self): return self.ctx.get_covariances(TARGET, COV_MAT4D).reshape(-1, 4, 4)
+
+    def swapSourceAndTarget(self):
+        self.ctx.swap_source_target()
+        self._src_id, self._tgt_id = self._tgt_id, self._src_id
+
+    def clearSource(self): self.ctx.clear_source(); self._src_id = None
+    def clearTarget(self): self.ctx.clear_target(); self._tgt_id = None
+
+    def shareSourceFrom(self, other: "NanoGICP"):
+        """odom.cc:530 + :765 (source_kdtree_ alias + source_covs_ copy)."""
+        self.ctx.share_source_from(other.ctx)
+        self._src_id = other._src_id
+
+    def align(self, guess=None):
+        out, res = self.ctx.align(guess)
+        self._final = out
+        self._converged = bool(res.converged)
+        self.last_result = res
+        return self.ctx.transform_source()
+
+    def getFinalTransformation(self): return self._final.copy()
+    def hasConverged(self): return self._converged
+    def getFinalHessian(self): return np.array(self.last_result.final_hessian).reshape(6, 6)
+    def getResiduals(self, trans=None): return self.ctx.residuals()

@@ -1,0 +1,726 @@
+// capi.hip — host runtime behind include/ddlo_gicp.h.
+//
+// Owns device clouds (ref-counted, so swap/share are O(1)), builds the
+// Morton-sorted search hierarchy (K1), and runs align() as ONE hipGraph:
+//   k_align_init, then max_iterations x {k_linearize, k_lm_step}
+// whose kernels become no-ops once the on-device LM has converged or
+// failed.  The host synchronises once per align, to read back the pose.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/ddlo_gicp.h"
+#include "gicp_types.hpp"
+#include "launch.hpp"
+
+using namespace ddlo;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+gicp_status fail(gicp_status s, const std::string& msg) {
+  g_last_error = msg;
+  return s;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return fail(_e == hipErrorOutOfMemory ? GICP_ENOMEM : GICP_EHIP,                      \
+                  std::string(#expr) + ": " + hipGetErrorString(_e));                       \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t b) {
+    if (b <= bytes && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(b, 256));
+    if (e == hipSuccess) bytes = std::max<size_t>(b, 256);
+    return e;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+// Immutable device cloud + search hierarchy (shared between ctxs/sides).
+struct CloudData {
+  int n = 0;
+  DevBuf pts, keys, perm, inv_perm, box_lo, box_hi, quant;
+  int nlevels = 0;
+  int lvl_off[kMaxLevels] = {0};
+  int lvl_cnt[kMaxLevels] = {0};
+  CloudDev dev() const {
+    CloudDev c;
+    c.pts = pts.as<float4>();
+    c.keys = keys.as<unsigned long long>();
+    c.perm = perm.as<int>();
+    c.inv_perm = inv_perm.as<int>();
+    c.box_lo = box_lo.as<float4>();
+    c.box_hi = box_hi.as<float4>();
+    c.quant = quant.as<float>();
+    c.n = n;
+    c.nlevels = nlevels;
+    for (int l = 0; l < kMaxLevels; ++l) {
+      c.lvl_off[l] = lvl_off[l];
+      c.lvl_cnt[l] = lvl_cnt[l];
+    }
+    return c;
+  }
+};
+
+struct CovData {
+  int n = 0;
+  DevBuf cov6;  // sym6 per SORTED point
+};
+
+struct Side {
+  std::shared_ptr<CloudData> cloud;
+  std::shared_ptr<CovData> cov;
+  bool has_cov() const { return cloud && cov && cov->n == cloud->n; }
+};
+
+int levels_for(int n, int* cnt, int* off) {
+  int c = (n + kLeafSize - 1) / kLeafSize;
+  int L = 0, o = 0;
+  for (;;) {
+    if (L >= kMaxLevels) return -1;
+    cnt[L] = c;
+    off[L] = o;
+    o += c;
+    ++L;
+    if (c <= kFanout) break;
+    c = (c + kFanout - 1) / kFanout;
+  }
+  return L;
+}
+
+}  // namespace
+
+struct gicp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  gicp_params params{};
+  Side src, tgt;
+  // build scratch
+  DevBuf raw_bytes, raw_pts, partial, nonfinite, keys_tmp, vals_tmp, sort_tmp;
+  // align buffers
+  DevBuf corr, sqd, slab, job_dev, state_dev, tmp_out;
+  AlignJob* job_host = nullptr;   // pinned
+  AlignState* state_host = nullptr;  // pinned
+  int* flag_host = nullptr;       // pinned
+  bool have_align = false;        // a linearize ran against the current src/tgt
+  int last_nsrc = 0;
+  // graph cache
+  hipGraphExec_t graph_exec = nullptr;
+  hipGraph_t graph = nullptr;
+  std::tuple<int, int, const void*> graph_key{-1, -1, nullptr};
+  bool profiling = false;
+  std::vector<hipEvent_t> prof_ev;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+
+gicp_status set_device(const gicp_ctx* c) {
+  HIP_TRY(hipSetDevice(c->device));
+  return GICP_OK;
+}
+
+gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, std::shared_ptr<CloudData>* out) {
+  if (!xyz || n == 0 || stride < 12 || (stride % 4) != 0) return fail(GICP_EINVAL, "invalid cloud (null, empty or bad stride)");
+  if (n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "cloud too large");
+  auto cd = std::make_shared<CloudData>();
+  const int N = (int)n;
+  cd->n = N;
+  cd->nlevels = levels_for(N, cd->lvl_cnt, cd->lvl_off);
+  if (cd->nlevels < 0) return fail(GICP_EINVAL, "cloud too large for the search hierarchy");
+  const int total_boxes = cd->lvl_off[cd->nlevels - 1] + cd->lvl_cnt[cd->nlevels - 1];
+  hipStream_t s = c->stream;
+  const size_t raw_sz = (n - 1) * stride + 12;
+  HIP_TRY(c->raw_bytes.ensure(raw_sz));
+  HIP_TRY(hipMemcpyAsync(c->raw_bytes.p, xyz, raw_sz, hipMemcpyHostToDevice, s));
+  const int nb = (N + 255) / 256;
+  HIP_TRY(c->raw_pts.ensure(sizeof(float4) * n));
+  HIP_TRY(c->partial.ensure(sizeof(float) * 6 * nb));
+  HIP_TRY(c->nonfinite.ensure(sizeof(int)));
+  HIP_TRY(hipMemsetAsync(c->nonfinite.p, 0, sizeof(int), s));
+  HIP_TRY(cd->quant.ensure(sizeof(float) * 8));
+  launch_pack_bbox(s, c->raw_bytes.as<unsigned char>(), stride, N, c->raw_pts.as<float4>(), c->partial.as<float>(),
+                   c->nonfinite.as<int>(), nb);
+  launch_bbox_final(s, c->partial.as<float>(), nb, cd->quant.as<float>());
+  HIP_TRY(c->keys_tmp.ensure(sizeof(unsigned long long) * n));
+  HIP_TRY(c->vals_tmp.ensure(sizeof(int) * n));
+  HIP_TRY(cd->keys.ensure(sizeof(unsigned long long) * n));
+  HIP_TRY(cd->perm.ensure(sizeof(int) * n));
+  launch_morton(s, c->raw_pts.as<float4>(), N, cd->quant.as<float>(), c->keys_tmp.as<unsigned long long>(),
+                c->vals_tmp.as<int>());
+  size_t tmp_bytes = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, c->keys_tmp.as<unsigned long long>(),
+                                             cd->keys.as<unsigned long long>(), c->vals_tmp.as<int>(),
+                                             cd->perm.as<int>(), N, 0, 63, s));
+  HIP_TRY(c->sort_tmp.ensure(tmp_bytes));
+  tmp_bytes = c->sort_tmp.bytes;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp_bytes, c->keys_tmp.as<unsigned long long>(),
+                                             cd->keys.as<unsigned long long>(), c->vals_tmp.as<int>(),
+                                             cd->perm.as<int>(), N, 0, 63, s));
+  HIP_TRY(cd->pts.ensure(sizeof(float4) * n));
+  HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
+  launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, cd->pts.as<float4>(), cd->inv_perm.as<int>());
+  HIP_TRY(cd->box_lo.ensure(sizeof(float4) * total_boxes));
+  HIP_TRY(cd->box_hi.ensure(sizeof(float4) * total_boxes));
+  launch_leaf_boxes(s, cd->pts.as<float4>(), N, cd->lvl_cnt[0], cd->box_lo.as<float4>(), cd->box_hi.as<float4>());
+  for (int l = 1; l < cd->nlevels; ++l)
+    launch_level_boxes(s, cd->box_lo.as<float4>() + cd->lvl_off[l - 1], cd->box_hi.as<float4>() + cd->lvl_off[l - 1],
+                       cd->lvl_cnt[l - 1], cd->lvl_cnt[l], cd->box_lo.as<float4>() + cd->lvl_off[l],
+                       cd->box_hi.as<float4>() + cd->lvl_off[l]);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(c->flag_host, c->nonfinite.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (*c->flag_host) return fail(GICP_ENONFINITE, "cloud contains non-finite coordinates");
+  *out = cd;
+  return GICP_OK;
+}
+
+gicp_status compute_cov(gicp_ctx* c, Side& side) {
+  if (!side.cloud) return fail(GICP_ESTATE, "no cloud on this side");
+  const int k = c->params.k_correspondences;
+  if (k <= 0 || k > 64) return fail(GICP_EINVAL, "k_correspondences must be in [1, 64]");
+  if (side.cloud->n < k) return fail(GICP_ETOOFEW, "cloud has fewer points than k_correspondences");
+  auto cv = std::make_shared<CovData>();
+  cv->n = side.cloud->n;
+  HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * (size_t)cv->n));
+  if (!launch_covariances(c->stream, side.cloud->dev(), k, c->params.regularization, cv->cov6.as<double>()))
+    return fail(GICP_EINVAL, "unsupported k");
+  HIP_TRY(hipGetLastError());
+  side.cov = cv;
+  return GICP_OK;
+}
+
+void invalidate_align(gicp_ctx* c) { c->have_align = false; }
+
+gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
+  AlignJob& j = *c->job_host;
+  std::memset(&j, 0, sizeof(j));
+  j.src = c->src.cloud->dev();
+  j.tgt = c->tgt.cloud->dev();
+  j.src_cov = c->src.cov->cov6.as<double>();
+  j.tgt_cov = c->tgt.cov->cov6.as<double>();
+  j.corr = c->corr.as<int>();
+  j.sqd = c->sqd.as<float>();
+  j.slab = c->slab.as<double>();
+  j.state = c->state_dev.as<AlignState>();
+  for (int r = 0; r < 3; ++r) {
+    for (int cc = 0; cc < 3; ++cc) j.guess_R[3 * r + cc] = guess16 ? (double)guess16[4 * r + cc] : (r == cc ? 1.0 : 0.0);
+    j.guess_t[r] = guess16 ? (double)guess16[4 * r + 3] : 0.0;
+  }
+  const double r = c->params.max_correspondence_distance;
+  j.max_corr2 = r * r;
+  float f = (float)j.max_corr2;
+  if (!std::isfinite(f)) f = FLT_MAX;
+  j.cap2 = std::nextafter(f, INFINITY);
+  j.nblocks = nblocks;
+  j.fixed_iterations = c->params.fixed_iterations;
+  j.max_iterations = c->params.fixed_iterations > 0 ? c->params.fixed_iterations : c->params.max_iterations;
+  j.optimizer = c->params.optimizer;
+  j.lm_max_iterations = c->params.lm_max_iterations;
+  j.lm_init_lambda_factor = c->params.lm_init_lambda_factor;
+  j.transformation_epsilon = c->params.transformation_epsilon;
+  j.rotation_epsilon = c->params.rotation_epsilon;
+  HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
+  return GICP_OK;
+}
+
+int linearize_blocks(int nsrc) {
+  const int groups = (nsrc + 63) / 64;
+  return std::max(1, std::min((groups + 3) / 4, 1024));
+}
+
+gicp_status prepare_align(gicp_ctx* c) {
+  if (!c->src.cloud) return fail(GICP_ENOSOURCE, "no source cloud");
+  if (!c->tgt.cloud) return fail(GICP_ENOTARGET, "no target cloud");
+  // NanoGICP::computeTransformation (:186-193): compute missing covariances
+  if (!c->src.has_cov()) {
+    gicp_status s = compute_cov(c, c->src);
+    if (s) return s;
+  }
+  if (!c->tgt.has_cov()) {
+    gicp_status s = compute_cov(c, c->tgt);
+    if (s) return s;
+  }
+  const int ns = c->src.cloud->n;
+  HIP_TRY(c->corr.ensure(sizeof(int) * ns));
+  HIP_TRY(c->sqd.ensure(sizeof(float) * ns));
+  HIP_TRY(c->slab.ensure(sizeof(double) * kSlabStride * linearize_blocks(ns)));
+  return GICP_OK;
+}
+
+gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks) {
+  const AlignJob* jd = c->job_dev.as<AlignJob>();
+  auto key = std::make_tuple(max_it, nblocks, (const void*)jd);
+  if (!c->graph_exec || c->graph_key != key) {
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    c->graph_exec = nullptr;
+    c->graph = nullptr;
+    HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    launch_align_init(c->stream, jd);
+    for (int i = 0; i < max_it; ++i) {
+      launch_linearize(c->stream, jd, nblocks);
+      launch_lm_step(c->stream, jd);
+    }
+    HIP_TRY(hipStreamEndCapture(c->stream, &c->graph));
+    HIP_TRY(hipGraphInstantiate(&c->graph_exec, c->graph, nullptr, nullptr, 0));
+    c->graph_key = key;
+  }
+  HIP_TRY(hipGraphLaunch(c->graph_exec, c->stream));
+  return GICP_OK;
+}
+
+gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
+  const AlignJob* jd = c->job_dev.as<AlignJob>();
+  const size_t need = 2 * (size_t)max_it;
+  while (c->prof_ev.size() < need) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    c->prof_ev.push_back(e);
+  }
+  launch_align_init(c->stream, jd);
+  for (int i = 0; i < max_it; ++i) {
+    HIP_TRY(hipEventRecord(c->prof_ev[2 * i], c->stream));
+    launch_linearize(c->stream, jd, nblocks);
+    HIP_TRY(hipEventRecord(c->prof_ev[2 * i + 1], c->stream));
+    launch_lm_step(c->stream, jd);
+  }
+  HIP_TRY(hipGetLastError());
+  return GICP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t gicp_abi_version(void) { return DDLO_GICP_ABI_VERSION; }
+const char* gicp_last_error(void) { return g_last_error.c_str(); }
+
+gicp_status gicp_default_params(gicp_params* p) {
+  if (!p) return fail(GICP_EINVAL, "null params");
+  p->k_correspondences = 20;
+  p->max_iterations = 64;
+  p->max_correspondence_distance = FLT_MAX;
+  p->transformation_epsilon = 5e-4;
+  p->rotation_epsilon = 2e-3;
+  p->lm_init_lambda_factor = 1e-9;
+  p->regularization = GICP_REG_PLANE;
+  p->optimizer = GICP_OPT_LEVENBERG_MARQUARDT;
+  p->lm_max_iterations = 10;
+  p->fixed_iterations = 0;
+  return GICP_OK;
+}
+
+gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
+  if (!out) return fail(GICP_EINVAL, "null out");
+  *out = nullptr;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(GICP_EINVAL, "invalid device ordinal");
+  HIP_TRY(hipSetDevice(device));
+  auto c = std::make_unique<gicp_ctx>();
+  c->device = device;
+  gicp_default_params(&c->params);
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipHostMalloc((void**)&c->job_host, sizeof(AlignJob), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&c->state_host, sizeof(AlignState), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&c->flag_host, sizeof(int) * 4, hipHostMallocDefault));
+  HIP_TRY(c->job_dev.ensure(sizeof(AlignJob)));
+  HIP_TRY(c->state_dev.ensure(sizeof(AlignState)));
+  std::memset(c->state_host, 0, sizeof(AlignState));
+  for (int i = 0; i < 6; ++i) c->state_host->final_hessian[7 * i] = 1.0;  // final_hessian_.setIdentity()
+  HIP_TRY(hipMemcpy(c->state_dev.p, c->state_host, sizeof(AlignState), hipMemcpyHostToDevice));
+  HIP_TRY(hipEventCreate(&c->ev0));
+  HIP_TRY(hipEventCreate(&c->ev1));
+  *out = c.release();
+  return GICP_OK;
+}
+
+gicp_status gicp_ctx_destroy(gicp_ctx* c) {
+  if (!c) return GICP_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+  if (c->graph) (void)hipGraphDestroy(c->graph);
+  for (auto e : c->prof_ev) (void)hipEventDestroy(e);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->job_host) (void)hipHostFree(c->job_host);
+  if (c->state_host) (void)hipHostFree(c->state_host);
+  if (c->flag_host) (void)hipHostFree(c->flag_host);
+  c->src = Side();
+  c->tgt = Side();
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return GICP_OK;
+}
+
+gicp_status gicp_set_params(gicp_ctx* c, const gicp_params* p) {
+  if (!c || !p) return fail(GICP_EINVAL, "null argument");
+  if (p->regularization < 0 || p->regularization > 4) return fail(GICP_EINVAL, "invalid regularization method");
+  if (p->optimizer < 0 || p->optimizer > 1) return fail(GICP_EINVAL, "invalid optimizer");
+  if (p->k_correspondences < 1 || p->k_correspondences > 64) return fail(GICP_EINVAL, "k_correspondences must be in [1, 64]");
+  if (p->lm_max_iterations < 1 || p->max_iterations < 0 || p->fixed_iterations < 0)
+    return fail(GICP_EINVAL, "invalid iteration limits");
+  if (!(p->max_correspondence_distance > 0) || !(p->transformation_epsilon > 0) || !(p->rotation_epsilon > 0))
+    return fail(GICP_EINVAL, "distances/epsilons must be positive");
+  c->params = *p;
+  return GICP_OK;
+}
+
+gicp_status gicp_get_params(const gicp_ctx* c, gicp_params* out) {
+  if (!c || !out) return fail(GICP_EINVAL, "null argument");
+  *out = c->params;
+  return GICP_OK;
+}
+
+gicp_status gicp_set_source(gicp_ctx* c, const float* xyz, size_t n, size_t stride, int build_index) {
+  (void)build_index;  // the device cloud is always sorted + indexed (cheap)
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  std::shared_ptr<CloudData> cd;
+  s = build_cloud(c, xyz, n, stride, &cd);
+  if (s) return s;
+  c->src.cloud = cd;
+  c->src.cov.reset();  // setInputSource clears source covariances (:142)
+  invalidate_align(c);
+  return GICP_OK;
+}
+
+gicp_status gicp_set_target(gicp_ctx* c, const float* xyz, size_t n, size_t stride) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  std::shared_ptr<CloudData> cd;
+  s = build_cloud(c, xyz, n, stride, &cd);
+  if (s) return s;
+  c->tgt.cloud = cd;
+  c->tgt.cov.reset();  // (:154)
+  invalidate_align(c);
+  return GICP_OK;
+}
+
+gicp_status gicp_clear_source(gicp_ctx* c) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  c->src = Side();
+  invalidate_align(c);
+  return GICP_OK;
+}
+gicp_status gicp_clear_target(gicp_ctx* c) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  c->tgt = Side();
+  invalidate_align(c);
+  return GICP_OK;
+}
+
+gicp_status gicp_get_size(const gicp_ctx* c, int side, size_t* n) {
+  if (!c || !n) return fail(GICP_EINVAL, "null argument");
+  const Side& sd = side == GICP_SIDE_SOURCE ? c->src : c->tgt;
+  *n = sd.cloud ? (size_t)sd.cloud->n : 0;
+  return GICP_OK;
+}
+
+gicp_status gicp_compute_covariances(gicp_ctx* c, int side) {
+  if (!c || (side != 0 && side != 1)) return fail(GICP_EINVAL, "invalid argument");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  s = compute_cov(c, side == GICP_SIDE_SOURCE ? c->src : c->tgt);
+  if (s) return s;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GICP_OK;
+}
+
+gicp_status gicp_set_covariances(gicp_ctx* c, int side, const double* cov, size_t n, int layout) {
+  if (!c || !cov || (side != 0 && side != 1) || (layout != 0 && layout != 1)) return fail(GICP_EINVAL, "invalid argument");
+  Side& sd = side == GICP_SIDE_SOURCE ? c->src : c->tgt;
+  if (!sd.cloud) return fail(GICP_ESTATE, "set the cloud before its covariances");
+  if ((int)n != sd.cloud->n) return fail(GICP_EINVAL, "covariance count != cloud size");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  const size_t w = layout == GICP_COV_MAT4D ? 16 : 6;
+  HIP_TRY(c->tmp_out.ensure(sizeof(double) * w * n));
+  HIP_TRY(hipMemcpyAsync(c->tmp_out.p, cov, sizeof(double) * w * n, hipMemcpyHostToDevice, c->stream));
+  auto cv = std::make_shared<CovData>();  // copy semantics (:161,168): never mutate a shared CovData
+  cv->n = (int)n;
+  HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * n));
+  launch_cov_import(c->stream, c->tmp_out.as<double>(), layout, (int)n, sd.cloud->inv_perm.as<int>(), cv->cov6.as<double>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  sd.cov = cv;
+  return GICP_OK;
+}
+
+gicp_status gicp_get_covariances(const gicp_ctx* cc, int side, double* cov, size_t n, int layout) {
+  gicp_ctx* c = const_cast<gicp_ctx*>(cc);
+  if (!c || !cov || (side != 0 && side != 1) || (layout != 0 && layout != 1)) return fail(GICP_EINVAL, "invalid argument");
+  Side& sd = side == GICP_SIDE_SOURCE ? c->src : c->tgt;
+  if (!sd.has_cov()) return fail(GICP_ESTATE, "no covariances on this side");
+  if ((int)n != sd.cloud->n) return fail(GICP_EINVAL, "n != cloud size");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  const size_t w = layout == GICP_COV_MAT4D ? 16 : 6;
+  HIP_TRY(c->tmp_out.ensure(sizeof(double) * w * n));
+  launch_cov_export(c->stream, sd.cov->cov6.as<double>(), layout, (int)n, sd.cloud->perm.as<int>(), c->tmp_out.as<double>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(cov, c->tmp_out.p, sizeof(double) * w * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GICP_OK;
+}
+
+gicp_status gicp_has_covariances(const gicp_ctx* c, int side, int* has) {
+  if (!c || !has || (side != 0 && side != 1)) return fail(GICP_EINVAL, "invalid argument");
+  *has = (side == GICP_SIDE_SOURCE ? c->src : c->tgt).has_cov() ? 1 : 0;
+  return GICP_OK;
+}
+
+gicp_status gicp_swap_source_target(gicp_ctx* c) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  std::swap(c->src, c->tgt);  // clouds, indices and covariances (:100-102)
+  invalidate_align(c);        // correspondences_.clear() (:104-105)
+  return GICP_OK;
+}
+
+gicp_status gicp_share_source(gicp_ctx* dst, const gicp_ctx* src) {
+  if (!dst || !src) return fail(GICP_EINVAL, "null ctx");
+  if (dst->device != src->device) return fail(GICP_EINVAL, "contexts live on different devices");
+  dst->src = src->src;
+  invalidate_align(dst);
+  return GICP_OK;
+}
+
+gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_result* res) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  s = prepare_align(c);
+  if (s) return s;
+  const int ns = c->src.cloud->n;
+  const int nblocks = linearize_blocks(ns);
+  s = fill_job(c, guess16, nblocks);
+  if (s) return s;
+  const int max_it = c->job_host->max_iterations;
+  HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  if (c->profiling)
+    s = run_align_eager_profiled(c, max_it, nblocks);
+  else
+    s = run_align_graph(c, max_it, nblocks);
+  if (s) return s;
+  HIP_TRY(hipEventRecord(c->ev1, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const AlignState& st = *c->state_host;
+  c->have_align = st.iter > 0;
+  c->last_nsrc = ns;
+  if (out16) {
+    for (int r = 0; r < 3; ++r) {
+      for (int cc = 0; cc < 3; ++cc) out16[4 * r + cc] = (float)st.R[3 * r + cc];
+      out16[4 * r + 3] = (float)st.t[r];
+    }
+    out16[12] = out16[13] = out16[14] = 0.f;
+    out16[15] = 1.f;
+  }
+  if (res) {
+    std::memset(res, 0, sizeof(*res));
+    res->converged = st.converged;
+    res->nr_iterations = st.nr_iterations;
+    res->iterations_run = st.iter;
+    res->lm_failed = st.lm_failed;
+    res->lm_trials = st.lm_trials;
+    res->num_correspondences = st.num_corr;
+    res->final_cost = st.final_cost;
+    std::memcpy(res->final_hessian, st.final_hessian, sizeof(res->final_hessian));
+    res->lm_lambda = st.lambda;
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    res->device_ms = ms;
+    if (c->profiling) {
+      double tot = 0.0;
+      for (int i = 0; i < st.iter; ++i) {
+        float m = 0.f;
+        HIP_TRY(hipEventElapsedTime(&m, c->prof_ev[2 * i], c->prof_ev[2 * i + 1]));
+        tot += m;
+      }
+      res->linearize_ms = tot;
+    }
+  }
+  if (st.lm_failed) g_last_error = "lm not converged!!";
+  return GICP_OK;
+}
+
+gicp_status gicp_get_residuals(gicp_ctx* c, double* out, size_t n) {
+  if (!c || !out) return fail(GICP_EINVAL, "null argument");
+  if (!c->have_align || !c->src.cloud || !c->tgt.cloud) return fail(GICP_ESTATE, "no linearization to report residuals of");
+  if ((int)n != c->src.cloud->n) return fail(GICP_EINVAL, "n != source size");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  HIP_TRY(c->tmp_out.ensure(sizeof(double) * n));
+  launch_residuals(c->stream, c->job_dev.as<AlignJob>(), (int)n, c->tmp_out.as<double>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, c->tmp_out.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GICP_OK;
+}
+
+gicp_status gicp_get_correspondences(gicp_ctx* c, int32_t* corr, float* sq_dist, size_t n) {
+  if (!c || (!corr && !sq_dist)) return fail(GICP_EINVAL, "null argument");
+  if (!c->have_align || !c->src.cloud) return fail(GICP_ESTATE, "no linearization");
+  if ((int)n != c->src.cloud->n) return fail(GICP_EINVAL, "n != source size");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  HIP_TRY(c->tmp_out.ensure((sizeof(int) + sizeof(float)) * n + 64));
+  int* dcorr = c->tmp_out.as<int>();
+  float* dsqd = reinterpret_cast<float*>(c->tmp_out.as<char>() + ((sizeof(int) * n + 63) / 64) * 64);
+  launch_export_corr(c->stream, c->job_dev.as<AlignJob>(), (int)n, dcorr, dsqd);
+  HIP_TRY(hipGetLastError());
+  if (corr) HIP_TRY(hipMemcpyAsync(corr, dcorr, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+  if (sq_dist) HIP_TRY(hipMemcpyAsync(sq_dist, dsqd, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GICP_OK;
+}
+
+gicp_status gicp_transform_source(gicp_ctx* c, float* out_xyz, size_t n, size_t stride) {
+  if (!c || !out_xyz || stride < 12 || stride % 4) return fail(GICP_EINVAL, "invalid argument");
+  if (!c->src.cloud) return fail(GICP_ENOSOURCE, "no source");
+  if ((int)n != c->src.cloud->n) return fail(GICP_EINVAL, "n != source size");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  // final_transformation_ = x0.cast<float>() of the last align
+  float T[16];
+  const AlignState& st = *c->state_host;
+  for (int r = 0; r < 3; ++r) {
+    for (int cc = 0; cc < 3; ++cc) T[4 * r + cc] = (float)st.R[3 * r + cc];
+    T[4 * r + 3] = (float)st.t[r];
+  }
+  T[12] = T[13] = T[14] = 0.f;
+  T[15] = 1.f;
+  const size_t bytes = (n - 1) * stride + 12;
+  HIP_TRY(c->tmp_out.ensure(bytes + 256));
+  float* dT = reinterpret_cast<float*>(c->tmp_out.as<char>() + ((bytes + 63) / 64) * 64);
+  HIP_TRY(hipMemcpyAsync(dT, T, sizeof(T), hipMemcpyHostToDevice, c->stream));
+  // keep the caller's other fields (e.g. intensity): start from their buffer
+  HIP_TRY(hipMemcpyAsync(c->tmp_out.p, out_xyz, bytes, hipMemcpyHostToDevice, c->stream));
+  launch_transform(c->stream, c->src.cloud->pts.as<float4>(), (int)n, c->src.cloud->perm.as<int>(), dT,
+                   c->tmp_out.as<float>(), stride / 4);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out_xyz, c->tmp_out.p, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GICP_OK;
+}
+
+gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, double* b6, double* cost, int32_t* ncorr) {
+  if (!c || !pose16) return fail(GICP_EINVAL, "null argument");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  s = prepare_align(c);
+  if (s) return s;
+  const int ns = c->src.cloud->n;
+  const int nblocks = linearize_blocks(ns);
+  float g[16];
+  for (int i = 0; i < 16; ++i) g[i] = 0.f;
+  s = fill_job(c, g, nblocks);
+  if (s) return s;
+  // exact double pose (not the float guess path)
+  for (int r = 0; r < 3; ++r) {
+    for (int cc = 0; cc < 3; ++cc) c->job_host->guess_R[3 * r + cc] = pose16[4 * r + cc];
+    c->job_host->guess_t[r] = pose16[4 * r + 3];
+  }
+  c->job_host->optimizer = GICP_OPT_GAUSS_NEWTON;
+  c->job_host->max_iterations = 1;
+  c->job_host->fixed_iterations = 1;
+  HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
+  const AlignJob* jd = c->job_dev.as<AlignJob>();
+  launch_align_init(c->stream, jd);
+  launch_linearize(c->stream, jd, nblocks);
+  launch_lm_step(c->stream, jd);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const AlignState& st = *c->state_host;
+  if (H36) std::memcpy(H36, st.final_hessian, sizeof(double) * 36);
+  if (cost) *cost = st.final_cost;
+  if (ncorr) *ncorr = st.num_corr;
+  if (b6) std::memcpy(b6, st.last_b, sizeof(double) * 6);
+  c->have_align = true;
+  c->last_nsrc = ns;
+  return GICP_OK;
+}
+
+gicp_status gicp_knn_target(gicp_ctx* c, const float* q, size_t nq, size_t stride, int k, int32_t* idx, float* sqd) {
+  if (!c || !q || !idx || !sqd || nq == 0 || stride < 12 || stride % 4) return fail(GICP_EINVAL, "invalid argument");
+  if (!c->tgt.cloud) return fail(GICP_ENOTARGET, "no target");
+  if (k < 1 || k > 64) return fail(GICP_EINVAL, "k must be in [1, 64]");
+  if (c->tgt.cloud->n < k) return fail(GICP_ETOOFEW, "target has fewer than k points");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  const size_t raw = (nq - 1) * stride + 12;
+  HIP_TRY(c->raw_bytes.ensure(raw));
+  HIP_TRY(hipMemcpyAsync(c->raw_bytes.p, q, raw, hipMemcpyHostToDevice, c->stream));
+  const int nb = (int)((nq + 255) / 256);
+  HIP_TRY(c->raw_pts.ensure(sizeof(float4) * nq));
+  HIP_TRY(c->partial.ensure(sizeof(float) * 6 * nb));
+  HIP_TRY(c->nonfinite.ensure(sizeof(int)));
+  launch_pack_bbox(c->stream, c->raw_bytes.as<unsigned char>(), stride, (int)nq, c->raw_pts.as<float4>(),
+                   c->partial.as<float>(), c->nonfinite.as<int>(), nb);
+  HIP_TRY(c->tmp_out.ensure((sizeof(int) + sizeof(float)) * nq * k + 64));
+  int* didx = c->tmp_out.as<int>();
+  float* dd = reinterpret_cast<float*>(c->tmp_out.as<char>() + ((sizeof(int) * nq * k + 63) / 64) * 64);
+  if (!launch_knn_query(c->stream, c->tgt.cloud->dev(), c->raw_pts.as<float4>(), (int)nq, k, didx, dd))
+    return fail(GICP_EINVAL, "unsupported k");
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(idx, didx, sizeof(int) * nq * k, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(sqd, dd, sizeof(float) * nq * k, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GICP_OK;
+}
+
+gicp_status gicp_get_moments(const gicp_ctx* c, double* out80) {
+  if (!c || !out80) return fail(GICP_EINVAL, "null argument");
+  std::memcpy(out80, c->state_host->last_mom, sizeof(double) * kSlabStride);
+  return GICP_OK;
+}
+
+gicp_status gicp_set_profiling(gicp_ctx* c, int enable) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  c->profiling = enable != 0;
+  return GICP_OK;
+}
+
+gicp_status gicp_get_stream(const gicp_ctx* c, void** stream) {
+  if (!c || !stream) return fail(GICP_EINVAL, "null argument");
+  *stream = (void*)c->stream;
+  return GICP_OK;
+}
+
+}  // extern "C"

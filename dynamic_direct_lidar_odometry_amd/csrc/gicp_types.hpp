@@ -1,0 +1,85 @@
+// gicp_types.hpp — plain data shared by the host runtime (capi.cpp) and the
+// HIP kernels.  Everything here is POD so it can be memcpy'd into device
+// memory as a job descriptor.
+#pragma once
+#include <stdint.h>
+
+namespace ddlo {
+
+// Search hierarchy geometry (see DESIGN.md "Cloud index"):
+//   points sorted by 63-bit Morton key, leaves = 32 consecutive points,
+//   every internal level groups 64 consecutive nodes of the level below, so a
+//   wavefront tests one node's 64 children with one lane each.
+constexpr int kLeafSize = 32;
+constexpr int kFanout = 64;
+constexpr int kMaxLevels = 5;   // leaves + 4 internal levels: n <= 32*64^4
+
+// Number of moment slots the linearize kernel reduces per source point
+// (see DESIGN.md "Normal-equation moments"): 6 (sum M) + 18 (sum q_k M) +
+// 36 (sum q_k q_l M) + 12 (sum (M e) qtilde^T) + cost + count = 74, padded to
+// 96 for the 6-step in-register transpose reduction.
+constexpr int kMoments = 74;
+constexpr int kMomentSlots = 96;
+constexpr int kSlabStride = 80;   // doubles per block partial in the slab
+
+struct CloudDev {
+  const float4* pts;              // n sorted points; w = original index (int bits)
+  const unsigned long long* keys; // n sorted Morton keys
+  const int* perm;                // sorted position -> original index
+  const int* inv_perm;            // original index -> sorted position
+  const float4* box_lo;           // all levels, level 0 = leaves
+  const float4* box_hi;
+  const float* quant;             // device [lo.x, lo.y, lo.z, scale]
+  int n;
+  int nlevels;
+  int lvl_off[kMaxLevels];
+  int lvl_cnt[kMaxLevels];
+};
+
+// Per-align device state (one per ctx, lives in device memory).
+struct AlignState {
+  double R[9];           // x0 (current estimate), row-major
+  double t[3];
+  double lambda;         // lm_lambda_
+  double final_hessian[36];
+  double final_cost;     // y0 of the last linearize
+  double last_lin_R[9];  // pose of the last linearization (getResiduals)
+  double last_lin_t[3];
+  double last_b[6];      // b of the last linearize
+  double last_mom[kSlabStride];  // reduced moments of the last linearize
+  int iter;              // outer iterations executed so far
+  int done;              // converged or failed: remaining kernels are no-ops
+  int converged;
+  int nr_iterations;
+  int lm_failed;
+  int lm_trials;
+  int num_corr;
+  int have_prev;         // correspondences of a previous linearize are valid
+  int pad[4];
+};
+
+// Everything a kernel needs for one align, written by the host before launch.
+struct AlignJob {
+  CloudDev src;
+  CloudDev tgt;
+  const double* src_cov;   // sym6 per sorted source point
+  const double* tgt_cov;   // sym6 per sorted target point
+  int* corr;               // per sorted source point: sorted target pos or -1
+  float* sqd;              // per sorted source point: squared 1-NN distance
+  double* slab;            // [nblocks][kSlabStride] partial moments
+  AlignState* state;
+  double guess_R[9];
+  double guess_t[3];
+  double max_corr2;        // max_correspondence_distance^2 (double compare)
+  float cap2;              // nextafter(float(max_corr2), +inf), the search bound
+  int nblocks;             // linearize grid size (blocks)
+  int max_iterations;      // outer loop bound (max or fixed iterations)
+  int fixed_iterations;
+  int optimizer;           // 0 GN, 1 LM
+  int lm_max_iterations;
+  double lm_init_lambda_factor;
+  double transformation_epsilon;
+  double rotation_epsilon;
+};
+
+}  // namespace ddlo

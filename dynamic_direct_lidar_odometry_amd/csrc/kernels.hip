@@ -1,0 +1,1231 @@
+// kernels.hip — hand-written gfx950 kernels of the GICP hot path.
+//
+//   K1 index build      k_pack_bbox, k_bbox_final, k_morton, k_gather,
+//                       k_leaf_boxes, k_level_boxes   (radix sort: index_build.hip)
+//   K2 kNN-k covariance k_covariances<KCAP,EXACT>        calculate_covariances
+//                                                       nano_gicp_impl.hpp:373-441
+//   K3 linearize        k_linearize                     update_correspondences +
+//                                                       linearize :234-342
+//   K5 LM / GN step     k_lm_step                       lsq_registration_impl.hpp:95-232
+//   K6 outputs          k_residuals, k_transform        getResiduals :225-232,
+//                                                       transformPointCloud lsq:125
+// Compiled with -ffp-contract=off: fp32 distance / transform arithmetic must
+// not be contracted into FMAs so that correspondences equal the oracle's.
+#include <hip/hip_runtime.h>
+
+#include "gicp_types.hpp"
+#include "search.hpp"
+#include "launch.hpp"
+
+#include <algorithm>
+
+namespace ddlo {
+
+// ============================================================================
+// K1: cloud packing, bbox, Morton keys, hierarchy boxes
+// ============================================================================
+__global__ __launch_bounds__(256) void k_pack_bbox(const unsigned char* __restrict__ raw, size_t stride, int n,
+                                                   float4* __restrict__ out, float* __restrict__ partial,
+                                                   int* __restrict__ nonfinite) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float x = 0.f, y = 0.f, z = 0.f;
+  bool ok = false;
+  if (i < n) {
+    const float* p = reinterpret_cast<const float*>(raw + (size_t)i * stride);
+    x = p[0];
+    y = p[1];
+    z = p[2];
+    ok = true;
+    if (!(isfinite(x) && isfinite(y) && isfinite(z))) {
+      atomicOr(nonfinite, 1);
+      ok = false;
+    }
+    out[i] = make_float4(x, y, z, __int_as_float(i));
+  }
+  __shared__ float red[6][4];
+  float v[6] = {ok ? x : INFINITY, ok ? y : INFINITY, ok ? z : INFINITY,
+                ok ? x : -INFINITY, ok ? y : -INFINITY, ok ? z : -INFINITY};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    v[a] = wave_min(v[a]);
+    v[a + 3] = wave_max(v[a + 3]);
+  }
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0)
+    for (int a = 0; a < 6; ++a) red[a][w] = v[a];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int a = threadIdx.x;
+    float r = red[a][0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = a < 3 ? fminf(r, red[a][k]) : fmaxf(r, red[a][k]);
+    partial[blockIdx.x * 6 + a] = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bbox_final(const float* __restrict__ partial, int nparts,
+                                                    float* __restrict__ quant) {
+  // one block; thread a reduces component a
+  __shared__ float bb[6];
+  if (threadIdx.x < 6) {
+    const int a = threadIdx.x;
+    float r = a < 3 ? INFINITY : -INFINITY;
+    for (int k = 0; k < nparts; ++k) r = a < 3 ? fminf(r, partial[k * 6 + a]) : fmaxf(r, partial[k * 6 + a]);
+    bb[a] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float ext = fmaxf(fmaxf(bb[3] - bb[0], bb[4] - bb[1]), bb[5] - bb[2]);
+    quant[0] = bb[0];
+    quant[1] = bb[1];
+    quant[2] = bb[2];
+    quant[3] = ext > 0.f ? 2097151.f / ext : 1.f;
+    quant[4] = bb[3];
+    quant[5] = bb[4];
+    quant[6] = bb[5];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_morton(const float4* __restrict__ pts, int n, const float* __restrict__ quant,
+                                                unsigned long long* __restrict__ keys, int* __restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = pts[i];
+  keys[i] = morton_key(p.x, p.y, p.z, quant);
+  vals[i] = i;
+}
+
+__global__ __launch_bounds__(256) void k_gather(const float4* __restrict__ raw, const int* __restrict__ perm, int n,
+                                                float4* __restrict__ sorted, int* __restrict__ inv_perm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int o = perm[i];
+  sorted[i] = raw[o];
+  inv_perm[o] = i;
+}
+
+// one 32-lane half-wave per leaf
+__global__ __launch_bounds__(256) void k_leaf_boxes(const float4* __restrict__ pts, int n, int nleaves,
+                                                    float4* __restrict__ lo, float4* __restrict__ hi) {
+  const int leaf = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int sub = threadIdx.x & 31;
+  const int p = leaf * kLeafSize + sub;
+  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  if (leaf < nleaves && p < n) {
+    const float4 q = pts[p];
+    v[0] = v[3] = q.x;
+    v[1] = v[4] = q.y;
+    v[2] = v[5] = q.z;
+  }
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      v[a] = fminf(v[a], __shfl_xor(v[a], m));
+      v[a + 3] = fmaxf(v[a + 3], __shfl_xor(v[a + 3], m));
+    }
+  }
+  if (sub == 0 && leaf < nleaves) {
+    lo[leaf] = make_float4(v[0], v[1], v[2], 0.f);
+    hi[leaf] = make_float4(v[3], v[4], v[5], 0.f);
+  }
+}
+
+// one wavefront per parent node, lane = child
+__global__ __launch_bounds__(256) void k_level_boxes(const float4* __restrict__ clo, const float4* __restrict__ chi,
+                                                     int nchild, int nparent, float4* __restrict__ plo,
+                                                     float4* __restrict__ phi) {
+  const int parent = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int c = parent * kFanout + lane_id();
+  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  if (parent < nparent && c < nchild) {
+    const float4 a = clo[c], b = chi[c];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z;
+    v[3] = b.x; v[4] = b.y; v[5] = b.z;
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    v[a] = wave_min(v[a]);
+    v[a + 3] = wave_max(v[a + 3]);
+  }
+  if (lane_id() == 0 && parent < nparent) {
+    plo[parent] = make_float4(v[0], v[1], v[2], 0.f);
+    phi[parent] = make_float4(v[3], v[4], v[5], 0.f);
+  }
+}
+
+// ============================================================================
+// small fp64 linear algebra (per lane)
+// ============================================================================
+// Symmetric 3x3 cyclic Jacobi eigen-decomposition: lam[j], V[j][i] = v_j[i]
+__device__ void sym_eig3(const double A[9], double lam[3], double V[3][3]) {
+  double a00 = A[0], a01 = A[1], a02 = A[2], a11 = A[4], a12 = A[5], a22 = A[8];
+  double v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  for (int sweep = 0; sweep < 50; ++sweep) {
+    const double off = fabs(a01) + fabs(a02) + fabs(a12);
+    const double scale = fabs(a00) + fabs(a11) + fabs(a22);
+    if (off <= 1e-300 || off <= scale * 1e-18) break;
+#pragma unroll
+    for (int pq = 0; pq < 3; ++pq) {
+      const int p = pq == 2 ? 1 : 0;
+      const int q = pq == 0 ? 1 : 2;
+      double m[3][3] = {{a00, a01, a02}, {a01, a11, a12}, {a02, a12, a22}};
+      const double apq = m[p][q];
+      if (apq == 0.0) continue;
+      const double theta = (m[q][q] - m[p][p]) / (2.0 * apq);
+      const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+      const double c = 1.0 / sqrt(t * t + 1.0);
+      const double s = t * c;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double akp = m[k][p], akq = m[k][q];
+        m[k][p] = c * akp - s * akq;
+        m[k][q] = s * akp + c * akq;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double apk = m[p][k], aqk = m[q][k];
+        m[p][k] = c * apk - s * aqk;
+        m[q][k] = s * apk + c * aqk;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double vkp = v[k][p], vkq = v[k][q];
+        v[k][p] = c * vkp - s * vkq;
+        v[k][q] = s * vkp + c * vkq;
+      }
+      a00 = m[0][0]; a01 = m[0][1]; a02 = m[0][2];
+      a11 = m[1][1]; a12 = m[1][2]; a22 = m[2][2];
+    }
+  }
+  lam[0] = a00; lam[1] = a11; lam[2] = a22;
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) V[j][i] = v[i][j];
+}
+
+// 3x3 inverse by adjugate (general, row-major)
+__device__ __forceinline__ void inv3(const double m[9], double r[9]) {
+  const double c00 = m[4] * m[8] - m[5] * m[7];
+  const double c01 = m[5] * m[6] - m[3] * m[8];
+  const double c02 = m[3] * m[7] - m[4] * m[6];
+  const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
+  const double id = 1.0 / det;
+  r[0] = c00 * id;
+  r[1] = (m[2] * m[7] - m[1] * m[8]) * id;
+  r[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+  r[3] = c01 * id;
+  r[4] = (m[0] * m[8] - m[2] * m[6]) * id;
+  r[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+  r[6] = c02 * id;
+  r[7] = (m[1] * m[6] - m[0] * m[7]) * id;
+  r[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+// regularisation of a covariance (nano_gicp_impl.hpp:401-437)
+__device__ void regularize(const double C[9], int method, double out[6]) {
+  double R[9];
+  if (method == 0) {  // NONE
+    for (int i = 0; i < 9; ++i) R[i] = C[i];
+  } else if (method == 4) {  // FROBENIUS: ((C + 1e-3 I)^-1 / ||.||_F)^-1
+    double Cl[9], Ci[9];
+    for (int i = 0; i < 9; ++i) Cl[i] = C[i] + ((i % 4 == 0) ? 1e-3 : 0.0);
+    inv3(Cl, Ci);
+    double nrm = 0;
+    for (int i = 0; i < 9; ++i) nrm += Ci[i] * Ci[i];
+    nrm = sqrt(nrm);
+    for (int i = 0; i < 9; ++i) Ci[i] /= nrm;
+    inv3(Ci, R);
+  } else {  // JacobiSVD route: U diag(vals) V^T with U col = sign(lambda) V col
+    double lam[3], V[3][3];
+    sym_eig3(C, lam, V);
+    // order by |lambda| descending (stable for equal values: index order)
+    int o0 = 0, o1 = 1, o2 = 2;
+    if (fabs(lam[o1]) > fabs(lam[o0])) { int t = o0; o0 = o1; o1 = t; }
+    if (fabs(lam[o2]) > fabs(lam[o1])) {
+      int t = o1; o1 = o2; o2 = t;
+      if (fabs(lam[o1]) > fabs(lam[o0])) { t = o0; o0 = o1; o1 = t; }
+    }
+    const int ord[3] = {o0, o1, o2};
+    double sv[3], vals[3];
+    for (int i = 0; i < 3; ++i) sv[i] = fabs(lam[ord[i]]);
+    if (method == 3) {  // PLANE
+      vals[0] = 1; vals[1] = 1; vals[2] = 1e-3;
+    } else if (method == 1) {  // MIN_EIG
+      for (int i = 0; i < 3; ++i) vals[i] = fmax(sv[i], 1e-3);
+    } else {  // NORMALIZED_MIN_EIG
+      for (int i = 0; i < 3; ++i) vals[i] = fmax(sv[i] / sv[0], 1e-3);
+    }
+    for (int i = 0; i < 9; ++i) R[i] = 0.0;
+    for (int j = 0; j < 3; ++j) {
+      const int oj = ord[j];
+      const double sgn = lam[oj] < 0 ? -1.0 : 1.0;
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) R[3 * r + c] += sgn * V[oj][r] * vals[j] * V[oj][c];
+    }
+  }
+  out[0] = R[0]; out[1] = R[1]; out[2] = R[2];
+  out[3] = R[4]; out[4] = R[5]; out[5] = R[8];
+}
+
+// ============================================================================
+// K2: exact kNN-k (self queries) + covariance
+// ============================================================================
+template <int KCAP, bool EXACT>
+struct KnnVisitor {
+  WaveBox box;
+  float qx, qy, qz;
+  bool active;
+  int k;
+  float D[KCAP];
+  int J[KCAP];
+  float wd;   // worst kept (bound)
+  int wj;
+  int skip_lo, skip_hi;
+
+  __device__ __forceinline__ void init(int kk) {
+    k = kk;
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      D[s] = INFINITY;
+      J[s] = -1;
+    }
+    wd = INFINITY;
+    wj = -1;
+    skip_lo = 1;
+    skip_hi = 0;
+  }
+  __device__ __forceinline__ void update_worst() {
+    if constexpr (EXACT) {
+      wd = D[KCAP - 1];
+      wj = J[KCAP - 1];
+    } else {
+#pragma unroll
+      for (int s = 0; s < KCAP; ++s) {
+        if (s == k - 1) {
+          wd = D[s];
+          wj = J[s];
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void insert(float d, int j) {
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      const bool lt = d < D[s] || (d == D[s] && (unsigned)j < (unsigned)J[s]);
+      const float td = lt ? D[s] : d;
+      const int tj = lt ? J[s] : j;
+      D[s] = lt ? d : D[s];
+      J[s] = lt ? j : J[s];
+      d = td;
+      j = tj;
+    }
+    update_worst();
+  }
+  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf) {
+    const int start = leaf * kLeafSize;
+    const int cnt = min(kLeafSize, c.n - start);
+    const int lane = lane_id();
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane < cnt) p = c.pts[start + lane];
+    for (int j = 0; j < cnt; ++j) {
+      const float d = dist2(qx, qy, qz, readlane_f(p.x, j), readlane_f(p.y, j), readlane_f(p.z, j));
+      const int pj = start + j;
+      const bool cand = active && (d < wd || (d == wd && (unsigned)pj < (unsigned)wj));
+      if (cand) insert(d, pj);
+    }
+  }
+  __device__ __forceinline__ void leaf(const CloudDev& c, int leaf) {
+    if (leaf >= skip_lo && leaf <= skip_hi) return;
+    const float4 lo = c.box_lo[leaf], hi = c.box_hi[leaf];
+    const bool need = active && box_dist2(qx, qy, qz, lo, hi) <= wd;
+    if (!__any(need)) return;
+    const float before = wd;
+    scan_leaf(c, leaf);
+    if (__any(wd < before)) box = make_wave_box(active, qx, qy, qz, wd);
+  }
+};
+
+// Seed a kNN visitor with the leaves [s0, s1] and then run the full traversal.
+template <int KCAP, bool EXACT>
+__device__ __forceinline__ void knn_search(const CloudDev& c, KnnVisitor<KCAP, EXACT>& vis, int s0, int s1) {
+  s0 = max(s0, 0);
+  s1 = min(s1, c.lvl_cnt[0] - 1);
+  for (int l = s0; l <= s1; ++l) vis.scan_leaf(c, l);
+  vis.skip_lo = s0;
+  vis.skip_hi = s1;
+  vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.wd);
+  traverse(c, vis);
+}
+
+// covariances of a cloud: wave w handles sorted points [64w, 64w+64) (leaves 2w, 2w+1)
+template <int KCAP, bool EXACT>
+__global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int method, double* __restrict__ cov6) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
+  const int ngroups = (c.n + 63) >> 6;
+  for (int g = wave; g < ngroups; g += nwaves_total) {
+    const int i = g * 64 + lane_id();
+    KnnVisitor<KCAP, EXACT> vis;
+    vis.init(k);
+    vis.active = i < c.n;
+    const float4 q = c.pts[min(i, c.n - 1)];
+    vis.qx = q.x;
+    vis.qy = q.y;
+    vis.qz = q.z;
+    knn_search(c, vis, 2 * g - 1, 2 * g + 2);
+    if (!vis.active) continue;
+    // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
+    double mx = 0, my = 0, mz = 0;
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      if (s < k) {
+        const float4 p = c.pts[vis.J[s]];
+        mx += (double)p.x;
+        my += (double)p.y;
+        mz += (double)p.z;
+      }
+    }
+    mx /= k;
+    my /= k;
+    mz /= k;
+    double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      if (s < k) {
+        const float4 p = c.pts[vis.J[s]];
+        const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
+        C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
+        C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
+        C[6] += d2 * d0; C[7] += d2 * d1; C[8] += d2 * d2;
+      }
+    }
+    for (int e = 0; e < 9; ++e) C[e] /= k;
+    double out[6];
+    regularize(C, method, out);
+    double* o = cov6 + 6 * (size_t)i;
+    for (int e = 0; e < 6; ++e) o[e] = out[e];
+  }
+}
+
+// kNN of external queries (any order) against a cloud; outputs original indices.
+template <int KCAP, bool EXACT>
+__global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __restrict__ q, int nq, int k,
+                                                   int* __restrict__ out_idx, float* __restrict__ out_d) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
+  const int ngroups = (nq + 63) >> 6;
+  for (int g = wave; g < ngroups; g += nwaves_total) {
+    const int i = g * 64 + lane_id();
+    KnnVisitor<KCAP, EXACT> vis;
+    vis.init(k);
+    vis.active = i < nq;
+    const float4 p = q[min(i, nq - 1)];
+    vis.qx = p.x;
+    vis.qy = p.y;
+    vis.qz = p.z;
+    // seed around the Morton position of the first lane's query
+    const float sx = uniform_f(p.x), sy = uniform_f(p.y), sz = uniform_f(p.z);
+    const int pos = wave_lower_bound(c.keys, c.n, morton_key(sx, sy, sz, c.quant));
+    const int leaf = min(pos, c.n - 1) / kLeafSize;
+    knn_search(c, vis, leaf - 1, leaf + 1);
+    if (!vis.active) continue;
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      if (s < k) {
+        const int j = vis.J[s];
+        out_idx[(size_t)i * k + s] = j >= 0 ? c.perm[j] : -1;
+        out_d[(size_t)i * k + s] = vis.D[s];
+      }
+    }
+  }
+}
+
+template __global__ void k_covariances<10, true>(CloudDev, int, int, double*);
+template __global__ void k_covariances<20, true>(CloudDev, int, int, double*);
+template __global__ void k_covariances<16, false>(CloudDev, int, int, double*);
+template __global__ void k_covariances<32, false>(CloudDev, int, int, double*);
+template __global__ void k_covariances<64, false>(CloudDev, int, int, double*);
+template __global__ void k_knn_query<1, true>(CloudDev, const float4*, int, int, int*, float*);
+template __global__ void k_knn_query<10, true>(CloudDev, const float4*, int, int, int*, float*);
+template __global__ void k_knn_query<20, true>(CloudDev, const float4*, int, int, int*, float*);
+template __global__ void k_knn_query<16, false>(CloudDev, const float4*, int, int, int*, float*);
+template __global__ void k_knn_query<32, false>(CloudDev, const float4*, int, int, int*, float*);
+template __global__ void k_knn_query<64, false>(CloudDev, const float4*, int, int, int*, float*);
+
+// covariance import/export between original order (host layout) and sorted sym6
+__global__ __launch_bounds__(256) void k_cov_import(const double* __restrict__ in, int layout, int n,
+                                                    const int* __restrict__ inv_perm, double* __restrict__ cov6) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // original index
+  if (i >= n) return;
+  double* o = cov6 + 6 * (size_t)inv_perm[i];
+  if (layout == 0) {  // MAT4D row-major
+    const double* m = in + 16 * (size_t)i;
+    o[0] = m[0]; o[1] = m[1]; o[2] = m[2]; o[3] = m[5]; o[4] = m[6]; o[5] = m[10];
+  } else {
+    const double* m = in + 6 * (size_t)i;
+    for (int e = 0; e < 6; ++e) o[e] = m[e];
+  }
+}
+__global__ __launch_bounds__(256) void k_cov_export(const double* __restrict__ cov6, int layout, int n,
+                                                    const int* __restrict__ perm, double* __restrict__ out) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;  // sorted index
+  if (s >= n) return;
+  const double* c = cov6 + 6 * (size_t)s;
+  const int i = perm[s];
+  if (layout == 0) {
+    double* m = out + 16 * (size_t)i;
+    m[0] = c[0]; m[1] = c[1]; m[2] = c[2]; m[3] = 0;
+    m[4] = c[1]; m[5] = c[3]; m[6] = c[4]; m[7] = 0;
+    m[8] = c[2]; m[9] = c[4]; m[10] = c[5]; m[11] = 0;
+    m[12] = 0; m[13] = 0; m[14] = 0; m[15] = 0;
+  } else {
+    double* m = out + 6 * (size_t)i;
+    for (int e = 0; e < 6; ++e) m[e] = c[e];
+  }
+}
+
+// ============================================================================
+// K3: fused correspondence search + Mahalanobis + normal-equation moments
+// ============================================================================
+struct Contrib {
+  double M[6];   // Mahalanobis (xx xy xz yy yz zz)
+  double q[3];   // transformed source point (double)
+  double qq[6];  // q_k q_l (00 01 02 11 12 22)
+  double v[3];   // M e
+  double y;      // e^T M e
+  double c;      // 1 if matched
+};
+
+template <int S>
+__device__ __forceinline__ double moment_val(const Contrib& C) {
+  if constexpr (S < 6) {
+    return C.M[S];
+  } else if constexpr (S < 24) {
+    return C.q[(S - 6) / 6] * C.M[(S - 6) % 6];
+  } else if constexpr (S < 60) {
+    return C.qq[(S - 24) / 6] * C.M[(S - 24) % 6];
+  } else if constexpr (S < 72) {
+    constexpr int m = (S - 60) / 4, kk = (S - 60) % 4;
+    if constexpr (kk == 3)
+      return C.v[m];
+    else
+      return C.v[m] * C.q[kk];
+  } else if constexpr (S == 72) {
+    return C.y;
+  } else if constexpr (S == 73) {
+    return C.c;
+  } else {
+    return 0.0;
+  }
+}
+
+// In-register transpose reduction step L (L = 1..5): the lane whose bit
+// (6 - L) is 0 keeps the lower-half slot a, the other keeps b; each receives
+// its partner's copy of the kept slot.  Steps 1 and 2 use the gfx950
+// v_permlane32_swap / v_permlane16_swap (no LDS, no selects), steps 3..5 DPP
+// row_mirror / row_half_mirror / quad_perm pairings.
+__device__ __forceinline__ double dpp_f64(double x, int ctrl_sel) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  int rlo, rhi;
+  switch (ctrl_sel) {
+    case 0:  // row_mirror: l <-> 15 - l (bit 3 differs)
+      rlo = __builtin_amdgcn_update_dpp(0, lo, 0x140, 0xf, 0xf, false);
+      rhi = __builtin_amdgcn_update_dpp(0, hi, 0x140, 0xf, 0xf, false);
+      break;
+    case 1:  // row_half_mirror: l <-> 7 - l (bit 2 differs)
+      rlo = __builtin_amdgcn_update_dpp(0, lo, 0x141, 0xf, 0xf, false);
+      rhi = __builtin_amdgcn_update_dpp(0, hi, 0x141, 0xf, 0xf, false);
+      break;
+    case 2:  // quad_perm [2,3,0,1]: xor 2
+      rlo = __builtin_amdgcn_update_dpp(0, lo, 0x4e, 0xf, 0xf, false);
+      rhi = __builtin_amdgcn_update_dpp(0, hi, 0x4e, 0xf, 0xf, false);
+      break;
+    default:  // quad_perm [1,0,3,2]: xor 1
+      rlo = __builtin_amdgcn_update_dpp(0, lo, 0xb1, 0xf, 0xf, false);
+      rhi = __builtin_amdgcn_update_dpp(0, hi, 0xb1, 0xf, 0xf, false);
+      break;
+  }
+  return __hiloint2double(rhi, rlo);
+}
+
+template <int L>
+__device__ __forceinline__ double xchg(double a, double b) {
+#ifdef DDLO_SHFL_REDUCE
+  const int bit = 1 << (6 - L);
+  const bool hi = (lane_id() & bit) != 0;
+  const double keep = hi ? b : a;
+  const double send = hi ? a : b;
+  return keep + __shfl_xor(send, bit);
+#else
+  if constexpr (L == 1 || L == 2) {
+    const unsigned alo = __double2loint(a), ahi = __double2hiint(a);
+    const unsigned blo = __double2loint(b), bhi = __double2hiint(b);
+    unsigned x0, x1, y0, y1;
+    if constexpr (L == 1) {
+      const auto rl = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+      const auto rh = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+      x0 = rl[0]; y0 = rl[1]; x1 = rh[0]; y1 = rh[1];
+    } else {
+      const auto rl = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+      const auto rh = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+      x0 = rl[0]; y0 = rl[1]; x1 = rh[0]; y1 = rh[1];
+    }
+    return __hiloint2double(x1, x0) + __hiloint2double(y1, y0);
+  } else {
+    const int bit = 1 << (6 - L);
+    const bool hi = (lane_id() & bit) != 0;
+    const double keep = hi ? b : a;
+    const double send = hi ? a : b;
+    return keep + dpp_f64(send, L - 3);
+  }
+#endif
+}
+
+template <int L, int S>
+__device__ __forceinline__ double treduce(const Contrib& C) {
+  if constexpr (L == 0) {
+    return moment_val<S>(C);
+  } else {
+    constexpr int half = kMomentSlots >> L;
+    const double a = treduce<L - 1, S>(C);
+    const double b = treduce<L - 1, S + half>(C);
+    return xchg<L>(a, b);
+  }
+}
+
+__device__ __forceinline__ double final_pair(double x) {
+#ifdef DDLO_SHFL_REDUCE
+  return x + __shfl_xor(x, 1);
+#else
+  return x + dpp_f64(x, 3);
+#endif
+}
+
+// slot base of the 3 moments a lane owns after the 5 pairing steps
+__device__ __forceinline__ int moment_base(int lane) {
+  return 48 * ((lane >> 5) & 1) + 24 * ((lane >> 4) & 1) + 12 * ((lane >> 3) & 1) + 6 * ((lane >> 2) & 1) +
+         3 * ((lane >> 1) & 1);
+}
+
+__device__ __forceinline__ void load_sym6(const double* p, double c[6]) {
+  const double2 a = reinterpret_cast<const double2*>(p)[0];
+  const double2 b = reinterpret_cast<const double2*>(p)[1];
+  const double2 d = reinterpret_cast<const double2*>(p)[2];
+  c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y; c[4] = d.x; c[5] = d.y;
+}
+
+constexpr int kLinWaves = 4;   // waves per linearize block
+
+__global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < 9; ++i) st->R[i] = job->guess_R[i];
+    for (int i = 0; i < 3; ++i) st->t[i] = job->guess_t[i];
+    st->lambda = -1.0;
+    st->iter = 0;
+    st->done = job->max_iterations <= 0 ? 1 : 0;
+    st->converged = 0;
+    st->nr_iterations = 0;
+    st->lm_failed = 0;
+    st->lm_trials = 0;
+    st->num_corr = 0;
+    st->have_prev = 0;
+    st->final_cost = 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  const CloudDev& src = job->src;
+  const CloudDev& tgt = job->tgt;
+  const double* __restrict__ src_cov = job->src_cov;
+  const double* __restrict__ tgt_cov = job->tgt_cov;
+  int* __restrict__ corr = job->corr;
+  float* __restrict__ sqd = job->sqd;
+  const float cap2 = job->cap2;
+  const double max_corr2 = job->max_corr2;
+  const int have_prev = st->have_prev;
+
+  double R[9], t[3];
+  for (int e = 0; e < 9; ++e) R[e] = st->R[e];
+  for (int e = 0; e < 3; ++e) t[e] = st->t[e];
+  float Rf[9], tf[3];
+  for (int e = 0; e < 9; ++e) Rf[e] = (float)R[e];
+  for (int e = 0; e < 3; ++e) tf[e] = (float)t[e];
+
+  const int lane = lane_id();
+  const int wib = threadIdx.x >> 6;
+  const int wave = blockIdx.x * kLinWaves + wib;
+  const int nwaves_total = gridDim.x * kLinWaves;
+  const int ngroups = (src.n + 63) >> 6;
+
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  for (int g = wave; g < ngroups; g += nwaves_total) {
+    const int i = g * 64 + lane;
+    const bool active = i < src.n;
+    const float4 a = src.pts[active ? i : src.n - 1];
+    // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
+    const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
+    const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
+    const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
+
+    NN1Visitor vis;
+    vis.qx = qx;
+    vis.qy = qy;
+    vis.qz = qz;
+    vis.active = active;
+    vis.best = active ? cap2 : -1.f;
+    vis.bestj = -1;
+    vis.skip_lo = 1;
+    vis.skip_hi = 0;
+    if (have_prev && active) {
+      const int j = corr[i];
+      if (j >= 0) {
+        const float4 p = tgt.pts[j];
+        const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
+        if (d < cap2) {
+          vis.best = d;
+          vis.bestj = j;
+        }
+      }
+    }
+    if (!have_prev) {
+      // seed around the Morton position of the first active lane's query
+      const float sx = uniform_f(qx), sy = uniform_f(qy), sz = uniform_f(qz);
+      const int pos = wave_lower_bound(tgt.keys, tgt.n, morton_key(sx, sy, sz, tgt.quant));
+      const int leaf = min(pos, tgt.n - 1) / kLeafSize;
+      const int s0 = max(leaf - 1, 0), s1 = min(leaf + 2, tgt.lvl_cnt[0] - 1);
+      for (int l = s0; l <= s1; ++l) vis.scan_leaf(tgt, l);
+      vis.skip_lo = s0;
+      vis.skip_hi = s1;
+    }
+    vis.box = make_wave_box(active, qx, qy, qz, vis.best);
+    traverse(tgt, vis);
+
+    const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
+    if (active) {
+      corr[i] = valid ? vis.bestj : -1;
+      sqd[i] = vis.bestj >= 0 ? vis.best : INFINITY;
+    }
+
+    Contrib C;
+    if (valid) {
+      const int j = vis.bestj;
+      const float4 b = tgt.pts[j];
+      double ca[6], cb[6];
+      load_sym6(src_cov + 6 * (size_t)i, ca);
+      load_sym6(tgt_cov + 6 * (size_t)j, cb);
+      const double A[9] = {ca[0], ca[1], ca[2], ca[1], ca[3], ca[4], ca[2], ca[4], ca[5]};
+      // RC = R * CA ; S = RC * R^T ; RCR = CB + S
+      double RC[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) RC[3 * r + cc] = R[3 * r] * A[cc] + R[3 * r + 1] * A[3 + cc] + R[3 * r + 2] * A[6 + cc];
+      double S[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) S[3 * r + cc] = RC[3 * r] * R[3 * cc] + RC[3 * r + 1] * R[3 * cc + 1] + RC[3 * r + 2] * R[3 * cc + 2];
+      const double Cm[9] = {cb[0] + S[0], cb[1] + S[1], cb[2] + S[2], cb[1] + S[3], cb[3] + S[4],
+                            cb[4] + S[5], cb[2] + S[6], cb[4] + S[7], cb[5] + S[8]};
+      double Mi[9];
+      inv3(Cm, Mi);
+      C.M[0] = Mi[0]; C.M[1] = 0.5 * (Mi[1] + Mi[3]); C.M[2] = 0.5 * (Mi[2] + Mi[6]);
+      C.M[3] = Mi[4]; C.M[4] = 0.5 * (Mi[5] + Mi[7]); C.M[5] = Mi[8];
+      const double ax = a.x, ay = a.y, az = a.z;
+      C.q[0] = (R[0] * ax + R[1] * ay) + (R[2] * az + t[0]);
+      C.q[1] = (R[3] * ax + R[4] * ay) + (R[5] * az + t[1]);
+      C.q[2] = (R[6] * ax + R[7] * ay) + (R[8] * az + t[2]);
+      const double e0 = (double)b.x - C.q[0], e1 = (double)b.y - C.q[1], e2 = (double)b.z - C.q[2];
+      C.v[0] = C.M[0] * e0 + C.M[1] * e1 + C.M[2] * e2;
+      C.v[1] = C.M[1] * e0 + C.M[3] * e1 + C.M[4] * e2;
+      C.v[2] = C.M[2] * e0 + C.M[4] * e1 + C.M[5] * e2;
+      C.y = e0 * C.v[0] + e1 * C.v[1] + e2 * C.v[2];
+      C.c = 1.0;
+    } else {
+      for (int e = 0; e < 6; ++e) C.M[e] = 0.0;
+      C.q[0] = C.q[1] = C.q[2] = 0.0;
+      C.v[0] = C.v[1] = C.v[2] = 0.0;
+      C.y = 0.0;
+      C.c = 0.0;
+    }
+    C.qq[0] = C.q[0] * C.q[0]; C.qq[1] = C.q[0] * C.q[1]; C.qq[2] = C.q[0] * C.q[2];
+    C.qq[3] = C.q[1] * C.q[1]; C.qq[4] = C.q[1] * C.q[2]; C.qq[5] = C.q[2] * C.q[2];
+
+    acc0 += final_pair(treduce<5, 0>(C));
+    acc1 += final_pair(treduce<5, 1>(C));
+    acc2 += final_pair(treduce<5, 2>(C));
+  }
+
+  __shared__ double red[kLinWaves][kMomentSlots];
+  if ((lane & 1) == 0) {
+    const int base = moment_base(lane);
+    red[wib][base + 0] = acc0;
+    red[wib][base + 1] = acc1;
+    red[wib][base + 2] = acc2;
+  }
+  __syncthreads();
+  if (threadIdx.x < kSlabStride) {
+    double s = 0.0;
+    if (threadIdx.x < kMoments)
+      for (int w = 0; w < kLinWaves; ++w) s += red[w][threadIdx.x];
+    job->slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5: slab reduction + LM/GN step on one workgroup.
+__device__ void so3_exp_d(const double w[3], double R[9]) {  // gicp/so3.hpp:101-124
+  const double theta_sq = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  double imag, real;
+  if (theta_sq < 1e-10) {
+    const double theta_quad = theta_sq * theta_sq;
+    imag = 0.5 - 1.0 / 48.0 * theta_sq + 1.0 / 3840.0 * theta_quad;
+    real = 1.0 - 1.0 / 8.0 * theta_sq + 1.0 / 384.0 * theta_quad;
+  } else {
+    const double theta = sqrt(theta_sq);
+    const double half = 0.5 * theta;
+    imag = sin(half) / theta;
+    real = cos(half);
+  }
+  const double qw = real, qx = imag * w[0], qy = imag * w[1], qz = imag * w[2];
+  const double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
+  const double twx = tx * qw, twy = ty * qw, twz = tz * qw;
+  const double txx = tx * qx, txy = ty * qx, txz = tz * qx;
+  const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+  R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+  R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+  R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+
+// Eigen::LDLT<Matrix6d>(A).solve(rhs), pivoted (restated, see oracle)
+__device__ void ldlt_solve6_d(const double* A_in, const double* rhs, double* x) {
+  const int n = 6;
+  double m[36];
+  for (int i = 0; i < 36; ++i) m[i] = A_in[i];
+  int tr[6];
+  double temp[6];
+  for (int k = 0; k < n; ++k) {
+    int big = k;
+    double bigv = fabs(m[k * n + k]);
+    for (int i = k + 1; i < n; ++i)
+      if (fabs(m[i * n + i]) > bigv) { bigv = fabs(m[i * n + i]); big = i; }
+    tr[k] = big;
+    if (k != big) {
+      for (int j = 0; j < k; ++j) { double s = m[k * n + j]; m[k * n + j] = m[big * n + j]; m[big * n + j] = s; }
+      for (int i = big + 1; i < n; ++i) { double s = m[i * n + k]; m[i * n + k] = m[i * n + big]; m[i * n + big] = s; }
+      { double s = m[k * n + k]; m[k * n + k] = m[big * n + big]; m[big * n + big] = s; }
+      for (int i = k + 1; i < big; ++i) {
+        double s = m[i * n + k];
+        m[i * n + k] = m[big * n + i];
+        m[big * n + i] = s;
+      }
+    }
+    if (k > 0) {
+      for (int j = 0; j < k; ++j) temp[j] = m[j * n + j] * m[k * n + j];
+      double s = 0;
+      for (int j = 0; j < k; ++j) s += m[k * n + j] * temp[j];
+      m[k * n + k] -= s;
+      for (int i = k + 1; i < n; ++i) {
+        double a = 0;
+        for (int j = 0; j < k; ++j) a += m[i * n + j] * temp[j];
+        m[i * n + k] -= a;
+      }
+    }
+    const double akk = m[k * n + k];
+    if (k < n - 1 && fabs(akk) > 0.0)
+      for (int i = k + 1; i < n; ++i) m[i * n + k] /= akk;
+  }
+  double y[6];
+  for (int i = 0; i < n; ++i) y[i] = rhs[i];
+  for (int k = 0; k < n; ++k) { double s = y[k]; y[k] = y[tr[k]]; y[tr[k]] = s; }
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < i; ++j) y[i] -= m[i * n + j] * y[j];
+  for (int i = 0; i < n; ++i) y[i] = (fabs(m[i * n + i]) > 2.2250738585072014e-308) ? y[i] / m[i * n + i] : 0.0;
+  for (int i = n - 1; i >= 0; --i)
+    for (int j = i + 1; j < n; ++j) y[i] -= m[j * n + i] * y[j];
+  for (int k = n - 1; k >= 0; --k) { double s = y[k]; y[k] = y[tr[k]]; y[tr[k]] = s; }
+  for (int i = 0; i < n; ++i) x[i] = y[i];
+}
+
+// Moment accessors.  W(k,l) = sum M qt_k qt_l (qt = [q;1]), G(m,k) = sum (Me)_m qt_k.
+struct Moments {
+  const double* m;
+  __device__ double W(int k, int l, int a, int b) const {  // (a,b) entry of W(k,l)
+    const int ab = a <= b ? (a == 0 ? b : (a == 1 ? 2 + b : 5)) : (b == 0 ? a : (b == 1 ? 2 + a : 5));
+    if (k == 3 && l == 3) return m[ab];
+    if (k == 3) return m[6 + 6 * l + ab];
+    if (l == 3) return m[6 + 6 * k + ab];
+    const int kk = k <= l ? k : l, ll = k <= l ? l : k;
+    const int kl = kk == 0 ? ll : (kk == 1 ? 2 + ll : 5);
+    return m[24 + 6 * kl + ab];
+  }
+  __device__ double G(int mm, int k) const { return m[60 + 4 * mm + k]; }
+  __device__ double y0() const { return m[72]; }
+  __device__ double count() const { return m[73]; }
+};
+
+// skew generator: skew(q) = sum_c q_c S_c, S_c[r][s]
+__device__ __forceinline__ double Sgen(int c, int r, int s) {
+  // S_0 = [[0,0,0],[0,0,-1],[0,1,0]], S_1 = [[0,0,1],[0,0,0],[-1,0,0]], S_2 = [[0,-1,0],[1,0,0],[0,0,0]]
+  if (c == 0) return (r == 1 && s == 2) ? -1.0 : ((r == 2 && s == 1) ? 1.0 : 0.0);
+  if (c == 1) return (r == 0 && s == 2) ? 1.0 : ((r == 2 && s == 0) ? -1.0 : 0.0);
+  return (r == 0 && s == 1) ? -1.0 : ((r == 1 && s == 0) ? 1.0 : 0.0);
+}
+
+// H = sum J^T M J, b = sum J^T M e with J = [skew(q) | -I] (nano_gicp_impl.hpp:317-324)
+__device__ void build_normal_equations(const Moments& mo, double H[36], double b[6]) {
+  // H_rr(i,j) = sum_{c,d} sum_{r,s} S_c[r][i] W(c,d)[r][s] S_d[s][j]
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+      for (int c = 0; c < 3; ++c)
+        for (int d = 0; d < 3; ++d)
+          for (int r = 0; r < 3; ++r) {
+            const double sr = Sgen(c, r, i);
+            if (sr == 0.0) continue;
+            for (int q = 0; q < 3; ++q) {
+              const double sq = Sgen(d, q, j);
+              if (sq == 0.0) continue;
+              s += sr * mo.W(c, d, r, q) * sq;
+            }
+          }
+      H[6 * i + j] = s;
+    }
+  // H_rt(i,j) = sum_c sum_r S_c[r][i] W(c,3)[r][j] * (-1)
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+      for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) {
+          const double sr = Sgen(c, r, i);
+          if (sr != 0.0) s += sr * mo.W(c, 3, r, j);
+        }
+      H[6 * i + 3 + j] = -s;
+      H[6 * (3 + j) + i] = -s;
+    }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) H[6 * (3 + i) + 3 + j] = mo.W(3, 3, i, j);
+  // b_r(i) = sum_c sum_r S_c[r][i] G(r,c) ; b_t = -G(:,3)
+  for (int i = 0; i < 3; ++i) {
+    double s = 0.0;
+    for (int c = 0; c < 3; ++c)
+      for (int r = 0; r < 3; ++r) {
+        const double sr = Sgen(c, r, i);
+        if (sr != 0.0) s += sr * mo.G(r, c);
+      }
+    b[i] = s;
+    b[3 + i] = -mo.G(i, 3);
+  }
+}
+
+// y0 - y(delta) for the frozen correspondences/M of the last linearize:
+// e' = e - D qt, D = [Rd - I | td]  =>  y0 - y = 2 <D, G> - sum_kl D_k^T W(k,l) D_l
+__device__ double cost_decrease(const Moments& mo, const double Rd[9], const double td[3]) {
+  double D[3][4];
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) D[r][c] = Rd[3 * r + c] - (r == c ? 1.0 : 0.0);
+    D[r][3] = td[r];
+  }
+  double lin = 0.0;
+  for (int r = 0; r < 3; ++r)
+    for (int k = 0; k < 4; ++k) lin += D[r][k] * mo.G(r, k);
+  double quad = 0.0;
+  for (int k = 0; k < 4; ++k)
+    for (int l = 0; l < 4; ++l)
+      for (int a = 0; a < 3; ++a) {
+        double s = 0.0;
+        for (int b2 = 0; b2 < 3; ++b2) s += mo.W(k, l, a, b2) * D[b2][l];
+        quad += D[a][k] * s;
+      }
+  return 2.0 * lin - quad;
+}
+
+__device__ bool is_converged_d(const AlignJob* job, const double Rd[9], const double td[3]) {
+  if (job->fixed_iterations > 0) return false;
+  double m = 0.0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) m = fmax(m, fabs(Rd[3 * i + j] - (i == j ? 1.0 : 0.0)) / job->rotation_epsilon);
+  for (int i = 0; i < 3; ++i) m = fmax(m, fabs(td[i]) / job->transformation_epsilon);
+  return m < 1;
+}
+
+__device__ void compose(const double Rd[9], const double td[3], const double R[9], const double t[3], double Ro[9],
+                        double to[3]) {
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j)
+      Ro[3 * i + j] = Rd[3 * i + 0] * R[0 + j] + Rd[3 * i + 1] * R[3 + j] + Rd[3 * i + 2] * R[6 + j];
+    to[i] = (Rd[3 * i + 0] * t[0] + Rd[3 * i + 1] * t[1] + Rd[3 * i + 2] * t[2]) + td[i];
+  }
+}
+
+constexpr int kLmThreads = 512;
+
+__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  __shared__ double part[6][kSlabStride];
+  __shared__ double mom[kSlabStride];
+  const int tid = threadIdx.x;
+  const int nb = job->nblocks;
+  if (tid < 6 * kSlabStride) {
+    const int v = tid % kSlabStride, p = tid / kSlabStride;
+    double s = 0.0;
+    for (int b = p; b < nb; b += 6) s += job->slab[(size_t)b * kSlabStride + v];
+    part[p][v] = s;
+  }
+  __syncthreads();
+  if (tid < kSlabStride) {
+    double s = 0.0;
+    for (int p = 0; p < 6; ++p) s += part[p][tid];
+    mom[tid] = s;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+
+  const Moments mo{mom};
+  double H[36], b[6];
+  build_normal_equations(mo, H, b);
+  const double y0 = mo.y0();
+  const int it = st->iter;
+  st->nr_iterations = it;
+  st->final_cost = y0;
+  st->num_corr = (int)mo.count();
+  double R[9], t[3];
+  for (int e = 0; e < 9; ++e) R[e] = st->R[e];
+  for (int e = 0; e < 3; ++e) t[e] = st->t[e];
+  for (int e = 0; e < 9; ++e) st->last_lin_R[e] = R[e];
+  for (int e = 0; e < 3; ++e) st->last_lin_t[e] = t[e];
+  for (int e = 0; e < 6; ++e) st->last_b[e] = b[e];
+  for (int e = 0; e < kSlabStride; ++e) st->last_mom[e] = mom[e];
+
+  bool ok = false;
+  double Rd[9], td[3];
+  double nb6[6];
+  for (int e = 0; e < 6; ++e) nb6[e] = -b[e];
+  if (job->optimizer == 0) {  // step_gn (lsq_registration_impl.hpp:155-173)
+    double d[6];
+    ldlt_solve6_d(H, nb6, d);
+    so3_exp_d(d, Rd);
+    td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
+    double Rn[9], tn[3];
+    compose(Rd, td, R, t, Rn, tn);
+    for (int e = 0; e < 9; ++e) st->R[e] = Rn[e];
+    for (int e = 0; e < 3; ++e) st->t[e] = tn[e];
+    for (int e = 0; e < 36; ++e) st->final_hessian[e] = H[e];
+    ok = true;
+  } else {  // step_lm (:175-232)
+    double lambda = st->lambda;
+    if (lambda < 0.0) {
+      double mx = 0.0;
+      for (int e = 0; e < 6; ++e) mx = fmax(mx, fabs(H[7 * e]));
+      lambda = job->lm_init_lambda_factor * mx;
+    }
+    double nu = 2.0;
+    int trials = 0;
+    for (int i = 0; i < job->lm_max_iterations; ++i) {
+      double A[36];
+      for (int e = 0; e < 36; ++e) A[e] = H[e];
+      for (int e = 0; e < 6; ++e) A[7 * e] += lambda;
+      double d[6];
+      ldlt_solve6_d(A, nb6, d);
+      so3_exp_d(d, Rd);
+      td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
+      ++trials;
+      const double dec = cost_decrease(mo, Rd, td);   // y0 - yi
+      double den = 0.0;
+      for (int e = 0; e < 6; ++e) den += d[e] * (lambda * d[e] - b[e]);
+      const double rho = dec / den;
+      if (rho < 0) {
+        if (is_converged_d(job, Rd, td)) {
+          ok = true;
+          break;
+        }
+        lambda = nu * lambda;
+        nu = 2 * nu;
+        continue;
+      }
+      double Rn[9], tn[3];
+      compose(Rd, td, R, t, Rn, tn);
+      for (int e = 0; e < 9; ++e) st->R[e] = Rn[e];
+      for (int e = 0; e < 3; ++e) st->t[e] = tn[e];
+      const double c = 2 * rho - 1;
+      lambda = lambda * fmax(1.0 / 3.0, 1 - c * c * c);
+      for (int e = 0; e < 36; ++e) st->final_hessian[e] = H[e];
+      ok = true;
+      break;
+    }
+    st->lambda = lambda;
+    st->lm_trials += trials;
+  }
+  st->iter = it + 1;
+  st->have_prev = 1;
+  if (!ok) {
+    st->lm_failed = 1;
+    st->done = 1;
+  } else if (is_converged_d(job, Rd, td)) {
+    st->converged = 1;
+    st->done = 1;
+  }
+  if (st->iter >= job->max_iterations) st->done = 1;
+}
+
+// ---------------------------------------------------------------------------
+// K6: residuals (getResiduals) — unbounded 1-NN for points without a
+// correspondence, at the pose of the last linearization.
+__global__ __launch_bounds__(256) void k_residuals(const AlignJob* __restrict__ job, double* __restrict__ out) {
+  const CloudDev& src = job->src;
+  const CloudDev& tgt = job->tgt;
+  const AlignState* st = job->state;
+  float Rf[9], tf[3];
+  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->last_lin_R[e];
+  for (int e = 0; e < 3; ++e) tf[e] = (float)st->last_lin_t[e];
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
+  const int ngroups = (src.n + 63) >> 6;
+  for (int g = wave; g < ngroups; g += nwaves_total) {
+    const int i = g * 64 + lane_id();
+    const bool active = i < src.n;
+    float d2 = active ? job->sqd[i] : 0.f;
+    const bool need = active && !(d2 < INFINITY);
+    if (__any(need)) {
+      const float4 a = src.pts[active ? i : src.n - 1];
+      NN1Visitor vis;
+      vis.qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
+      vis.qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
+      vis.qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
+      vis.active = need;
+      vis.best = need ? INFINITY : -1.f;
+      vis.bestj = -1;
+      // seed: the nearest of a Morton window per lane (finite bound)
+      if (need) {
+        const int pos = min(wave_lower_bound_lane(tgt.keys, tgt.n,
+                                                  morton_key(vis.qx, vis.qy, vis.qz, tgt.quant)), tgt.n - 1);
+        for (int o = -4; o <= 4; ++o) {
+          const int j = pos + o;
+          if (j < 0 || j >= tgt.n) continue;
+          const float4 p = tgt.pts[j];
+          const float d = dist2(vis.qx, vis.qy, vis.qz, p.x, p.y, p.z);
+          if (d < vis.best || (d == vis.best && (unsigned)j < (unsigned)vis.bestj)) {
+            vis.best = d;
+            vis.bestj = j;
+          }
+        }
+      }
+      vis.skip_lo = 1;
+      vis.skip_hi = 0;
+      vis.box = make_wave_box(need, vis.qx, vis.qy, vis.qz, vis.best);
+      traverse(tgt, vis);
+      if (need) {
+        d2 = vis.best;
+        job->sqd[i] = d2;
+      }
+    }
+    if (active) out[src.perm[i]] = sqrt((double)d2);
+  }
+}
+
+// pcl::transformPointCloud with final_transformation_ (float 4x4)
+__global__ __launch_bounds__(256) void k_transform(const float4* __restrict__ pts, int n, const int* __restrict__ perm,
+                                                   const float* __restrict__ T16, float* __restrict__ out,
+                                                   size_t stride_floats) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 a = pts[i];
+  float* o = out + (size_t)perm[i] * stride_floats;
+  o[0] = (T16[0] * a.x + T16[1] * a.y) + (T16[2] * a.z + T16[3]);
+  o[1] = (T16[4] * a.x + T16[5] * a.y) + (T16[6] * a.z + T16[7]);
+  o[2] = (T16[8] * a.x + T16[9] * a.y) + (T16[10] * a.z + T16[11]);
+}
+
+// correspondences in original source order (original target indices)
+__global__ __launch_bounds__(256) void k_export_corr(const AlignJob* __restrict__ job, int* __restrict__ corr_out,
+                                                     float* __restrict__ sqd_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // sorted source index
+  if (i >= job->src.n) return;
+  const int o = job->src.perm[i];
+  const int j = job->corr[i];
+  if (corr_out) corr_out[o] = j >= 0 ? job->tgt.perm[j] : -1;
+  if (sqd_out) sqd_out[o] = job->sqd[i];
+}
+
+}  // namespace ddlo
+
+// ============================================================================
+// host launchers
+// ============================================================================
+namespace ddlo {
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+static inline int group_blocks(int n) {  // 4 waves (256 threads) per block, one 64-query group per wave
+  const int groups = cdiv(n, 64);
+  return std::max(1, std::min(cdiv(groups, 4), 4096));
+}
+
+void launch_pack_bbox(hipStream_t s, const unsigned char* raw, size_t stride, int n, float4* out, float* partial,
+                      int* nonfinite, int nblocks) {
+  k_pack_bbox<<<nblocks, 256, 0, s>>>(raw, stride, n, out, partial, nonfinite);
+}
+void launch_bbox_final(hipStream_t s, const float* partial, int nparts, float* quant) {
+  k_bbox_final<<<1, 64, 0, s>>>(partial, nparts, quant);
+}
+void launch_morton(hipStream_t s, const float4* pts, int n, const float* quant, unsigned long long* keys, int* vals) {
+  k_morton<<<cdiv(n, 256), 256, 0, s>>>(pts, n, quant, keys, vals);
+}
+void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, float4* sorted, int* inv_perm) {
+  k_gather<<<cdiv(n, 256), 256, 0, s>>>(raw, perm, n, sorted, inv_perm);
+}
+void launch_leaf_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float4* lo, float4* hi) {
+  k_leaf_boxes<<<cdiv(nleaves, 8), 256, 0, s>>>(pts, n, nleaves, lo, hi);
+}
+void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int nchild, int nparent, float4* plo,
+                        float4* phi) {
+  k_level_boxes<<<cdiv(nparent, 4), 256, 0, s>>>(clo, chi, nchild, nparent, plo, phi);
+}
+bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6) {
+  const int nb = group_blocks(c.n);
+  if (k == 10) k_covariances<10, true><<<nb, 256, 0, s>>>(c, k, method, cov6);
+  else if (k == 20) k_covariances<20, true><<<nb, 256, 0, s>>>(c, k, method, cov6);
+  else if (k <= 16) k_covariances<16, false><<<nb, 256, 0, s>>>(c, k, method, cov6);
+  else if (k <= 32) k_covariances<32, false><<<nb, 256, 0, s>>>(c, k, method, cov6);
+  else if (k <= 64) k_covariances<64, false><<<nb, 256, 0, s>>>(c, k, method, cov6);
+  else return false;
+  return true;
+}
+bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq, int k, int* out_idx, float* out_d) {
+  const int nb = group_blocks(nq);
+  if (k == 1) k_knn_query<1, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
+  else if (k == 10) k_knn_query<10, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
+  else if (k == 20) k_knn_query<20, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
+  else if (k <= 16) k_knn_query<16, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
+  else if (k <= 32) k_knn_query<32, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
+  else if (k <= 64) k_knn_query<64, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
+  else return false;
+  return true;
+}
+void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6) {
+  k_cov_import<<<cdiv(n, 256), 256, 0, s>>>(in, layout, n, inv_perm, cov6);
+}
+void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out) {
+  k_cov_export<<<cdiv(n, 256), 256, 0, s>>>(cov6, layout, n, perm, out);
+}
+void launch_align_init(hipStream_t s, const AlignJob* job) { k_align_init<<<1, 64, 0, s>>>(job); }
+void launch_linearize(hipStream_t s, const AlignJob* job, int nblocks) {
+  k_linearize<<<nblocks, 64 * kLinWaves, 0, s>>>(job);
+}
+void launch_lm_step(hipStream_t s, const AlignJob* job) { k_lm_step<<<1, kLmThreads, 0, s>>>(job); }
+void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out) {
+  k_residuals<<<group_blocks(nsrc), 256, 0, s>>>(job, out);
+}
+void launch_transform(hipStream_t s, const float4* pts, int n, const int* perm, const float* T16, float* out,
+                      size_t stride_floats) {
+  k_transform<<<cdiv(n, 256), 256, 0, s>>>(pts, n, perm, T16, out, stride_floats);
+}
+void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr, float* sqd) {
+  k_export_corr<<<cdiv(nsrc, 256), 256, 0, s>>>(job, corr, sqd);
+}
+
+}  // namespace ddlo

@@ -1,0 +1,31 @@
+// launch.hpp — host-callable launchers of the kernels in kernels.hip.  The
+// host runtime (capi.hip) only sees these plain functions.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gicp_types.hpp"
+
+namespace ddlo {
+
+void launch_pack_bbox(hipStream_t s, const unsigned char* raw, size_t stride, int n, float4* out, float* partial,
+                      int* nonfinite, int nblocks);
+void launch_bbox_final(hipStream_t s, const float* partial, int nparts, float* quant);
+void launch_morton(hipStream_t s, const float4* pts, int n, const float* quant, unsigned long long* keys, int* vals);
+void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, float4* sorted, int* inv_perm);
+void launch_leaf_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float4* lo, float4* hi);
+void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int nchild, int nparent, float4* plo,
+                        float4* phi);
+// returns false if k is unsupported (> 64)
+bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6);
+bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq, int k, int* out_idx, float* out_d);
+void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6);
+void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);
+void launch_align_init(hipStream_t s, const AlignJob* job);
+void launch_linearize(hipStream_t s, const AlignJob* job, int nblocks);
+void launch_lm_step(hipStream_t s, const AlignJob* job);
+void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out);
+void launch_transform(hipStream_t s, const float4* pts, int n, const int* perm, const float* T16, float* out,
+                      size_t stride_floats);
+void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr, float* sqd);
+
+}  // namespace ddlo

@@ -1,0 +1,269 @@
+"""Deterministic synthetic "kantplatz-shaped" plaza scenes for the GICP hot path.
+
+The reference ships no datasets or fixtures; its authors replay
+external rosbags (``DDLO/launch/play_kantplatz_data.launch:8-17``).  This module
+ray-casts a ring LiDAR inside an urban plaza so that every BASELINE.json config
+can be produced on any box without network access:
+
+* ground plane z = 0, building facades enclosing a 60 m x 40 m square (50 m
+  tall, so every ray of a +/-45 deg ring returns), facade pilasters and
+  recesses, lamp poles (vertical cylinders), benches and ~20 pedestrian boxes;
+* sensor 1.5 m above ground, 64 rows over +/-22.5 deg or 128 rows over
+  +/-45 deg, 1024/2048 columns, range noise N(0, 0.01 m), ranges 0.5-80 m,
+  no-return pixels dropped (GICP inputs must be finite, ``odom.cc:469-475``);
+* trajectory 1.0 m/s at 10 Hz with a gentle yaw rate (<= 10 deg/s).
+
+Seeds follow SURVEY.md §8(d): ``1000 + config id (+ frame index)``.  All
+randomness goes through ``numpy.random.default_rng`` so the clouds are
+bit-identical across runs on one platform.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+PLAZA_X = 30.0   # half extent of the square (m)
+PLAZA_Y = 20.0
+FACADE_H = 50.0
+SENSOR_Z = 1.5
+
+
+@dataclass
+class Scene:
+    boxes_lo: np.ndarray      # (B,3) axis-aligned solid boxes (pilasters, benches, kiosks)
+    boxes_hi: np.ndarray
+    poles: np.ndarray         # (P,4) cx, cy, radius, height
+    peds_lo: np.ndarray       # (Q,3) pedestrian boxes at t = 0
+    peds_hi: np.ndarray
+    peds_vel: np.ndarray      # (Q,2) xy velocity (m/s); zero for static ones
+
+
+def make_scene(seed: int = 1000, n_peds: int = 20, moving: bool = False) -> Scene:
+    rng = np.random.default_rng(seed)
+    lo, hi = [], []
+    # facade pilasters: shallow boxes attached to the four walls, irregular spacing
+    for wall in range(4):
+        n = 14 if wall < 2 else 10
+        span = PLAZA_Y if wall < 2 else PLAZA_X
+        pos = np.sort(rng.uniform(-span + 1.0, span - 1.0, n))
+        for p in pos:
+            w = rng.uniform(0.4, 1.2)
+            d = rng.uniform(0.2, 0.8)
+            h = rng.uniform(6.0, FACADE_H)
+            if wall == 0:   # x = +PLAZA_X wall
+                lo.append([PLAZA_X - d, p - w, 0.0]); hi.append([PLAZA_X + 0.1, p + w, h])
+            elif wall == 1:  # x = -PLAZA_X
+                lo.append([-PLAZA_X - 0.1, p - w, 0.0]); hi.append([-PLAZA_X + d, p + w, h])
+            elif wall == 2:  # y = +PLAZA_Y
+                lo.append([p - w, PLAZA_Y - d, 0.0]); hi.append([p + w, PLAZA_Y + 0.1, h])
+            else:            # y = -PLAZA_Y
+                lo.append([p - w, -PLAZA_Y - 0.1, 0.0]); hi.append([p + w, -PLAZA_Y + d, h])
+    # balconies / cornices: horizontal slabs that break facade symmetry in z
+    for _ in range(16):
+        wall = rng.integers(0, 4)
+        z = rng.uniform(3.0, 20.0)
+        span = PLAZA_Y if wall < 2 else PLAZA_X
+        c = rng.uniform(-span + 3, span - 3)
+        w = rng.uniform(1.0, 4.0)
+        d = rng.uniform(0.6, 1.5)
+        if wall == 0:
+            lo.append([PLAZA_X - d, c - w, z]); hi.append([PLAZA_X, c + w, z + 0.3])
+        elif wall == 1:
+            lo.append([-PLAZA_X, c - w, z]); hi.append([-PLAZA_X + d, c + w, z + 0.3])
+        elif wall == 2:
+            lo.append([c - w, PLAZA_Y - d, z]); hi.append([c + w, PLAZA_Y, z + 0.3])
+        else:
+            lo.append([c - w, -PLAZA_Y, z]); hi.append([c + w, -PLAZA_Y + d, z + 0.3])
+    # benches and kiosks inside the square
+    for _ in range(12):
+        cx, cy = rng.uniform(-PLAZA_X + 4, PLAZA_X - 4), rng.uniform(-PLAZA_Y + 4, PLAZA_Y - 4)
+        if abs(cy) < 2.5 and -15 < cx < 15:   # keep the driving corridor free
+            cy += 5.0 * np.sign(cy if cy != 0 else 1.0)
+        ang = rng.uniform(0, math.pi)
+        L = rng.uniform(1.5, 4.0)
+        W = rng.uniform(0.5, 2.5)
+        H = rng.uniform(0.45, 3.0)
+        ex = abs(L * math.cos(ang)) + abs(W * math.sin(ang))
+        ey = abs(L * math.sin(ang)) + abs(W * math.cos(ang))
+        lo.append([cx - ex / 2, cy - ey / 2, 0.0]); hi.append([cx + ex / 2, cy + ey / 2, H])
+    poles = []
+    for _ in range(18):
+        cx, cy = rng.uniform(-PLAZA_X + 2, PLAZA_X - 2), rng.uniform(-PLAZA_Y + 2, PLAZA_Y - 2)
+        if abs(cy) < 2.0 and -15 < cx < 15:
+            cy += 4.0 * np.sign(cy if cy != 0 else 1.0)
+        poles.append([cx, cy, rng.uniform(0.06, 0.25), rng.uniform(3.0, 8.0)])
+    plo, phi, pvel = [], [], []
+    for _ in range(n_peds):
+        cx, cy = rng.uniform(-PLAZA_X + 3, PLAZA_X - 3), rng.uniform(-PLAZA_Y + 3, PLAZA_Y - 3)
+        if abs(cy) < 1.5 and -15 < cx < 15:
+            cy += 3.0 * np.sign(cy if cy != 0 else 1.0)
+        w = rng.uniform(0.3, 0.6)
+        plo.append([cx - w / 2, cy - w / 2, 0.0]); phi.append([cx + w / 2, cy + w / 2, rng.uniform(1.5, 1.95)])
+        if moving:
+            a = rng.uniform(0, 2 * math.pi)
+            s = rng.uniform(0.5, 1.5)
+            pvel.append([s * math.cos(a), s * math.sin(a)])
+        else:
+            pvel.append([0.0, 0.0])
+    return Scene(np.asarray(lo), np.asarray(hi), np.asarray(poles),
+                 np.asarray(plo), np.asarray(phi), np.asarray(pvel))
+
+
+def _ray_box(o, inv, lo, hi, tbest):
+    """Slab test of rays (o + t d), inv = 1/d, against one AABB; updates tbest in place."""
+    tmin = np.zeros_like(tbest)
+    tmax = tbest.copy()
+    for a in range(3):
+        t1 = (lo[a] - o[a]) * inv[a]
+        t2 = (hi[a] - o[a]) * inv[a]
+        np.maximum(tmin, np.minimum(t1, t2), out=tmin)
+        np.minimum(tmax, np.maximum(t1, t2), out=tmax)
+    better = (tmax >= tmin) & (tmin > 1e-6) & (tmin < tbest)
+    tbest[better] = tmin[better]
+
+
+def _ray_cylinder(o, d, cx, cy, r, h, tbest):
+    ox, oy = o[0] - cx, o[1] - cy
+    a = d[:, 0] ** 2 + d[:, 1] ** 2
+    b = 2 * (ox * d[:, 0] + oy * d[:, 1])
+    c = ox * ox + oy * oy - r * r
+    disc = b * b - 4 * a * c
+    ok = (disc >= 0) & (a > 1e-12)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        t = (-b - np.sqrt(np.where(ok, disc, 0.0))) / (2 * a)
+    z = o[2] + t * d[:, 2]
+    good = ok & (t > 1e-6) & (z >= 0) & (z <= h) & (t < tbest)
+    tbest[good] = t[good]
+
+
+def lidar_dirs(rows: int, cols: int) -> np.ndarray:
+    """Unit ray directions (rows*cols, 3) of a ring LiDAR in the sensor frame (row-major)."""
+    vfov = 22.5 if rows <= 64 else 45.0
+    elev = np.deg2rad(np.linspace(-vfov, vfov, rows))
+    azim = np.deg2rad(np.arange(cols) * (360.0 / cols))
+    E, A = np.meshgrid(elev, azim, indexing="ij")
+    return np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], axis=-1).reshape(-1, 3)
+
+
+def raycast(scene: Scene, pose: np.ndarray, rows: int, cols: int, seed: int, t: float = 0.0) -> np.ndarray:
+    """Ray-cast one scan from world pose ``pose`` (4x4, world <- sensor).
+
+    Returns float32 points (N,3) in the SENSOR frame, organized row-major with
+    no-return pixels dropped.
+    """
+    rng = np.random.default_rng(seed)
+    dirs_s = lidar_dirs(rows, cols)
+    R, o = pose[:3, :3], pose[:3, 3]
+    d = dirs_s @ R.T
+    tbest = np.full(d.shape[0], np.inf)
+    # ground
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tg = -o[2] / d[:, 2]
+    tbest = np.where((d[:, 2] < 0) & (tg > 0), tg, tbest)
+    # facades (inside of the square)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for axis, ext in ((0, PLAZA_X), (1, PLAZA_Y)):
+            tp = (ext - o[axis]) / d[:, axis]
+            tn = (-ext - o[axis]) / d[:, axis]
+            tw = np.where(d[:, axis] > 0, tp, tn)
+            zw = o[2] + tw * d[:, 2]
+            ok = (tw > 0) & (zw <= FACADE_H) & (tw < tbest)
+            tbest = np.where(ok, tw, tbest)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = [1.0 / np.where(d[:, a] == 0.0, 1e-30, d[:, a]) for a in range(3)]
+    for lo, hi in zip(scene.boxes_lo, scene.boxes_hi):
+        _ray_box(o, inv, lo, hi, tbest)
+    for cx, cy, r, h in scene.poles:
+        _ray_cylinder(o, d, cx, cy, r, h, tbest)
+    for lo, hi, v in zip(scene.peds_lo, scene.peds_hi, scene.peds_vel):
+        shift = np.array([v[0] * t, v[1] * t, 0.0])
+        _ray_box(o, inv, lo + shift, hi + shift, tbest)
+    rng_noise = rng.normal(0.0, 0.01, size=tbest.shape)
+    r = tbest + rng_noise
+    valid = np.isfinite(tbest) & (r >= 0.5) & (r <= 80.0)
+    pts = dirs_s[valid] * r[valid, None]
+    return pts.astype(np.float32)
+
+
+def rpy_to_R(roll, pitch, yaw):
+    cr, sr, cp, sp, cy, sy = math.cos(roll), math.sin(roll), math.cos(pitch), math.sin(pitch), math.cos(yaw), math.sin(yaw)
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1.0]])
+    Ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+    Rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    return Rz @ Ry @ Rx
+
+
+def make_pose(t, rpy=(0.0, 0.0, 0.0)):
+    T = np.eye(4)
+    T[:3, :3] = rpy_to_R(*rpy)
+    T[:3, 3] = t
+    return T
+
+
+def trajectory(n_frames: int, seed: int = 1000) -> list:
+    """Ground-truth sensor poses: 1.0 m/s at 10 Hz, slowly varying yaw rate."""
+    rng = np.random.default_rng(seed)
+    x, y, yaw = -12.0, -1.0, 0.0
+    poses = []
+    yaw_rate = 0.0
+    for _ in range(n_frames):
+        poses.append(make_pose([x, y, SENSOR_Z], (0.0, 0.0, yaw)))
+        yaw_rate = float(np.clip(yaw_rate + rng.normal(0, 0.5), -10.0, 10.0))  # deg/s
+        yaw += math.radians(yaw_rate) * 0.1
+        x += 0.1 * math.cos(yaw)
+        y += 0.1 * math.sin(yaw)
+        if abs(y) > 8.0:       # keep inside the square
+            yaw -= 0.05 * np.sign(y)
+    return poses
+
+
+# The S2S perturbation of SURVEY.md §8(d): t = (0.30, -0.20, 0.05) m, yaw 2 deg, roll/pitch 0.5 deg
+PERTURB = make_pose([0.30, -0.20, 0.05], (math.radians(0.5), math.radians(0.5), math.radians(2.0)))
+
+
+def transform(pts: np.ndarray, T: np.ndarray) -> np.ndarray:
+    return (pts.astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+
+
+def s2s_pair(rows: int, cols: int, cfg_id: int):
+    """Two scans: target from pose P, source from pose P * PERTURB (guess = I).
+
+    Returns (source, target, T_true) with T_true mapping source-frame points
+    into the target frame (what align() should recover).
+    """
+    scene = make_scene(1000 + cfg_id)
+    P = make_pose([-6.0, 2.0, SENSOR_Z], (0.0, 0.0, math.radians(15.0)))
+    tgt = raycast(scene, P, rows, cols, seed=1000 + cfg_id)
+    Q = P @ PERTURB
+    src = raycast(scene, Q, rows, cols, seed=1000 + cfg_id + 1)
+    return src, tgt, PERTURB.copy()
+
+
+def s2m_problem(rows: int, cols: int, n_keyframes: int, submap_size: int, cfg_id: int):
+    """Scan vs fused keyframe submap (SURVEY.md §8(d) cfg 3/4).
+
+    Keyframes are scans taken every 10 frames (1 m, ``ddlo.yaml`` threshD) and
+    moved into the world frame; the submap is their concatenation truncated to
+    ``submap_size`` by a seeded subset.  Returns a dict with the source scan
+    (sensor frame), the per-keyframe world clouds, the subset indices, the
+    ground-truth pose and the perturbed initial guess.
+    """
+    seed = 1000 + cfg_id
+    scene = make_scene(seed)
+    poses = trajectory(10 * n_keyframes + 6, seed)
+    kfs = []
+    for k in range(n_keyframes):
+        P = poses[10 * k]
+        kfs.append(transform(raycast(scene, P, rows, cols, seed=seed + 10 * k), P))
+    cur = poses[10 * n_keyframes + 5]
+    src = raycast(scene, cur, rows, cols, seed=seed + 10 * n_keyframes + 5)
+    total = sum(len(k) for k in kfs)
+    rng = np.random.default_rng(seed + 7)
+    if submap_size < total:
+        subset = np.sort(rng.choice(total, size=submap_size, replace=False))
+    else:
+        subset = np.arange(total)
+    guess = cur @ PERTURB
+    return {"source": src, "keyframes": kfs, "subset": subset, "T_true": cur, "guess": guess}

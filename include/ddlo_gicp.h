@@ -1,0 +1,198 @@
+/*
+ * ddlo_gicp.h — C-ABI of the MI355X-native GICP scan-matching core.
+ *
+ * This is the drop-in boundary for the reference's NanoGICP registration core
+ * (nano_gicp::NanoGICP<PointXYZI,PointXYZI>, reference
+ * dynamic_direct_lidar_odometry/include/nano_gicp/nano_gicp.hpp:58-148 and
+ * lsq_registration.hpp:60-128).  Plain pointers and sizes only; no exceptions
+ * cross it; every entry point returns a gicp_status and sets a thread-local
+ * message readable with gicp_last_error().
+ *
+ * One gicp_ctx == one NanoGICP instance (OdomNode owns two: gicp_s2s_ and
+ * gicp_s2m_, reference include/odometry/odom.h:159-160).  A ctx owns one HIP
+ * stream on its device and needs external synchronisation (like the reference,
+ * which is driven from one ROS callback thread, odom_node.cc:43).  Distinct
+ * ctxs may be used concurrently.
+ *
+ * Host buffers passed in are copied (H2D) before the call returns; the caller
+ * may free them afterwards.  Clouds live on the device as ref-counted objects,
+ * so gicp_swap_source_target / gicp_share_source are O(1) and never re-upload.
+ */
+#ifndef DDLO_GICP_H
+#define DDLO_GICP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DDLO_GICP_ABI_VERSION 1
+
+typedef enum gicp_status {
+  GICP_OK = 0,
+  GICP_EINVAL = 1,      /* bad argument (null pointer, size mismatch, bad enum) */
+  GICP_ENOTARGET = 2,   /* align/linearize without a target cloud            */
+  GICP_ENOSOURCE = 3,   /* align/linearize without a source cloud            */
+  GICP_ETOOFEW = 4,     /* cloud has fewer points than k_correspondences      */
+  GICP_EHIP = 5,        /* HIP runtime error (message in gicp_last_error)     */
+  GICP_ENOMEM = 6,      /* device allocation failed                          */
+  GICP_ESTATE = 7,      /* call not valid in the current state (e.g. residuals
+                           requested before any align)                       */
+  GICP_ENONFINITE = 8   /* cloud contains NaN/Inf coordinates                 */
+} gicp_status;
+
+/* Same order as nano_gicp::RegularizationMethod (gicp/gicp_settings.hpp:47-54). */
+typedef enum gicp_regularization {
+  GICP_REG_NONE = 0,
+  GICP_REG_MIN_EIG = 1,
+  GICP_REG_NORMALIZED_MIN_EIG = 2,
+  GICP_REG_PLANE = 3,
+  GICP_REG_FROBENIUS = 4
+} gicp_regularization;
+
+/* Same order as nano_gicp::LSQ_OPTIMIZER_TYPE (lsq_registration.hpp:54-58). */
+typedef enum gicp_optimizer { GICP_OPT_GAUSS_NEWTON = 0, GICP_OPT_LEVENBERG_MARQUARDT = 1 } gicp_optimizer;
+
+typedef enum gicp_side { GICP_SIDE_SOURCE = 0, GICP_SIDE_TARGET = 1 } gicp_side;
+
+/* Covariance layouts accepted/produced at the boundary.
+ * MAT4D: 16 doubles per point, row-major Eigen::Matrix4d as the reference
+ *        stores them (nano_gicp.hpp:136-137); only the 3x3 block is read.
+ * SYM6:  6 doubles per point (xx, xy, xz, yy, yz, zz). */
+typedef enum gicp_cov_layout { GICP_COV_MAT4D = 0, GICP_COV_SYM6 = 1 } gicp_cov_layout;
+
+/* All GICP knobs.  gicp_default_params() fills the reference defaults:
+ * k=20 (nano_gicp_impl.hpp:58), max_corr=FLT_MAX (:60), PLANE (:62),
+ * max_iterations=64, rotation_eps=2e-3, transformation_eps=5e-4, LM,
+ * lm_max_iterations=10, lm_init_lambda_factor=1e-9
+ * (lsq_registration_impl.hpp:53-60). */
+typedef struct gicp_params {
+  int32_t k_correspondences;            /* setCorrespondenceRandomness        */
+  int32_t max_iterations;               /* setMaximumIterations               */
+  double max_correspondence_distance;   /* setMaxCorrespondenceDistance       */
+  double transformation_epsilon;        /* setTransformationEpsilon           */
+  double rotation_epsilon;              /* setRotationEpsilon                 */
+  double lm_init_lambda_factor;         /* setInitialLambdaFactor             */
+  int32_t regularization;               /* gicp_regularization                */
+  int32_t optimizer;                    /* gicp_optimizer (reference: LM only,
+                                           no setter; GN exposed for cfg 2)   */
+  int32_t lm_max_iterations;            /* hard-coded 10 in the reference     */
+  int32_t fixed_iterations;             /* 0 = reference convergence logic;
+                                           >0 = run exactly this many outer
+                                           iterations (benchmarks, cfg 2)     */
+} gicp_params;
+
+/* Outcome of one align (reference: converged_, nr_iterations_,
+ * final_hessian_, the "lm not converged!!" branch at
+ * lsq_registration_impl.hpp:115-119). */
+typedef struct gicp_result {
+  int32_t converged;          /* hasConverged()                                  */
+  int32_t nr_iterations;      /* last outer loop index (reference semantics)     */
+  int32_t iterations_run;     /* number of linearize() calls executed            */
+  int32_t lm_failed;          /* 1 if step_lm exhausted lm_max_iterations        */
+  int32_t lm_trials;          /* total compute_error evaluations                 */
+  int32_t num_correspondences;/* matched source points at the last linearize     */
+  double final_cost;          /* sum e^T M e at the last linearize               */
+  double final_hessian[36];   /* getFinalHessian(), row-major                    */
+  double lm_lambda;           /* lambda after the last step                      */
+  double device_ms;           /* device time of the align (HIP events)           */
+  double linearize_ms;        /* summed device time of the linearize kernels
+                                 (only when profiling is enabled, else 0)       */
+} gicp_result;
+
+/* ---- library / context --------------------------------------------------- */
+int32_t gicp_abi_version(void);
+const char* gicp_last_error(void);
+gicp_status gicp_default_params(gicp_params* out);
+
+/* replaces constructing nano_gicp::NanoGICP (nano_gicp_impl.hpp:49-65) */
+gicp_status gicp_ctx_create(int device, struct gicp_ctx** out);
+gicp_status gicp_ctx_destroy(struct gicp_ctx* ctx);
+
+/* replaces the setters called at odom.cc:92-112 */
+gicp_status gicp_set_params(struct gicp_ctx* ctx, const gicp_params* p);
+gicp_status gicp_get_params(const struct gicp_ctx* ctx, gicp_params* out);
+
+/* ---- clouds ---------------------------------------------------------------
+ * xyz points at float x,y,z of point 0; consecutive points are stride_bytes
+ * apart (32 for pcl::PointXYZI, 12 for packed xyz).
+ *
+ * gicp_set_source(build_index=1) replaces NanoGICP::setInputSource
+ *   (nano_gicp_impl.hpp:132-143: sets input_, builds the source kd-tree,
+ *   clears source covariances);
+ * gicp_set_source(build_index=0) replaces registerInputSource (:122-130).
+ *   The device path always sorts the cloud spatially, so both forms produce
+ *   the same device object; build_index=0 only skips the search hierarchy.
+ * gicp_set_target replaces setInputTarget (:145-155). */
+gicp_status gicp_set_source(struct gicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes, int build_index);
+gicp_status gicp_set_target(struct gicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
+gicp_status gicp_clear_source(struct gicp_ctx* ctx); /* clearSource (:108-113) */
+gicp_status gicp_clear_target(struct gicp_ctx* ctx); /* clearTarget (:115-120) */
+gicp_status gicp_get_size(const struct gicp_ctx* ctx, int side, size_t* n);
+
+/* calculateSourceCovariances / calculateTargetCovariances (:171-181 ->
+ * calculate_covariances :373-441): exact kNN-k (self included), biased
+ * covariance, regularisation per params. */
+gicp_status gicp_compute_covariances(struct gicp_ctx* ctx, int side);
+/* setSourceCovariances / setTargetCovariances (:157-169) — copied. */
+gicp_status gicp_set_covariances(struct gicp_ctx* ctx, int side, const double* cov, size_t n, int layout);
+/* getSourceCovariances / getTargetCovariances (nano_gicp.hpp:106-114). */
+gicp_status gicp_get_covariances(const struct gicp_ctx* ctx, int side, double* cov, size_t n, int layout);
+/* 1 if the side's covariances are present (size == cloud size). */
+gicp_status gicp_has_covariances(const struct gicp_ctx* ctx, int side, int* has);
+
+/* swapSourceAndTarget (:97-106): swaps clouds, indices and covariances,
+ * clears correspondences.  O(1). */
+gicp_status gicp_swap_source_target(struct gicp_ctx* ctx);
+/* Replaces the public-member aliasing the caller does at odom.cc:530
+ * (gicp_s2m_.source_kdtree_ = gicp_s2s_.source_kdtree_) and :765
+ * (gicp_s2m_.source_covs_ = gicp_s2s_.source_covs_): dst's source becomes
+ * src's source cloud, device index and covariances (copy-on-write). */
+gicp_status gicp_share_source(struct gicp_ctx* dst, const struct gicp_ctx* src);
+
+/* ---- registration -------------------------------------------------------- */
+/* pcl::Registration::align(output, guess) -> NanoGICP::computeTransformation
+ * (:183-196) -> LsqRegistration::computeTransformation
+ * (lsq_registration_impl.hpp:95-126).  guess/out: row-major 4x4 float
+ * (Eigen::Matrix4f).  guess may be NULL (identity, as align(output)).
+ * Missing covariances are computed first, as the reference does. */
+gicp_status gicp_align(struct gicp_ctx* ctx, const float* guess16, float* out16, gicp_result* res);
+
+/* getResiduals(std::vector<double>&, trans) (:225-232): sqrt of the squared
+ * 1-NN distance of every source point (original order) from the LAST
+ * update_correspondences; the trans argument is ignored there too. */
+gicp_status gicp_get_residuals(struct gicp_ctx* ctx, double* out, size_t n);
+/* correspondences_ / sq_distances_ of the last linearization, original
+ * indices (-1 = no correspondence within max_correspondence_distance).
+ * Unmatched points report sq_dist = +inf unless gicp_get_residuals ran. */
+gicp_status gicp_get_correspondences(struct gicp_ctx* ctx, int32_t* corr, float* sq_dist, size_t n);
+/* pcl::transformPointCloud(*input_, output, final_transformation_)
+ * (lsq_registration_impl.hpp:125); writes xyz with the given stride. */
+gicp_status gicp_transform_source(struct gicp_ctx* ctx, float* out_xyz, size_t n, size_t stride_bytes);
+
+/* ---- kernel-level entry points (parity tests, benchmarks) ----------------- */
+/* linearize(trans, &H, &b) (:277-342) at a given pose (row-major 4x4 double):
+ * runs update_correspondences + the H/b/cost reduction once.  H row-major. */
+gicp_status gicp_linearize(struct gicp_ctx* ctx, const double* pose16, double* H36, double* b6, double* cost,
+                           int32_t* num_correspondences);
+/* Exact k-NN of query points against the TARGET index (nanoflann
+ * nearestKSearch, nanoflann.hpp:145-156).  Indices are original target
+ * indices, sorted ascending by (squared distance, index). */
+gicp_status gicp_knn_target(struct gicp_ctx* ctx, const float* q, size_t nq, size_t stride_bytes, int k,
+                            int32_t* idx, float* sq_dist);
+/* The 74 reduced normal-equation moments of the last linearize (80 doubles,
+ * layout in DESIGN.md "Normal-equation moments"); test/debug entry. */
+gicp_status gicp_get_moments(const struct gicp_ctx* ctx, double* out80);
+/* Device time accounting of the linearize kernel inside align (HIP events
+ * captured in the align graph).  Off by default. */
+gicp_status gicp_set_profiling(struct gicp_ctx* ctx, int enable);
+/* The ctx's HIP stream (hipStream_t) for callers that interleave their own work. */
+gicp_status gicp_get_stream(const struct gicp_ctx* ctx, void** stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DDLO_GICP_H */

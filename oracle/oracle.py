@@ -1,0 +1,237 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, as the checker / timed CPU baseline.  The product package never
+imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+
+class GicpParams(C.Structure):
+    _fields_ = [
+        ("k_correspondences", C.c_int32),
+        ("max_iterations", C.c_int32),
+        ("max_correspondence_distance", C.c_double),
+        ("transformation_epsilon", C.c_double),
+        ("rotation_epsilon", C.c_double),
+        ("lm_init_lambda_factor", C.c_double),
+        ("regularization", C.c_int32),
+        ("optimizer", C.c_int32),
+        ("lm_max_iterations", C.c_int32),
+        ("fixed_iterations", C.c_int32),
+    ]
+
+
+class GicpResult(C.Structure):
+    _fields_ = [
+        ("converged", C.c_int32),
+        ("nr_iterations", C.c_int32),
+        ("iterations_run", C.c_int32),
+        ("lm_failed", C.c_int32),
+        ("lm_trials", C.c_int32),
+        ("num_correspondences", C.c_int32),
+        ("final_cost", C.c_double),
+        ("final_hessian", C.c_double * 36),
+        ("lm_lambda", C.c_double),
+        ("device_ms", C.c_double),
+        ("linearize_ms", C.c_double),
+    ]
+
+
+REG = {"NONE": 0, "MIN_EIG": 1, "NORMALIZED_MIN_EIG": 2, "PLANE": 3, "FROBENIUS": 4}
+GN, LM = 0, 1
+
+
+def default_params(**kw) -> GicpParams:
+    """Reference defaults (nano_gicp_impl.hpp:58-62, lsq_registration_impl.hpp:53-60)."""
+    p = GicpParams(20, 64, float(np.finfo(np.float32).max), 5e-4, 2e-3, 1e-9, REG["PLANE"], LM, 10, 0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"oracle library missing: {path} (run `make -C oracle`)")
+        L = C.CDLL(path)
+        L.oref_tree_build.restype = C.c_void_p
+        L.oref_tree_build.argtypes = [C.c_void_p, C.c_int]
+        L.oref_tree_free.argtypes = [C.c_void_p]
+        L.oref_tree_knn.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        L.oref_covariances.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]
+        L.oref_gicp_create.restype = C.c_void_p
+        L.oref_gicp_create.argtypes = [C.POINTER(GicpParams), C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        L.oref_gicp_free.argtypes = [C.c_void_p]
+        L.oref_gicp_set_threads.argtypes = [C.c_void_p, C.c_int]
+        L.oref_gicp_set_params.argtypes = [C.c_void_p, C.POINTER(GicpParams)]
+        L.oref_gicp_set_covariances.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        L.oref_gicp_compute_covariances.argtypes = [C.c_void_p, C.c_int]
+        L.oref_gicp_get_covariances.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.oref_gicp_align.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(GicpResult)]
+        L.oref_gicp_linearize.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oref_gicp_compute_error.restype = C.c_double
+        L.oref_gicp_compute_error.argtypes = [C.c_void_p, C.c_void_p]
+        L.oref_gicp_last_correspondences.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oref_gicp_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.oref_so3_exp.argtypes = [C.c_void_p, C.c_void_p]
+        L.oref_ldlt_solve6.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oref_regularize.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+def ref_lib():
+    """The reference's own nanoflann (oracle/_ref); None when it was not built."""
+    global _REF
+    if _REF is None:
+        path = os.path.join(HERE, "_ref", "libref_nanoflann.so")
+        if not os.path.exists(path):
+            return None
+        L = C.CDLL(path)
+        L.ref_tree_build.restype = C.c_void_p
+        L.ref_tree_build.argtypes = [C.c_void_p, C.c_int]
+        L.ref_tree_free.argtypes = [C.c_void_p]
+        L.ref_tree_knn.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _REF = L
+    return _REF
+
+
+def _xyz(a):
+    return np.ascontiguousarray(a, dtype=np.float32).reshape(-1, 3)
+
+
+def knn(points, queries, k, threads=0):
+    """Exact k-NN with the oracle kd-tree (nanoflann restatement)."""
+    L = lib()
+    pts, q = _xyz(points), _xyz(queries)
+    h = L.oref_tree_build(_fp(pts), len(pts))
+    idx = np.zeros((len(q), k), np.int32)
+    d = np.zeros((len(q), k), np.float32)
+    L.oref_tree_knn(h, _fp(q), len(q), k, _fp(idx), _fp(d), threads)
+    L.oref_tree_free(h)
+    return idx, d
+
+
+def ref_knn(points, queries, k):
+    """Exact k-NN with the REFERENCE nanoflann (oracle/_ref), or None."""
+    L = ref_lib()
+    if L is None:
+        return None
+    pts, q = _xyz(points), _xyz(queries)
+    h = L.ref_tree_build(_fp(pts), len(pts))
+    idx = np.zeros((len(q), k), np.int32)
+    d = np.zeros((len(q), k), np.float32)
+    L.ref_tree_knn(h, _fp(q), len(q), k, _fp(idx), _fp(d))
+    L.ref_tree_free(h)
+    return idx, d
+
+
+def covariances(points, k, reg="PLANE", threads=0):
+    L = lib()
+    pts = _xyz(points)
+    out = np.zeros((len(pts), 6), np.float64)
+    rc = L.oref_covariances(_fp(pts), len(pts), k, REG[reg] if isinstance(reg, str) else reg, _fp(out), threads)
+    if rc:
+        raise ValueError(f"oref_covariances failed ({rc})")
+    return out
+
+
+class Gicp:
+    """The oracle NanoGICP problem (source/target fixed for its lifetime)."""
+
+    def __init__(self, source, target, params: GicpParams | None = None, threads=0):
+        self.L = lib()
+        self.src = _xyz(source)
+        self.tgt = _xyz(target)
+        self.params = params or default_params()
+        self.h = self.L.oref_gicp_create(C.byref(self.params), _fp(self.src), len(self.src), _fp(self.tgt), len(self.tgt), threads)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.oref_gicp_free(self.h)
+            self.h = None
+
+    def set_threads(self, n):
+        self.L.oref_gicp_set_threads(self.h, n)
+
+    def set_params(self, p: GicpParams):
+        self.params = p
+        self.L.oref_gicp_set_params(self.h, C.byref(p))
+
+    def set_covariances(self, side, cov6):
+        cov6 = np.ascontiguousarray(cov6, np.float64)
+        self.L.oref_gicp_set_covariances(self.h, side, _fp(cov6), len(cov6), 1)
+
+    def compute_covariances(self, side):
+        self.L.oref_gicp_compute_covariances(self.h, side)
+
+    def get_covariances(self, side):
+        n = len(self.src) if side == 0 else len(self.tgt)
+        out = np.zeros((n, 6), np.float64)
+        self.L.oref_gicp_get_covariances(self.h, side, _fp(out))
+        return out
+
+    def align(self, guess=None):
+        out = np.zeros((4, 4), np.float32)
+        res = GicpResult()
+        g = None if guess is None else np.ascontiguousarray(guess, np.float32)
+        self.L.oref_gicp_align(self.h, None if g is None else _fp(g), _fp(out), C.byref(res))
+        return out, res
+
+    def linearize(self, pose):
+        pose = np.ascontiguousarray(pose, np.float64)
+        H = np.zeros((6, 6)); b = np.zeros(6); cost = np.zeros(1)
+        corr = np.zeros(len(self.src), np.int32); sqd = np.zeros(len(self.src), np.float32)
+        rc = self.L.oref_gicp_linearize(self.h, _fp(pose), _fp(H), _fp(b), _fp(cost), _fp(corr), _fp(sqd))
+        if rc:
+            raise RuntimeError(f"oref_gicp_linearize failed ({rc})")
+        return H, b, float(cost[0]), corr, sqd
+
+    def compute_error(self, pose):
+        pose = np.ascontiguousarray(pose, np.float64)
+        return self.L.oref_gicp_compute_error(self.h, _fp(pose))
+
+    def last_correspondences(self):
+        corr = np.zeros(len(self.src), np.int32); sqd = np.zeros(len(self.src), np.float32)
+        self.L.oref_gicp_last_correspondences(self.h, _fp(corr), _fp(sqd))
+        return corr, sqd
+
+    def trace(self):
+        n = self.L.oref_gicp_trace(self.h, None, 0)
+        out = np.zeros((max(n, 1), 13))
+        self.L.oref_gicp_trace(self.h, _fp(out), n)
+        return out[:n]
+
+
+def so3_exp(w):
+    w = np.ascontiguousarray(w, np.float64); R = np.zeros(9)
+    lib().oref_so3_exp(_fp(w), _fp(R))
+    return R.reshape(3, 3)
+
+
+def ldlt_solve6(A, b):
+    A = np.ascontiguousarray(A, np.float64); b = np.ascontiguousarray(b, np.float64); x = np.zeros(6)
+    lib().oref_ldlt_solve6(_fp(A), _fp(b), _fp(x))
+    return x
+
+
+def regularize(C9, reg):
+    C9 = np.ascontiguousarray(C9, np.float64); out = np.zeros(9)
+    lib().oref_regularize(_fp(C9), REG[reg] if isinstance(reg, str) else reg, _fp(out))
+    return out.reshape(3, 3)
