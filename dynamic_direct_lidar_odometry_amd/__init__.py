@@ -117,6 +117,7 @@ def load():
         "gicp_knn_target": (I, [P, P, S, S, I, P, P]),
         "gicp_get_moments": (I, [P, P]),
         "gicp_set_profiling": (I, [P, I]),
+        "gicp_debug_stats": (I, [P, I, P, S, C.POINTER(S)]),
         "gicp_get_stream": (I, [P, C.POINTER(P)]),
     }
     for name, (res, args) in sig.items():
@@ -280,6 +281,17 @@ class Context:
         d = np.zeros((len(q), k), np.float32)
         self._check(self.L.gicp_knn_target(self.h, _ptr(q), len(q), stride, k, _ptr(idx), _ptr(d)))
         return idx, d
+
+    def debug_stats(self, enable=True, read=False):
+        """Per 64-query group search counters of the last linearize (development)."""
+        if not read:
+            self._check(self.L.gicp_debug_stats(self.h, int(enable), None, 0, None))
+            return None
+        n = (self.size(SOURCE) + 63) // 64
+        out = np.zeros((n, 8), np.uint32)
+        nw = C.c_size_t()
+        self._check(self.L.gicp_debug_stats(self.h, int(enable), _ptr(out), out.size, C.byref(nw)))
+        return out
 
     def set_profiling(self, on=True):
         self._check(self.L.gicp_set_profiling(self.h, int(on)))

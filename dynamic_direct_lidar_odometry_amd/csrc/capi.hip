@@ -129,7 +129,8 @@ struct gicp_ctx {
   // build scratch
   DevBuf raw_bytes, raw_pts, partial, nonfinite, keys_tmp, vals_tmp, sort_tmp;
   // align buffers
-  DevBuf corr, sqd, slab, job_dev, state_dev, tmp_out;
+  DevBuf corr, sqd, slab, job_dev, state_dev, tmp_out, stats;
+  bool stats_on = false;
   AlignJob* job_host = nullptr;   // pinned
   AlignState* state_host = nullptr;  // pinned
   int* flag_host = nullptr;       // pinned
@@ -234,6 +235,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.sqd = c->sqd.as<float>();
   j.slab = c->slab.as<double>();
   j.state = c->state_dev.as<AlignState>();
+  j.stats = c->stats_on ? c->stats.as<unsigned int>() : nullptr;
   for (int r = 0; r < 3; ++r) {
     for (int cc = 0; cc < 3; ++cc) j.guess_R[3 * r + cc] = guess16 ? (double)guess16[4 * r + cc] : (r == cc ? 1.0 : 0.0);
     j.guess_t[r] = guess16 ? (double)guess16[4 * r + 3] : 0.0;
@@ -276,6 +278,7 @@ gicp_status prepare_align(gicp_ctx* c) {
   HIP_TRY(c->corr.ensure(sizeof(int) * ns));
   HIP_TRY(c->sqd.ensure(sizeof(float) * ns));
   HIP_TRY(c->slab.ensure(sizeof(double) * kSlabStride * linearize_blocks(ns)));
+  if (c->stats_on) HIP_TRY(c->stats.ensure(sizeof(unsigned int) * kStatFields * ((ns + 63) / 64)));
   return GICP_OK;
 }
 
@@ -708,6 +711,18 @@ gicp_status gicp_knn_target(gicp_ctx* c, const float* q, size_t nq, size_t strid
 gicp_status gicp_get_moments(const gicp_ctx* c, double* out80) {
   if (!c || !out80) return fail(GICP_EINVAL, "null argument");
   std::memcpy(out80, c->state_host->last_mom, sizeof(double) * kSlabStride);
+  return GICP_OK;
+}
+
+// diagnostics: per 64-query group counters of the LAST linearize launch
+gicp_status gicp_debug_stats(gicp_ctx* c, int enable, unsigned int* out, size_t max_words, size_t* nwords) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  c->stats_on = enable != 0;
+  if (out && c->src.cloud && c->stats.p) {
+    const size_t words = std::min(max_words, (size_t)kStatFields * ((c->src.cloud->n + 63) / 64));
+    HIP_TRY(hipMemcpy(out, c->stats.p, sizeof(unsigned int) * words, hipMemcpyDeviceToHost));
+    if (nwords) *nwords = words;
+  }
   return GICP_OK;
 }
 

@@ -21,6 +21,7 @@ constexpr int kMaxLevels = 5;   // leaves + 4 internal levels: n <= 32*64^4
 constexpr int kMoments = 74;
 constexpr int kMomentSlots = 96;
 constexpr int kSlabStride = 80;   // doubles per block partial in the slab
+constexpr int kStatFields = 8;    // per-wave diagnostic counters (DDLO_STATS)
 
 struct CloudDev {
   const float4* pts;              // n sorted points; w = original index (int bits)
@@ -68,6 +69,7 @@ struct AlignJob {
   float* sqd;              // per sorted source point: squared 1-NN distance
   double* slab;            // [nblocks][kSlabStride] partial moments
   AlignState* state;
+  unsigned int* stats;     // optional per-wave diagnostics [wave][kStatFields] (nullptr = off)
   double guess_R[9];
   double guess_t[3];
   double max_corr2;        // max_correspondence_distance^2 (double compare)

@@ -272,7 +272,7 @@ __device__ void regularize(const double C[9], int method, double out[6]) {
 // K2: exact kNN-k (self queries) + covariance
 // ============================================================================
 template <int KCAP, bool EXACT>
-struct KnnVisitor {
+struct KnnVisitor : VisitStats {
   WaveBox box;
   float qx, qy, qz;
   bool active;
@@ -322,12 +322,9 @@ struct KnnVisitor {
     }
     update_worst();
   }
-  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf) {
-    const int start = leaf * kLeafSize;
-    const int cnt = min(kLeafSize, c.n - start);
-    const int lane = lane_id();
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane < cnt) p = c.pts[start + lane];
+  __device__ __forceinline__ float bound() const { return wd; }
+  __device__ __forceinline__ bool need(float4 lo, float4 hi) const { return box_dist2(qx, qy, qz, lo, hi) <= wd; }
+  __device__ __forceinline__ void process(const CloudDev& c, int start, int cnt, float4 p) {
     for (int j = 0; j < cnt; ++j) {
       const float d = dist2(qx, qy, qz, readlane_f(p.x, j), readlane_f(p.y, j), readlane_f(p.z, j));
       const int pj = start + j;
@@ -335,14 +332,12 @@ struct KnnVisitor {
       if (cand) insert(d, pj);
     }
   }
-  __device__ __forceinline__ void leaf(const CloudDev& c, int leaf) {
-    if (leaf >= skip_lo && leaf <= skip_hi) return;
-    const float4 lo = c.box_lo[leaf], hi = c.box_hi[leaf];
-    const bool need = active && box_dist2(qx, qy, qz, lo, hi) <= wd;
-    if (!__any(need)) return;
-    const float before = wd;
-    scan_leaf(c, leaf);
-    if (__any(wd < before)) box = make_wave_box(active, qx, qy, qz, wd);
+  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf) {
+    const int start = leaf * kLeafSize;
+    const int cnt = min(kLeafSize, c.n - start);
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane_id() < cnt) p = c.pts[start + lane_id()];
+    process(c, start, cnt, p);
   }
 };
 
@@ -702,7 +697,19 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       vis.skip_hi = s1;
     }
     vis.box = make_wave_box(active, qx, qy, qz, vis.best);
+    const float ext0 = fmaxf(fmaxf(vis.box.hx - vis.box.lx, vis.box.hy - vis.box.ly), vis.box.hz - vis.box.lz);
     traverse(tgt, vis);
+    if (job->stats && lane == 0) {
+      unsigned int* o = job->stats + (size_t)g * kStatFields;
+      o[0] = vis.st_blocks;
+      o[1] = vis.st_box;
+      o[2] = vis.st_exact;
+      o[3] = vis.st_scan;
+      o[4] = __float_as_uint(ext0);
+      o[5] = (unsigned)__popcll(__ballot(active && vis.bestj < 0));
+      o[6] = (unsigned)__popcll(__ballot(active && vis.best > 0.25f));
+      o[7] = 1;
+    }
 
     const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
     if (active) {

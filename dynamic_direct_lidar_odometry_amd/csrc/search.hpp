@@ -146,19 +146,88 @@ __device__ __forceinline__ bool box_overlap(const WaveBox& w, float4 lo, float4 
 
 // ---------------------------------------------------------------------------
 // Generic cooperative traversal.  Visitor V provides:
-//   WaveBox box;                        current wave box (uniform)
-//   __device__ void leaf(const CloudDev&, int leaf);   may shrink box
+//   WaveBox box;                                  current wave box (uniform)
+//   bool need(float4 lo, float4 hi)               per-lane exact leaf test
+//   void process(const CloudDev&, int start, int cnt, float4 p)
+//                                                 scan one leaf whose points
+//                                                 lanes 0..cnt-1 hold in p
+//   float bound()                                 per-lane squared bound
+//   bool active; float qx, qy, qz; int skip_lo, skip_hi;
+//
+// Leaves are handled a block at a time (the <= 64 children of one level-1
+// node): lane c holds leaf c's box, the wave-box filter and then the EXACT
+// per-lane filter run on registers only (boxes broadcast with readlane), and
+// the surviving leaves are scanned with the next leaf's points prefetched, so
+// a wavefront keeps one global load in flight instead of a dependent chain.
+template <class V>
+__device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt, V& vis) {
+  const int lane = lane_id();
+  float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+  if (lane < cnt) {
+    lo = c.box_lo[base + lane];
+    hi = c.box_hi[base + lane];
+  }
+  const bool ov = lane < cnt && box_overlap(vis.box, lo, hi) && !(base + lane >= vis.skip_lo && base + lane <= vis.skip_hi);
+  unsigned long long mask = __ballot(ov);
+  vis.st_blocks += 1;
+  vis.st_box += __popcll(mask);
+  unsigned long long ex = 0ull;
+  while (mask) {
+    const int b = __builtin_ctzll(mask);
+    mask &= mask - 1;
+    const float4 blo = make_float4(readlane_f(lo.x, b), readlane_f(lo.y, b), readlane_f(lo.z, b), 0.f);
+    const float4 bhi = make_float4(readlane_f(hi.x, b), readlane_f(hi.y, b), readlane_f(hi.z, b), 0.f);
+    if (__any(vis.active && vis.need(blo, bhi))) ex |= 1ull << b;
+  }
+  vis.st_exact += __popcll(ex);
+  if (!ex) return;
+  int cur = __builtin_ctzll(ex);
+  ex &= ex - 1;
+  int start = (base + cur) * kLeafSize;
+  int n_in = min(kLeafSize, c.n - start);
+  float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lane < n_in) p = c.pts[start + lane];
+  bool improved = false;
+  for (;;) {
+    int nxt = -1, nstart = 0, nn = 0;
+    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ex) {
+      nxt = __builtin_ctzll(ex);
+      ex &= ex - 1;
+      nstart = (base + nxt) * kLeafSize;
+      nn = min(kLeafSize, c.n - nstart);
+      if (lane < nn) pn = c.pts[nstart + lane];
+    }
+    // re-check with the bounds tightened by the leaves scanned so far
+    const float4 blo = make_float4(readlane_f(lo.x, cur), readlane_f(lo.y, cur), readlane_f(lo.z, cur), 0.f);
+    const float4 bhi = make_float4(readlane_f(hi.x, cur), readlane_f(hi.y, cur), readlane_f(hi.z, cur), 0.f);
+    if (__any(vis.active && vis.need(blo, bhi))) {
+      const float before = vis.bound();
+      vis.st_scan += 1;
+      vis.process(c, start, n_in, p);
+      improved |= __any(vis.bound() < before);
+    }
+    if (nxt < 0) break;
+    cur = nxt;
+    start = nstart;
+    n_in = nn;
+    p = pn;
+  }
+  if (improved) vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
+}
+
 template <int LV, class V>
 __device__ __forceinline__ void trav_level(const CloudDev& c, int base, unsigned long long mask, V& vis) {
+  // LV >= 2: mask selects nodes of level LV; their children are at LV-1
   while (mask) {
     const int ci = __builtin_ctzll(mask);
     mask &= mask - 1;
     const int node = base + ci;
-    if constexpr (LV == 0) {
-      vis.leaf(c, node);
+    const int cb = node * kFanout;
+    const int cnt = min(kFanout, c.lvl_cnt[LV - 1] - cb);
+    if constexpr (LV == 1) {
+      leaf_block(c, cb, cnt, vis);
     } else {
-      const int cb = node * kFanout;
-      const int cnt = min(kFanout, c.lvl_cnt[LV - 1] - cb);
       const int lane = lane_id();
       bool ov = false;
       if (lane < cnt) {
@@ -181,6 +250,10 @@ __device__ __forceinline__ int level_sel(const int (&a)[kMaxLevels], int i) {
 template <class V>
 __device__ __forceinline__ void traverse(const CloudDev& c, V& vis) {
   const int T = c.nlevels - 1;
+  if (T == 0) {  // the leaves are the top level
+    leaf_block(c, 0, c.lvl_cnt[0], vis);
+    return;
+  }
   const int lane = lane_id();
   bool ov = false;
   if (lane < level_sel(c.lvl_cnt, T)) {
@@ -189,7 +262,6 @@ __device__ __forceinline__ void traverse(const CloudDev& c, V& vis) {
   }
   const unsigned long long m = __ballot(ov);
   switch (T) {
-    case 0: trav_level<0>(c, 0, m, vis); break;
     case 1: trav_level<1>(c, 0, m, vis); break;
     case 2: trav_level<2>(c, 0, m, vis); break;
     case 3: trav_level<3>(c, 0, m, vis); break;
@@ -199,7 +271,11 @@ __device__ __forceinline__ void traverse(const CloudDev& c, V& vis) {
 
 // ---------------------------------------------------------------------------
 // 1-NN visitor: per-lane (best, bestj); bound == best.
-struct NN1Visitor {
+struct VisitStats {
+  unsigned st_blocks = 0, st_box = 0, st_exact = 0, st_scan = 0;
+};
+
+struct NN1Visitor : VisitStats {
   WaveBox box;
   float qx, qy, qz;
   float best;   // squared distance bound (strict <, ties by position)
@@ -207,12 +283,10 @@ struct NN1Visitor {
   bool active;
   int skip_lo, skip_hi;  // leaves already scanned (seeding), uniform
 
-  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf) {
-    const int start = leaf * kLeafSize;
-    const int cnt = min(kLeafSize, c.n - start);
-    const int lane = lane_id();
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane < cnt) p = c.pts[start + lane];
+  __device__ __forceinline__ float bound() const { return best; }
+  __device__ __forceinline__ bool need(float4 lo, float4 hi) const { return box_dist2(qx, qy, qz, lo, hi) <= best; }
+
+  __device__ __forceinline__ void process(const CloudDev& c, int start, int cnt, float4 p) {
     float b = best;
     int bj = bestj;
 #pragma unroll
@@ -231,14 +305,12 @@ struct NN1Visitor {
     }
   }
 
-  __device__ __forceinline__ void leaf(const CloudDev& c, int leaf) {
-    if (leaf >= skip_lo && leaf <= skip_hi) return;
-    const float4 lo = c.box_lo[leaf], hi = c.box_hi[leaf];
-    const bool need = active && box_dist2(qx, qy, qz, lo, hi) <= best;
-    if (!__any(need)) return;
-    const float before = best;
-    scan_leaf(c, leaf);
-    if (__any(best < before)) box = make_wave_box(active, qx, qy, qz, best);
+  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf) {
+    const int start = leaf * kLeafSize;
+    const int cnt = min(kLeafSize, c.n - start);
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane_id() < cnt) p = c.pts[start + lane_id()];
+    process(c, start, cnt, p);
   }
 };
 

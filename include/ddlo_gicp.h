@@ -188,6 +188,9 @@ gicp_status gicp_get_moments(const struct gicp_ctx* ctx, double* out80);
 /* Device time accounting of the linearize kernel inside align (HIP events
  * captured in the align graph).  Off by default. */
 gicp_status gicp_set_profiling(struct gicp_ctx* ctx, int enable);
+/* Diagnostics (development): enable per 64-query-group search counters for
+ * subsequent linearize launches and/or read those of the last launch. */
+gicp_status gicp_debug_stats(struct gicp_ctx* ctx, int enable, unsigned int* out, size_t max_words, size_t* nwords);
 /* The ctx's HIP stream (hipStream_t) for callers that interleave their own work. */
 gicp_status gicp_get_stream(const struct gicp_ctx* ctx, void** stream);
 

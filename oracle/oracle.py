@@ -59,6 +59,16 @@ def default_params(**kw) -> GicpParams:
     return p
 
 
+def as_params(p) -> GicpParams:
+    """Copy any ctypes struct / object with the gicp_params fields into the oracle's type."""
+    if isinstance(p, GicpParams):
+        return p
+    q = GicpParams()
+    for name, _ in GicpParams._fields_:
+        setattr(q, name, getattr(p, name))
+    return q
+
+
 def _fp(a):
     return a.ctypes.data_as(C.c_void_p)
 
@@ -159,7 +169,7 @@ class Gicp:
         self.L = lib()
         self.src = _xyz(source)
         self.tgt = _xyz(target)
-        self.params = params or default_params()
+        self.params = as_params(params) if params is not None else default_params()
         self.h = self.L.oref_gicp_create(C.byref(self.params), _fp(self.src), len(self.src), _fp(self.tgt), len(self.tgt), threads)
 
     def __del__(self):
@@ -171,6 +181,7 @@ class Gicp:
         self.L.oref_gicp_set_threads(self.h, n)
 
     def set_params(self, p: GicpParams):
+        p = as_params(p)
         self.params = p
         self.L.oref_gicp_set_params(self.h, C.byref(p))
 

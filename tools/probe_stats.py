@@ -1,0 +1,47 @@
+"""Developer probe: per-wave search statistics of the linearize kernel."""
+import os, sys, time
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dynamic_direct_lidar_odometry_amd import scene, Context, default_params, SOURCE, TARGET  # noqa
+from oracle import oracle as O  # noqa
+
+
+def summarize(tag, st):
+    st = st[st[:, 7] == 1]
+    ext = st[:, 4].view(np.float32)
+    print(f"[{tag}] groups {len(st)}")
+    for i, name in enumerate(["blocks", "box", "exact", "scan"]):
+        v = st[:, i]
+        print(f"  {name:6s} mean {v.mean():8.1f} p50 {np.percentile(v,50):6.0f} p90 {np.percentile(v,90):6.0f} p99 {np.percentile(v,99):6.0f} max {v.max():6d} sum {v.sum()}")
+    print(f"  extent mean {ext.mean():.2f} p50 {np.percentile(ext,50):.2f} p90 {np.percentile(ext,90):.2f} p99 {np.percentile(ext,99):.2f} max {ext.max():.2f}")
+    print(f"  unmatched lanes/group mean {st[:,5].mean():.2f} max {st[:,5].max()}; lanes with best>0.25 mean {st[:,6].mean():.2f}")
+    top = np.argsort(-st[:, 3])[:5]
+    for t in top:
+        print(f"   worst group {t}: scan {st[t,3]} exact {st[t,2]} box {st[t,1]} ext {ext[t]:.2f} unmatched {st[t,5]} far {st[t,6]}")
+
+
+def main():
+    src, tgt, T = scene.s2s_pair(64, 2048, 1)
+    ctx = Context(0)
+    ctx.set_params(default_params(k_correspondences=10, max_correspondence_distance=1.0, max_iterations=32, transformation_epsilon=5e-4))
+    ctx.set_target(tgt); ctx.set_source(src)
+    ctx.debug_stats(True)
+    ctx.linearize(np.eye(4))
+    summarize("S2S iter0", ctx.debug_stats(True, read=True))
+    ctx.align()
+    summarize("S2S last iter", ctx.debug_stats(True, read=True))
+
+    prob = scene.s2m_problem(64, 2048, 4, 500000, 3)
+    sub = np.concatenate(prob["keyframes"])[prob["subset"]]
+    c2 = Context(0)
+    c2.set_params(default_params(k_correspondences=10, max_correspondence_distance=2.0, max_iterations=32, transformation_epsilon=0.01))
+    c2.set_target(sub); c2.set_source(prob["source"])
+    c2.debug_stats(True)
+    c2.linearize(prob["guess"].astype(np.float64))
+    summarize("S2M iter0", c2.debug_stats(True, read=True))
+    c2.align(prob["guess"])
+    summarize("S2M last iter", c2.debug_stats(True, read=True))
+
+
+if __name__ == "__main__":
+    main()
