@@ -85,10 +85,8 @@ struct CloudData {
     c.quant = quant.as<float>();
     c.n = n;
     c.nlevels = nlevels;
-    for (int l = 0; l < kMaxLevels; ++l) {
-      c.lvl_off[l] = lvl_off[l];
-      c.lvl_cnt[l] = lvl_cnt[l];
-    }
+    c.off0 = lvl_off[0]; c.off1 = lvl_off[1]; c.off2 = lvl_off[2]; c.off3 = lvl_off[3]; c.off4 = lvl_off[4];
+    c.cnt0 = lvl_cnt[0]; c.cnt1 = lvl_cnt[1]; c.cnt2 = lvl_cnt[2]; c.cnt3 = lvl_cnt[3]; c.cnt4 = lvl_cnt[4];
     return c;
   }
 };
@@ -136,10 +134,12 @@ struct gicp_ctx {
   int* flag_host = nullptr;       // pinned
   bool have_align = false;        // a linearize ran against the current src/tgt
   int last_nsrc = 0;
-  // graph cache
-  hipGraphExec_t graph_exec = nullptr;
-  hipGraph_t graph = nullptr;
+  // chunk graphs: [init + C iterations + flag copy] and [C iterations + flag copy]
+  hipGraphExec_t g_first = nullptr, g_rest = nullptr;
+  hipGraph_t gg_first = nullptr, gg_rest = nullptr;
   std::tuple<int, int, const void*> graph_key{-1, -1, nullptr};
+  std::vector<hipEvent_t> chunk_ev;
+  hipStream_t copy_stream = nullptr;
   bool profiling = false;
   std::vector<hipEvent_t> prof_ev;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -282,25 +282,73 @@ gicp_status prepare_align(gicp_ctx* c) {
   return GICP_OK;
 }
 
-gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks) {
+constexpr int kChunk = 4;  // outer iterations per graph launch
+
+gicp_status capture_chunk(gicp_ctx* c, bool with_init, int nblocks, hipGraph_t* g, hipGraphExec_t* ge) {
   const AlignJob* jd = c->job_dev.as<AlignJob>();
-  auto key = std::make_tuple(max_it, nblocks, (const void*)jd);
-  if (!c->graph_exec || c->graph_key != key) {
-    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
-    if (c->graph) (void)hipGraphDestroy(c->graph);
-    c->graph_exec = nullptr;
-    c->graph = nullptr;
-    HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    launch_align_init(c->stream, jd);
-    for (int i = 0; i < max_it; ++i) {
-      launch_linearize(c->stream, jd, nblocks);
-      launch_lm_step(c->stream, jd);
-    }
-    HIP_TRY(hipStreamEndCapture(c->stream, &c->graph));
-    HIP_TRY(hipGraphInstantiate(&c->graph_exec, c->graph, nullptr, nullptr, 0));
+  HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  if (with_init) launch_align_init(c->stream, jd);
+  for (int i = 0; i < kChunk; ++i) {
+    launch_linearize(c->stream, jd, nblocks);
+    launch_lm_step(c->stream, jd);
+  }
+  // publish {iter, done} to pinned host memory at the end of the chunk
+  (void)hipMemcpyAsync(c->flag_host, &c->state_dev.as<AlignState>()->iter, 2 * sizeof(int), hipMemcpyDeviceToHost,
+                       c->stream);
+  HIP_TRY(hipStreamEndCapture(c->stream, g));
+  HIP_TRY(hipGraphInstantiate(ge, *g, nullptr, nullptr, 0));
+  return GICP_OK;
+}
+
+// Launch chunks of kChunk iterations, keeping one chunk queued ahead while the
+// host checks the previous chunk's done flag: at most one chunk of no-op
+// launches runs after convergence, and it overlaps the final state read-back.
+// Returns the index of the chunk after which the state is final.
+gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chunk) {
+  const void* jd = c->job_dev.p;
+  auto key = std::make_tuple(kChunk, nblocks, jd);
+  if (!c->g_first || c->graph_key != key) {
+    if (c->g_first) (void)hipGraphExecDestroy(c->g_first);
+    if (c->g_rest) (void)hipGraphExecDestroy(c->g_rest);
+    if (c->gg_first) (void)hipGraphDestroy(c->gg_first);
+    if (c->gg_rest) (void)hipGraphDestroy(c->gg_rest);
+    c->g_first = c->g_rest = nullptr;
+    c->gg_first = c->gg_rest = nullptr;
+    gicp_status s = capture_chunk(c, true, nblocks, &c->gg_first, &c->g_first);
+    if (s) return s;
+    s = capture_chunk(c, false, nblocks, &c->gg_rest, &c->g_rest);
+    if (s) return s;
     c->graph_key = key;
   }
-  HIP_TRY(hipGraphLaunch(c->graph_exec, c->stream));
+  const int nchunks = (max_it + kChunk - 1) / kChunk;
+  while ((int)c->chunk_ev.size() < nchunks) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->chunk_ev.push_back(e);
+  }
+  c->flag_host[0] = 0;
+  c->flag_host[1] = 0;
+  HIP_TRY(hipGraphLaunch(c->g_first, c->stream));
+  HIP_TRY(hipEventRecord(c->chunk_ev[0], c->stream));
+  int launched = 1;
+  if (nchunks > 1) {
+    HIP_TRY(hipGraphLaunch(c->g_rest, c->stream));
+    HIP_TRY(hipEventRecord(c->chunk_ev[1], c->stream));
+    launched = 2;
+  }
+  int k = 0;
+  for (;;) {
+    HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
+    const volatile int* fl = c->flag_host;
+    if (fl[1] || k == nchunks - 1) break;
+    if (launched < nchunks) {
+      HIP_TRY(hipGraphLaunch(c->g_rest, c->stream));
+      HIP_TRY(hipEventRecord(c->chunk_ev[launched], c->stream));
+      ++launched;
+    }
+    ++k;
+  }
+  *final_chunk = k;
   return GICP_OK;
 }
 
@@ -356,6 +404,7 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   c->device = device;
   gicp_default_params(&c->params);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
   HIP_TRY(hipHostMalloc((void**)&c->job_host, sizeof(AlignJob), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&c->state_host, sizeof(AlignState), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&c->flag_host, sizeof(int) * 4, hipHostMallocDefault));
@@ -374,9 +423,12 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   if (!c) return GICP_OK;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
-  if (c->graph) (void)hipGraphDestroy(c->graph);
+  if (c->g_first) (void)hipGraphExecDestroy(c->g_first);
+  if (c->g_rest) (void)hipGraphExecDestroy(c->g_rest);
+  if (c->gg_first) (void)hipGraphDestroy(c->gg_first);
+  if (c->gg_rest) (void)hipGraphDestroy(c->gg_rest);
   for (auto e : c->prof_ev) (void)hipEventDestroy(e);
+  for (auto e : c->chunk_ev) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->job_host) (void)hipHostFree(c->job_host);
@@ -385,6 +437,7 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   c->src = Side();
   c->tgt = Side();
   (void)hipStreamDestroy(c->stream);
+  (void)hipStreamDestroy(c->copy_stream);
   delete c;
   return GICP_OK;
 }
@@ -535,14 +588,24 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
   if (s) return s;
   const int max_it = c->job_host->max_iterations;
   HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  if (c->profiling)
-    s = run_align_eager_profiled(c, max_it, nblocks);
-  else
-    s = run_align_graph(c, max_it, nblocks);
-  if (s) return s;
-  HIP_TRY(hipEventRecord(c->ev1, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->profiling || max_it <= 0) {
+    s = max_it > 0 ? run_align_eager_profiled(c, max_it, nblocks) : GICP_OK;
+    if (s) return s;
+    if (max_it <= 0) launch_align_init(c->stream, c->job_dev.as<AlignJob>());
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  } else {
+    int fc = 0;
+    s = run_align_graph(c, max_it, nblocks, &fc);
+    if (s) return s;
+    // the state is final after chunk fc; read it on the copy stream so the
+    // (at most one) speculative no-op chunk still queued does not delay us
+    HIP_TRY(hipStreamWaitEvent(c->copy_stream, c->chunk_ev[fc], 0));
+    HIP_TRY(hipEventRecord(c->ev1, c->copy_stream));
+    HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->copy_stream));
+    HIP_TRY(hipStreamSynchronize(c->copy_stream));
+  }
   const AlignState& st = *c->state_host;
   c->have_align = st.iter > 0;
   c->last_nsrc = ns;

@@ -33,9 +33,18 @@ struct CloudDev {
   const float* quant;             // device [lo.x, lo.y, lo.z, scale]
   int n;
   int nlevels;
-  int lvl_off[kMaxLevels];
-  int lvl_cnt[kMaxLevels];
+  // per-level node offset/count, kept as scalars (no array => no scratch
+  // when a kernel holds a CloudDev in registers); use lvl_off()/lvl_cnt()
+  int off0, off1, off2, off3, off4;
+  int cnt0, cnt1, cnt2, cnt3, cnt4;
 };
+
+__host__ __device__ inline int lvl_off(const CloudDev& c, int l) {
+  return l == 0 ? c.off0 : l == 1 ? c.off1 : l == 2 ? c.off2 : l == 3 ? c.off3 : c.off4;
+}
+__host__ __device__ inline int lvl_cnt(const CloudDev& c, int l) {
+  return l == 0 ? c.cnt0 : l == 1 ? c.cnt1 : l == 2 ? c.cnt2 : l == 3 ? c.cnt3 : c.cnt4;
+}
 
 // Per-align device state (one per ctx, lives in device memory).
 struct AlignState {

@@ -336,7 +336,7 @@ struct KnnVisitor : VisitStats {
     const int start = leaf * kLeafSize;
     const int cnt = min(kLeafSize, c.n - start);
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane_id() < cnt) p = c.pts[start + lane_id()];
+    if (lane_id() < cnt) p = ldg4(c.pts, start + lane_id());
     process(c, start, cnt, p);
   }
 };
@@ -345,7 +345,7 @@ struct KnnVisitor : VisitStats {
 template <int KCAP, bool EXACT>
 __device__ __forceinline__ void knn_search(const CloudDev& c, KnnVisitor<KCAP, EXACT>& vis, int s0, int s1) {
   s0 = max(s0, 0);
-  s1 = min(s1, c.lvl_cnt[0] - 1);
+  s1 = min(s1, c.cnt0 - 1);
   for (int l = s0; l <= s1; ++l) vis.scan_leaf(c, l);
   vis.skip_lo = s0;
   vis.skip_hi = s1;
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
     KnnVisitor<KCAP, EXACT> vis;
     vis.init(k);
     vis.active = i < c.n;
-    const float4 q = c.pts[min(i, c.n - 1)];
+    const float4 q = ldg4(c.pts, min(i, c.n - 1));
     vis.qx = q.x;
     vis.qy = q.y;
     vis.qz = q.z;
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
       if (s < k) {
-        const float4 p = c.pts[vis.J[s]];
+        const float4 p = ldg4(c.pts, vis.J[s]);
         mx += (double)p.x;
         my += (double)p.y;
         mz += (double)p.z;
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
       if (s < k) {
-        const float4 p = c.pts[vis.J[s]];
+        const float4 p = ldg4(c.pts, vis.J[s]);
         const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
         C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
         C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __r
     KnnVisitor<KCAP, EXACT> vis;
     vis.init(k);
     vis.active = i < nq;
-    const float4 p = q[min(i, nq - 1)];
+    const float4 p = ldg4(q, min(i, nq - 1));
     vis.qx = p.x;
     vis.qy = p.y;
     vis.qz = p.z;
@@ -603,14 +603,16 @@ __device__ __forceinline__ int moment_base(int lane) {
          3 * ((lane >> 1) & 1);
 }
 
-__device__ __forceinline__ void load_sym6(const double* p, double c[6]) {
-  const double2 a = reinterpret_cast<const double2*>(p)[0];
-  const double2 b = reinterpret_cast<const double2*>(p)[1];
-  const double2 d = reinterpret_cast<const double2*>(p)[2];
+__device__ __forceinline__ void load_sym6(const __attribute__((address_space(1))) double* p, double c[6]) {
+  const auto q = (const __attribute__((address_space(1))) d2v*)p;
+  const d2v a = q[0];
+  const d2v b = q[1];
+  const d2v d = q[2];
   c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y; c[4] = d.x; c[5] = d.y;
 }
 
 constexpr int kLinWaves = 4;   // waves per linearize block
+constexpr float kOptR2 = 0.25f;  // optimistic first-pass radius^2 (0.5 m)
 
 __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
@@ -633,12 +635,14 @@ __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__
 __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
-  const CloudDev& src = job->src;
-  const CloudDev& tgt = job->tgt;
-  const double* __restrict__ src_cov = job->src_cov;
-  const double* __restrict__ tgt_cov = job->tgt_cov;
-  int* __restrict__ corr = job->corr;
-  float* __restrict__ sqd = job->sqd;
+  const CloudDev src = job->src;
+  const CloudDev tgt = job->tgt;
+  const auto src_cov = gp(job->src_cov);
+  const auto tgt_cov = gp(job->tgt_cov);
+  const auto corr = gpw(job->corr);
+  const auto sqd = gpw(job->sqd);
+  const auto slab = gpw(job->slab);
+  unsigned int* const stats = job->stats;
   const float cap2 = job->cap2;
   const double max_corr2 = job->max_corr2;
   const int have_prev = st->have_prev;
@@ -660,54 +664,74 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const int i = g * 64 + lane;
     const bool active = i < src.n;
-    const float4 a = src.pts[active ? i : src.n - 1];
+    const float4 a = ldg4(src.pts, active ? i : src.n - 1);
     // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
 
+    // Pass 1: bound = distance to the previous correspondence at the new
+    // pose when there is one (tight), else an optimistic radius kOptR.
+    // Pass 2 (exact completion): lanes whose pass-1 radius was clipped to
+    // kOptR and found nothing search again with the full max_corr bound.
+    const float opt2 = fminf(cap2, kOptR2);
     NN1Visitor vis;
     vis.qx = qx;
     vis.qy = qy;
     vis.qz = qz;
     vis.active = active;
-    vis.best = active ? cap2 : -1.f;
+    vis.best = active ? opt2 : -1.f;
     vis.bestj = -1;
     vis.skip_lo = 1;
     vis.skip_hi = 0;
+    bool clipped = active;   // pass-1 bound below cap2 without a candidate
     if (have_prev && active) {
       const int j = corr[i];
       if (j >= 0) {
-        const float4 p = tgt.pts[j];
+        const float4 p = ldg4(tgt.pts, j);
         const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
         if (d < cap2) {
           vis.best = d;
           vis.bestj = j;
+          clipped = false;
         }
       }
     }
-    if (!have_prev) {
-      // seed around the Morton position of the first active lane's query
-      const float sx = uniform_f(qx), sy = uniform_f(qy), sz = uniform_f(qz);
-      const int pos = wave_lower_bound(tgt.keys, tgt.n, morton_key(sx, sy, sz, tgt.quant));
-      const int leaf = min(pos, tgt.n - 1) / kLeafSize;
-      const int s0 = max(leaf - 1, 0), s1 = min(leaf + 2, tgt.lvl_cnt[0] - 1);
-      for (int l = s0; l <= s1; ++l) vis.scan_leaf(tgt, l);
-      vis.skip_lo = s0;
-      vis.skip_hi = s1;
-    }
+    if (!(opt2 < cap2)) clipped = false;
     vis.box = make_wave_box(active, qx, qy, qz, vis.best);
     const float ext0 = fmaxf(fmaxf(vis.box.hx - vis.box.lx, vis.box.hy - vis.box.ly), vis.box.hz - vis.box.lz);
     traverse(tgt, vis);
-    if (job->stats && lane == 0) {
-      unsigned int* o = job->stats + (size_t)g * kStatFields;
+    const bool again = clipped && vis.bestj < 0;
+    if (__any(again)) {
+      NN1Visitor v2;
+      v2.qx = qx;
+      v2.qy = qy;
+      v2.qz = qz;
+      v2.active = again;
+      v2.best = again ? cap2 : -1.f;
+      v2.bestj = -1;
+      v2.skip_lo = 1;
+      v2.skip_hi = 0;
+      v2.box = make_wave_box(again, qx, qy, qz, v2.best);
+      traverse(tgt, v2);
+      if (again) {
+        vis.best = v2.best;
+        vis.bestj = v2.bestj;
+      }
+      vis.st_blocks += v2.st_blocks;
+      vis.st_box += v2.st_box;
+      vis.st_exact += v2.st_exact;
+      vis.st_scan += v2.st_scan;
+    }
+    if (stats && lane == 0) {
+      unsigned int* o = stats + (size_t)g * kStatFields;
       o[0] = vis.st_blocks;
       o[1] = vis.st_box;
       o[2] = vis.st_exact;
       o[3] = vis.st_scan;
       o[4] = __float_as_uint(ext0);
       o[5] = (unsigned)__popcll(__ballot(active && vis.bestj < 0));
-      o[6] = (unsigned)__popcll(__ballot(active && vis.best > 0.25f));
+      o[6] = (unsigned)__popcll(__ballot(again));
       o[7] = 1;
     }
 
@@ -720,7 +744,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
     Contrib C;
     if (valid) {
       const int j = vis.bestj;
-      const float4 b = tgt.pts[j];
+      const float4 b = ldg4(tgt.pts, j);
       double ca[6], cb[6];
       load_sym6(src_cov + 6 * (size_t)i, ca);
       load_sym6(tgt_cov + 6 * (size_t)j, cb);
@@ -779,7 +803,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
     double s = 0.0;
     if (threadIdx.x < kMoments)
       for (int w = 0; w < kLinWaves; ++w) s += red[w][threadIdx.x];
-    job->slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = s;
+    slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = s;
   }
 }
 
@@ -883,50 +907,46 @@ __device__ __forceinline__ double Sgen(int c, int r, int s) {
   return (r == 0 && s == 1) ? -1.0 : ((r == 1 && s == 0) ? 1.0 : 0.0);
 }
 
-// H = sum J^T M J, b = sum J^T M e with J = [skew(q) | -I] (nano_gicp_impl.hpp:317-324)
-__device__ void build_normal_equations(const Moments& mo, double H[36], double b[6]) {
-  // H_rr(i,j) = sum_{c,d} sum_{r,s} S_c[r][i] W(c,d)[r][s] S_d[s][j]
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) {
-      double s = 0.0;
-      for (int c = 0; c < 3; ++c)
-        for (int d = 0; d < 3; ++d)
-          for (int r = 0; r < 3; ++r) {
-            const double sr = Sgen(c, r, i);
-            if (sr == 0.0) continue;
-            for (int q = 0; q < 3; ++q) {
-              const double sq = Sgen(d, q, j);
-              if (sq == 0.0) continue;
-              s += sr * mo.W(c, d, r, q) * sq;
-            }
-          }
-      H[6 * i + j] = s;
-    }
-  // H_rt(i,j) = sum_c sum_r S_c[r][i] W(c,3)[r][j] * (-1)
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) {
-      double s = 0.0;
-      for (int c = 0; c < 3; ++c)
-        for (int r = 0; r < 3; ++r) {
-          const double sr = Sgen(c, r, i);
-          if (sr != 0.0) s += sr * mo.W(c, 3, r, j);
-        }
-      H[6 * i + 3 + j] = -s;
-      H[6 * (3 + j) + i] = -s;
-    }
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) H[6 * (3 + i) + 3 + j] = mo.W(3, 3, i, j);
-  // b_r(i) = sum_c sum_r S_c[r][i] G(r,c) ; b_t = -G(:,3)
-  for (int i = 0; i < 3; ++i) {
-    double s = 0.0;
+// H = sum J^T M J, b = sum J^T M e with J = [skew(q) | -I] (nano_gicp_impl.hpp:317-324),
+// one entry per thread: e in [0,36) -> H(e/6, e%6), e in [36,42) -> b(e-36).
+__device__ double normal_eq_entry(const Moments& mo, int e) {
+  if (e >= 36) {
+    const int i = e - 36;
+    if (i >= 3) return -mo.G(i - 3, 3);  // b_t = -G(:,3)
+    double s = 0.0;                      // b_r(i) = sum_c sum_r S_c[r][i] G(r,c)
     for (int c = 0; c < 3; ++c)
       for (int r = 0; r < 3; ++r) {
         const double sr = Sgen(c, r, i);
         if (sr != 0.0) s += sr * mo.G(r, c);
       }
-    b[i] = s;
-    b[3 + i] = -mo.G(i, 3);
+    return s;
   }
+  const int i = e / 6, j = e % 6;
+  if (i < 3 && j < 3) {  // H_rr(i,j) = sum_{c,d} sum_{r,q} S_c[r][i] W(c,d)[r][q] S_d[q][j]
+    double s = 0.0;
+    for (int c = 0; c < 3; ++c)
+      for (int d = 0; d < 3; ++d)
+        for (int r = 0; r < 3; ++r) {
+          const double sr = Sgen(c, r, i);
+          if (sr == 0.0) continue;
+          for (int q = 0; q < 3; ++q) {
+            const double sq = Sgen(d, q, j);
+            if (sq == 0.0) continue;
+            s += sr * mo.W(c, d, r, q) * sq;
+          }
+        }
+    return s;
+  }
+  if (i >= 3 && j >= 3) return mo.W(3, 3, i - 3, j - 3);  // H_tt = sum M
+  // H_rt(a, t) = -sum_c sum_r S_c[r][a] W(c,3)[r][t]
+  const int a = i < 3 ? i : j, t = i < 3 ? j - 3 : i - 3;
+  double s = 0.0;
+  for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < 3; ++r) {
+      const double sr = Sgen(c, r, a);
+      if (sr != 0.0) s += sr * mo.W(c, 3, r, t);
+    }
+  return -s;
 }
 
 // y0 - y(delta) for the frozen correspondences/M of the last linearize:
@@ -970,18 +990,31 @@ __device__ void compose(const double Rd[9], const double td[3], const double R[9
 }
 
 constexpr int kLmThreads = 512;
+constexpr int kMaxTrials = 64;
 
+// One workgroup: (1) fixed-order reduction of the linearize partials,
+// (2) H and b one entry per thread, (3) every LM trial in its own thread —
+// the reference's trial sequence is fully determined up front (lambda_i =
+// nu_{i-1} lambda_{i-1}, nu doubling: lsq_registration_impl.hpp:187-223), so
+// trial i is evaluated with exactly the lambda the sequential loop would use,
+// (4) thread 0 replays the sequential accept/reject decisions.
 __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
   __shared__ double part[6][kSlabStride];
   __shared__ double mom[kSlabStride];
+  __shared__ double Hs[36], bs[6];
+  __shared__ double tr_rho[kMaxTrials], tr_lambda[kMaxTrials];
+  __shared__ double tr_R[kMaxTrials][9], tr_t[kMaxTrials][3];
+  __shared__ int tr_conv[kMaxTrials];
+  __shared__ double lambda0_s;
   const int tid = threadIdx.x;
   const int nb = job->nblocks;
+  const auto slab = gp(job->slab);
   if (tid < 6 * kSlabStride) {
     const int v = tid % kSlabStride, p = tid / kSlabStride;
     double s = 0.0;
-    for (int b = p; b < nb; b += 6) s += job->slab[(size_t)b * kSlabStride + v];
+    for (int b = p; b < nb; b += 6) s += slab[(size_t)b * kSlabStride + v];
     part[p][v] = s;
   }
   __syncthreads();
@@ -991,89 +1024,120 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
     mom[tid] = s;
   }
   __syncthreads();
-  if (tid != 0) return;
-
   const Moments mo{mom};
-  double H[36], b[6];
-  build_normal_equations(mo, H, b);
-  const double y0 = mo.y0();
-  const int it = st->iter;
-  st->nr_iterations = it;
-  st->final_cost = y0;
-  st->num_corr = (int)mo.count();
+  if (tid < 42) {
+    const double v = normal_eq_entry(mo, tid);
+    if (tid < 36)
+      Hs[tid] = v;
+    else
+      bs[tid - 36] = v;
+  }
+  __syncthreads();
   double R[9], t[3];
   for (int e = 0; e < 9; ++e) R[e] = st->R[e];
   for (int e = 0; e < 3; ++e) t[e] = st->t[e];
-  for (int e = 0; e < 9; ++e) st->last_lin_R[e] = R[e];
-  for (int e = 0; e < 3; ++e) st->last_lin_t[e] = t[e];
-  for (int e = 0; e < 6; ++e) st->last_b[e] = b[e];
-  for (int e = 0; e < kSlabStride; ++e) st->last_mom[e] = mom[e];
-
-  bool ok = false;
-  double Rd[9], td[3];
-  double nb6[6];
-  for (int e = 0; e < 6; ++e) nb6[e] = -b[e];
-  if (job->optimizer == 0) {  // step_gn (lsq_registration_impl.hpp:155-173)
-    double d[6];
-    ldlt_solve6_d(H, nb6, d);
-    so3_exp_d(d, Rd);
-    td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
-    double Rn[9], tn[3];
-    compose(Rd, td, R, t, Rn, tn);
-    for (int e = 0; e < 9; ++e) st->R[e] = Rn[e];
-    for (int e = 0; e < 3; ++e) st->t[e] = tn[e];
-    for (int e = 0; e < 36; ++e) st->final_hessian[e] = H[e];
-    ok = true;
-  } else {  // step_lm (:175-232)
+  const bool lm = job->optimizer != 0;
+  if (lm && tid == 0) {
     double lambda = st->lambda;
     if (lambda < 0.0) {
       double mx = 0.0;
-      for (int e = 0; e < 6; ++e) mx = fmax(mx, fabs(H[7 * e]));
+      for (int e = 0; e < 6; ++e) mx = fmax(mx, fabs(Hs[7 * e]));
       lambda = job->lm_init_lambda_factor * mx;
     }
-    double nu = 2.0;
-    int trials = 0;
-    for (int i = 0; i < job->lm_max_iterations; ++i) {
-      double A[36];
-      for (int e = 0; e < 36; ++e) A[e] = H[e];
-      for (int e = 0; e < 6; ++e) A[7 * e] += lambda;
-      double d[6];
-      ldlt_solve6_d(A, nb6, d);
-      so3_exp_d(d, Rd);
-      td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
-      ++trials;
-      const double dec = cost_decrease(mo, Rd, td);   // y0 - yi
-      double den = 0.0;
-      for (int e = 0; e < 6; ++e) den += d[e] * (lambda * d[e] - b[e]);
-      const double rho = dec / den;
-      if (rho < 0) {
-        if (is_converged_d(job, Rd, td)) {
-          ok = true;
-          break;
-        }
+    lambda0_s = lambda;
+  }
+  __syncthreads();
+  const int ntr = lm ? min(job->lm_max_iterations, kMaxTrials) : 1;
+  if (tid < ntr) {
+    double lambda = 0.0;
+    if (lm) {
+      lambda = lambda0_s;
+      double nu = 2.0;
+      for (int k = 0; k < tid; ++k) {
         lambda = nu * lambda;
         nu = 2 * nu;
+      }
+    }
+    double A[36], nb6[6], d[6];
+    for (int e = 0; e < 36; ++e) A[e] = Hs[e];
+    if (lm)
+      for (int e = 0; e < 6; ++e) A[7 * e] += lambda;
+    for (int e = 0; e < 6; ++e) nb6[e] = -bs[e];
+    ldlt_solve6_d(A, nb6, d);
+    double Rd[9], td[3];
+    so3_exp_d(d, Rd);
+    td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
+    double rho = 1.0;
+    if (lm) {
+      const double dec = cost_decrease(mo, Rd, td);  // y0 - yi
+      double den = 0.0;
+      for (int e = 0; e < 6; ++e) den += d[e] * (lambda * d[e] - bs[e]);
+      rho = dec / den;
+    }
+    tr_rho[tid] = rho;
+    tr_lambda[tid] = lambda;
+    tr_conv[tid] = is_converged_d(job, Rd, td) ? 1 : 0;
+    for (int e = 0; e < 9; ++e) tr_R[tid][e] = Rd[e];
+    for (int e = 0; e < 3; ++e) tr_t[tid][e] = td[e];
+  }
+  __syncthreads();
+  if (tid != 0) return;
+
+  const int it = st->iter;
+  st->nr_iterations = it;
+  st->final_cost = mo.y0();
+  st->num_corr = (int)mo.count();
+  for (int e = 0; e < 9; ++e) st->last_lin_R[e] = R[e];
+  for (int e = 0; e < 3; ++e) st->last_lin_t[e] = t[e];
+  for (int e = 0; e < 6; ++e) st->last_b[e] = bs[e];
+  for (int e = 0; e < kSlabStride; ++e) st->last_mom[e] = mom[e];
+
+  bool ok = false;
+  int chosen = -1;
+  bool accept = false;
+  if (!lm) {  // step_gn: always take the step (lsq_registration_impl.hpp:155-173)
+    ok = true;
+    chosen = 0;
+    accept = true;
+  } else {    // step_lm decisions (:188-231)
+    int i = 0;
+    for (; i < ntr; ++i) {
+      if (tr_rho[i] < 0) {
+        if (tr_conv[i]) {
+          ok = true;
+          chosen = i;
+          break;
+        }
         continue;
       }
-      double Rn[9], tn[3];
-      compose(Rd, td, R, t, Rn, tn);
-      for (int e = 0; e < 9; ++e) st->R[e] = Rn[e];
-      for (int e = 0; e < 3; ++e) st->t[e] = tn[e];
-      const double c = 2 * rho - 1;
-      lambda = lambda * fmax(1.0 / 3.0, 1 - c * c * c);
-      for (int e = 0; e < 36; ++e) st->final_hessian[e] = H[e];
       ok = true;
+      accept = true;
+      chosen = i;
       break;
     }
-    st->lambda = lambda;
-    st->lm_trials += trials;
+    st->lm_trials += ok ? chosen + 1 : ntr;
+    if (accept) {
+      const double c = 2 * tr_rho[chosen] - 1;
+      st->lambda = tr_lambda[chosen] * fmax(1.0 / 3.0, 1 - c * c * c);
+    } else if (ok) {
+      st->lambda = tr_lambda[chosen];
+    } else {
+      st->lambda = tr_lambda[ntr - 1] * 2.0;  // not observable: the align ends
+    }
+  }
+  if (accept) {
+    double Rn[9], tn[3];
+    compose(tr_R[chosen], tr_t[chosen], R, t, Rn, tn);
+    for (int e = 0; e < 9; ++e) st->R[e] = Rn[e];
+    for (int e = 0; e < 3; ++e) st->t[e] = tn[e];
+    for (int e = 0; e < 36; ++e) st->final_hessian[e] = Hs[e];
   }
   st->iter = it + 1;
   st->have_prev = 1;
   if (!ok) {
     st->lm_failed = 1;
     st->done = 1;
-  } else if (is_converged_d(job, Rd, td)) {
+  } else if (tr_conv[chosen]) {
     st->converged = 1;
     st->done = 1;
   }
@@ -1084,8 +1148,8 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
 // K6: residuals (getResiduals) — unbounded 1-NN for points without a
 // correspondence, at the pose of the last linearization.
 __global__ __launch_bounds__(256) void k_residuals(const AlignJob* __restrict__ job, double* __restrict__ out) {
-  const CloudDev& src = job->src;
-  const CloudDev& tgt = job->tgt;
+  const CloudDev src = job->src;
+  const CloudDev tgt = job->tgt;
   const AlignState* st = job->state;
   float Rf[9], tf[3];
   for (int e = 0; e < 9; ++e) Rf[e] = (float)st->last_lin_R[e];
@@ -1099,7 +1163,7 @@ __global__ __launch_bounds__(256) void k_residuals(const AlignJob* __restrict__ 
     float d2 = active ? job->sqd[i] : 0.f;
     const bool need = active && !(d2 < INFINITY);
     if (__any(need)) {
-      const float4 a = src.pts[active ? i : src.n - 1];
+      const float4 a = ldg4(src.pts, active ? i : src.n - 1);
       NN1Visitor vis;
       vis.qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
       vis.qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
@@ -1114,7 +1178,7 @@ __global__ __launch_bounds__(256) void k_residuals(const AlignJob* __restrict__ 
         for (int o = -4; o <= 4; ++o) {
           const int j = pos + o;
           if (j < 0 || j >= tgt.n) continue;
-          const float4 p = tgt.pts[j];
+          const float4 p = ldg4(tgt.pts, j);
           const float d = dist2(vis.qx, vis.qy, vis.qz, p.x, p.y, p.z);
           if (d < vis.best || (d == vis.best && (unsigned)j < (unsigned)vis.bestj)) {
             vis.best = d;

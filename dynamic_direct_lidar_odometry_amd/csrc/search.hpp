@@ -28,6 +28,25 @@ namespace ddlo {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Global-address-space view of a generic pointer: loads through it compile to
+// global_load (counted on vmcnt only) instead of flat_load, whose lgkmcnt
+// share would make every scalar-load wait drain the prefetched leaf.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gp(const T* p) {
+  return (const __attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gpw(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+// 16-byte global load of a float4 element
+__device__ __forceinline__ float4 ldg4(const float4* p, long i) {
+  const f4v v = ((const __attribute__((address_space(1))) f4v*)p)[i];
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -89,7 +108,7 @@ __device__ __forceinline__ int wave_lower_bound(const unsigned long long* keys, 
   while (hi - lo > 64) {
     const int step = (hi - lo + 63) / 64;
     const int idx = lo + lane * step;
-    const bool less = idx < hi && keys[idx] < key;
+    const bool less = idx < hi && gp(keys)[idx] < key;
     const int cnt = __popcll(__ballot(less));   // pivots strictly below key
     // answer lies in (lo + (cnt-1)*step, lo + cnt*step]
     const int nlo = cnt == 0 ? lo : lo + (cnt - 1) * step + 1;
@@ -98,7 +117,7 @@ __device__ __forceinline__ int wave_lower_bound(const unsigned long long* keys, 
     hi = nhi;
   }
   const int idx = lo + lane;
-  const bool less = idx < hi && keys[idx] < key;
+  const bool less = idx < hi && gp(keys)[idx] < key;
   return lo + __popcll(__ballot(less));
 }
 
@@ -107,7 +126,7 @@ __device__ __forceinline__ int wave_lower_bound_lane(const unsigned long long* k
   int lo = 0, hi = n;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if (keys[mid] < key)
+    if (gp(keys)[mid] < key)
       lo = mid + 1;
     else
       hi = mid;
@@ -164,8 +183,8 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
   const int lane = lane_id();
   float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
   if (lane < cnt) {
-    lo = c.box_lo[base + lane];
-    hi = c.box_hi[base + lane];
+    lo = ldg4(c.box_lo, base + lane);
+    hi = ldg4(c.box_hi, base + lane);
   }
   const bool ov = lane < cnt && box_overlap(vis.box, lo, hi) && !(base + lane >= vis.skip_lo && base + lane <= vis.skip_hi);
   unsigned long long mask = __ballot(ov);
@@ -186,7 +205,7 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
   int start = (base + cur) * kLeafSize;
   int n_in = min(kLeafSize, c.n - start);
   float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (lane < n_in) p = c.pts[start + lane];
+  if (lane < n_in) p = ldg4(c.pts, start + lane);
   bool improved = false;
   for (;;) {
     int nxt = -1, nstart = 0, nn = 0;
@@ -196,7 +215,7 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
       ex &= ex - 1;
       nstart = (base + nxt) * kLeafSize;
       nn = min(kLeafSize, c.n - nstart);
-      if (lane < nn) pn = c.pts[nstart + lane];
+      if (lane < nn) pn = ldg4(c.pts, nstart + lane);
     }
     // re-check with the bounds tightened by the leaves scanned so far
     const float4 blo = make_float4(readlane_f(lo.x, cur), readlane_f(lo.y, cur), readlane_f(lo.z, cur), 0.f);
@@ -224,40 +243,32 @@ __device__ __forceinline__ void trav_level(const CloudDev& c, int base, unsigned
     mask &= mask - 1;
     const int node = base + ci;
     const int cb = node * kFanout;
-    const int cnt = min(kFanout, c.lvl_cnt[LV - 1] - cb);
+    const int cnt = min(kFanout, lvl_cnt(c, LV - 1) - cb);
     if constexpr (LV == 1) {
       leaf_block(c, cb, cnt, vis);
     } else {
       const int lane = lane_id();
       bool ov = false;
       if (lane < cnt) {
-        const int o = c.lvl_off[LV - 1] + cb + lane;
-        ov = box_overlap(vis.box, c.box_lo[o], c.box_hi[o]);
+        const int o = lvl_off(c, LV - 1) + cb + lane;
+        ov = box_overlap(vis.box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
       }
       trav_level<LV - 1>(c, cb, __ballot(ov), vis);
     }
   }
 }
 
-// runtime-indexed read of a small per-level array without scratch (rule 20)
-__device__ __forceinline__ int level_sel(const int (&a)[kMaxLevels], int i) {
-  int r = a[0];
-#pragma unroll
-  for (int l = 1; l < kMaxLevels; ++l) r = (i == l) ? a[l] : r;
-  return r;
-}
-
 template <class V>
 __device__ __forceinline__ void traverse(const CloudDev& c, V& vis) {
   const int T = c.nlevels - 1;
   if (T == 0) {  // the leaves are the top level
-    leaf_block(c, 0, c.lvl_cnt[0], vis);
+    leaf_block(c, 0, c.cnt0, vis);
     return;
   }
   const int lane = lane_id();
   bool ov = false;
-  if (lane < level_sel(c.lvl_cnt, T)) {
-    const int o = level_sel(c.lvl_off, T) + lane;
+  if (lane < lvl_cnt(c, T)) {
+    const int o = lvl_off(c, T) + lane;
     ov = box_overlap(vis.box, c.box_lo[o], c.box_hi[o]);
   }
   const unsigned long long m = __ballot(ov);
@@ -309,7 +320,7 @@ struct NN1Visitor : VisitStats {
     const int start = leaf * kLeafSize;
     const int cnt = min(kLeafSize, c.n - start);
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane_id() < cnt) p = c.pts[start + lane_id()];
+    if (lane_id() < cnt) p = ldg4(c.pts, start + lane_id());
     process(c, start, cnt, p);
   }
 };
