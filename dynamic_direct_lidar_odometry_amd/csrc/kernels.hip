@@ -353,6 +353,19 @@ __device__ __forceinline__ void knn_search(const CloudDev& c, KnnVisitor<KCAP, E
   traverse(c, vis);
 }
 
+// kNN-k of the cloud's own points: seed with the group's own leaves, then a
+// split search (keys = the cloud's sorted Morton keys)
+template <int KCAP, bool EXACT>
+__device__ __forceinline__ void knn_self_search(const CloudDev& c, KnnVisitor<KCAP, EXACT>& vis, int s0, int s1,
+                                                unsigned long long key) {
+  s0 = max(s0, 0);
+  s1 = min(s1, c.cnt0 - 1);
+  for (int l = s0; l <= s1; ++l) vis.scan_leaf(c, l);
+  vis.skip_lo = s0;
+  vis.skip_hi = s1;
+  split_search(c, vis, key);
+}
+
 // covariances of a cloud: wave w handles sorted points [64w, 64w+64) (leaves 2w, 2w+1)
 template <int KCAP, bool EXACT>
 __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int method, double* __restrict__ cov6) {
@@ -368,7 +381,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
     vis.qx = q.x;
     vis.qy = q.y;
     vis.qz = q.z;
-    knn_search(c, vis, 2 * g - 1, 2 * g + 2);
+    knn_self_search(c, vis, 2 * g - 1, 2 * g + 2, gp(c.keys)[min(i, c.n - 1)]);
     if (!vis.active) continue;
     // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
     double mx = 0, my = 0, mz = 0;
@@ -698,9 +711,9 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       }
     }
     if (!(opt2 < cap2)) clipped = false;
-    vis.box = make_wave_box(active, qx, qy, qz, vis.best);
-    const float ext0 = fmaxf(fmaxf(vis.box.hx - vis.box.lx, vis.box.hy - vis.box.ly), vis.box.hz - vis.box.lz);
-    traverse(tgt, vis);
+    const unsigned long long skey = gp(src.keys)[active ? i : src.n - 1];
+    const float ext0 = box_extent(make_wave_box(active, qx, qy, qz, vis.best));
+    split_search(tgt, vis, skey);
     const bool again = clipped && vis.bestj < 0;
     if (__any(again)) {
       NN1Visitor v2;
@@ -712,8 +725,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       v2.bestj = -1;
       v2.skip_lo = 1;
       v2.skip_hi = 0;
-      v2.box = make_wave_box(again, qx, qy, qz, v2.best);
-      traverse(tgt, v2);
+      split_search(tgt, v2, skey);
       if (again) {
         vis.best = v2.best;
         vis.bestj = v2.bestj;
@@ -722,6 +734,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       vis.st_box += v2.st_box;
       vis.st_exact += v2.st_exact;
       vis.st_scan += v2.st_scan;
+      vis.st_splits += v2.st_splits;
     }
     if (stats && lane == 0) {
       unsigned int* o = stats + (size_t)g * kStatFields;
@@ -731,7 +744,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       o[3] = vis.st_scan;
       o[4] = __float_as_uint(ext0);
       o[5] = (unsigned)__popcll(__ballot(active && vis.bestj < 0));
-      o[6] = (unsigned)__popcll(__ballot(again));
+      o[6] = (unsigned)__popcll(__ballot(again)) | (vis.st_splits << 16);
       o[7] = 1;
     }
 

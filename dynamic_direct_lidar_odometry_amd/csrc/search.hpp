@@ -281,9 +281,78 @@ __device__ __forceinline__ void traverse(const CloudDev& c, V& vis) {
 }
 
 // ---------------------------------------------------------------------------
+// Compact sub-groups.  A wavefront's 64 queries are consecutive in Morton
+// order, which is spatially compact except where the Z-curve jumps: a group
+// straddling a jump has a union box of tens of metres and would drag
+// thousands of leaves through the filters.  split_search() measures the union
+// box and, if it exceeds kSplitExtent, splits the lane range at its largest
+// Morton jump (at most twice => <= 4 sub-groups), searching each sub-range
+// with the other lanes inactive.  `key` is the lane's Morton key in the
+// query cloud's own quantisation (rigid transforms keep the geometry).
+constexpr float kSplitExtent = 3.0f;
+
+__device__ __forceinline__ int morton_jump_split(unsigned long long key, int lo, int hi) {
+  // lane with the largest (key ^ previous key) in (lo, hi); returns split lane
+  const int lane = lane_id();
+  const unsigned long long prev = __shfl_up(key, 1);
+  int score = -1;
+  if (lane > lo && lane < hi) score = (64 - __clzll(key ^ prev)) * 64 + lane;
+  int best = score;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) best = max(best, __shfl_xor(best, m));
+  best = __builtin_amdgcn_readfirstlane(best);
+  return best < 0 ? (lo + hi) / 2 : (best & 63);
+}
+
+template <class V>
+__device__ __forceinline__ void search_range(const CloudDev& c, V& vis, bool base_active, int lo, int hi) {
+  const int lane = lane_id();
+  vis.active = base_active && lane >= lo && lane < hi;
+  vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
+  traverse(c, vis);
+}
+
+__device__ __forceinline__ float box_extent(const WaveBox& b) {
+  return fmaxf(fmaxf(b.hx - b.lx, b.hy - b.ly), b.hz - b.lz);
+}
+
+template <class V>
+__device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned long long key) {
+  const bool base_active = vis.active;
+  const WaveBox whole = make_wave_box(base_active, vis.qx, vis.qy, vis.qz, vis.bound());
+  if (!(box_extent(whole) > kSplitExtent)) {
+    vis.box = whole;
+    traverse(c, vis);
+    return;
+  }
+  vis.st_splits += 1;
+  const int s = morton_jump_split(key, 0, 64);
+  // each half: split once more if still extended
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int lo = h == 0 ? 0 : s, hi = h == 0 ? s : 64;
+    if (lo >= hi) continue;
+    const int lane = lane_id();
+    const bool act = base_active && lane >= lo && lane < hi;
+    const WaveBox hb = make_wave_box(act, vis.qx, vis.qy, vis.qz, vis.bound());
+    if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
+      vis.st_splits += 1;
+      const int s2 = morton_jump_split(key, lo, hi);
+      search_range(c, vis, base_active, lo, s2);
+      search_range(c, vis, base_active, s2, hi);
+    } else if (__any(act)) {
+      vis.active = act;
+      vis.box = hb;
+      traverse(c, vis);
+    }
+  }
+  vis.active = base_active;
+}
+
+// ---------------------------------------------------------------------------
 // 1-NN visitor: per-lane (best, bestj); bound == best.
 struct VisitStats {
-  unsigned st_blocks = 0, st_box = 0, st_exact = 0, st_scan = 0;
+  unsigned st_blocks = 0, st_box = 0, st_exact = 0, st_scan = 0, st_splits = 0;
 };
 
 struct NN1Visitor : VisitStats {

@@ -14,7 +14,7 @@ def summarize(tag, st):
         v = st[:, i]
         print(f"  {name:6s} mean {v.mean():8.1f} p50 {np.percentile(v,50):6.0f} p90 {np.percentile(v,90):6.0f} p99 {np.percentile(v,99):6.0f} max {v.max():6d} sum {v.sum()}")
     print(f"  extent mean {ext.mean():.2f} p50 {np.percentile(ext,50):.2f} p90 {np.percentile(ext,90):.2f} p99 {np.percentile(ext,99):.2f} max {ext.max():.2f}")
-    print(f"  unmatched lanes/group mean {st[:,5].mean():.2f} max {st[:,5].max()}; lanes with best>0.25 mean {st[:,6].mean():.2f}")
+    print(f"  unmatched lanes/group mean {st[:,5].mean():.2f} max {st[:,5].max()}; pass-2 lanes mean {(st[:,6]&0xffff).mean():.2f}; splits mean {(st[:,6]>>16).mean():.3f} max {(st[:,6]>>16).max()}")
     top = np.argsort(-st[:, 3])[:5]
     for t in top:
         print(f"   worst group {t}: scan {st[t,3]} exact {st[t,2]} box {st[t,1]} ext {ext[t]:.2f} unmatched {st[t,5]} far {st[t,6]}")
