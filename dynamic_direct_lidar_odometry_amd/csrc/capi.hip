@@ -189,9 +189,10 @@ gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, 
   HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp_bytes, c->keys_tmp.as<unsigned long long>(),
                                              cd->keys.as<unsigned long long>(), c->vals_tmp.as<int>(),
                                              cd->perm.as<int>(), N, 0, 63, s));
-  HIP_TRY(cd->pts.ensure(sizeof(float4) * n));
+  const int npad = cd->lvl_cnt[0] * kLeafSize;  // whole leaves, sentinel-padded
+  HIP_TRY(cd->pts.ensure(sizeof(float4) * npad));
   HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
-  launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, cd->pts.as<float4>(), cd->inv_perm.as<int>());
+  launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
   HIP_TRY(cd->box_lo.ensure(sizeof(float4) * total_boxes));
   HIP_TRY(cd->box_hi.ensure(sizeof(float4) * total_boxes));
   launch_leaf_boxes(s, cd->pts.as<float4>(), N, cd->lvl_cnt[0], cd->box_lo.as<float4>(), cd->box_hi.as<float4>());

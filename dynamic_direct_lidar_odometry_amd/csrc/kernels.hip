@@ -94,10 +94,17 @@ __global__ __launch_bounds__(256) void k_morton(const float4* __restrict__ pts, 
   vals[i] = i;
 }
 
+// Sorted gather; positions [n, npad) get far sentinels (squared distance
+// ~3e36 to any real point) so leaf scans never need a bound check.
+constexpr float kFar = 1e18f;
 __global__ __launch_bounds__(256) void k_gather(const float4* __restrict__ raw, const int* __restrict__ perm, int n,
-                                                float4* __restrict__ sorted, int* __restrict__ inv_perm) {
+                                                int npad, float4* __restrict__ sorted, int* __restrict__ inv_perm) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= npad) return;
+  if (i >= n) {
+    sorted[i] = make_float4(kFar, kFar, kFar, __int_as_float(-1));
+    return;
+  }
   const int o = perm[i];
   sorted[i] = raw[o];
   inv_perm[o] = i;
@@ -324,51 +331,53 @@ struct KnnVisitor : VisitStats {
   }
   __device__ __forceinline__ float bound() const { return wd; }
   __device__ __forceinline__ bool need(float4 lo, float4 hi) const { return box_dist2(qx, qy, qz, lo, hi) <= wd; }
-  __device__ __forceinline__ void process(const CloudDev& c, int start, int cnt, float4 p) {
-    for (int j = 0; j < cnt; ++j) {
-      const float d = dist2(qx, qy, qz, readlane_f(p.x, j), readlane_f(p.y, j), readlane_f(p.z, j));
+  __device__ __forceinline__ void process(const WaveLds* L, int start) {
+    for (int j = 0; j < kLeafSize; ++j) {
+      const float d = dist2(qx, qy, qz, L->px[j], L->py[j], L->pz[j]);
       const int pj = start + j;
       const bool cand = active && (d < wd || (d == wd && (unsigned)pj < (unsigned)wj));
       if (cand) insert(d, pj);
     }
   }
-  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf) {
-    const int start = leaf * kLeafSize;
-    const int cnt = min(kLeafSize, c.n - start);
+  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane_id() < cnt) p = ldg4(c.pts, start + lane_id());
-    process(c, start, cnt, p);
+    if (lane_id() < kLeafSize) p = ldg4(c.pts, leaf * kLeafSize + lane_id());
+    stage_points<KnnVisitor>(L, p);
+    process(L, leaf * kLeafSize);
   }
 };
 
 // Seed a kNN visitor with the leaves [s0, s1] and then run the full traversal.
 template <int KCAP, bool EXACT>
-__device__ __forceinline__ void knn_search(const CloudDev& c, KnnVisitor<KCAP, EXACT>& vis, int s0, int s1) {
+__device__ __forceinline__ void knn_search(const CloudDev& c, KnnVisitor<KCAP, EXACT>& vis, int s0, int s1,
+                                           WaveLds* L) {
   s0 = max(s0, 0);
   s1 = min(s1, c.cnt0 - 1);
-  for (int l = s0; l <= s1; ++l) vis.scan_leaf(c, l);
+  for (int l = s0; l <= s1; ++l) vis.scan_leaf(c, l, L);
   vis.skip_lo = s0;
   vis.skip_hi = s1;
   vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.wd);
-  traverse(c, vis);
+  traverse(c, vis, L);
 }
 
 // kNN-k of the cloud's own points: seed with the group's own leaves, then a
 // split search (keys = the cloud's sorted Morton keys)
 template <int KCAP, bool EXACT>
 __device__ __forceinline__ void knn_self_search(const CloudDev& c, KnnVisitor<KCAP, EXACT>& vis, int s0, int s1,
-                                                unsigned long long key) {
+                                                unsigned long long key, WaveLds* L) {
   s0 = max(s0, 0);
   s1 = min(s1, c.cnt0 - 1);
-  for (int l = s0; l <= s1; ++l) vis.scan_leaf(c, l);
+  for (int l = s0; l <= s1; ++l) vis.scan_leaf(c, l, L);
   vis.skip_lo = s0;
   vis.skip_hi = s1;
-  split_search(c, vis, key);
+  split_search(c, vis, key, L);
 }
 
 // covariances of a cloud: wave w handles sorted points [64w, 64w+64) (leaves 2w, 2w+1)
 template <int KCAP, bool EXACT>
 __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int method, double* __restrict__ cov6) {
+  __shared__ WaveLds lds[4];
+  WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
   const int ngroups = (c.n + 63) >> 6;
@@ -381,7 +390,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
     vis.qx = q.x;
     vis.qy = q.y;
     vis.qz = q.z;
-    knn_self_search(c, vis, 2 * g - 1, 2 * g + 2, gp(c.keys)[min(i, c.n - 1)]);
+    knn_self_search(c, vis, 2 * g - 1, 2 * g + 2, gp(c.keys)[min(i, c.n - 1)], L);
     if (!vis.active) continue;
     // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
     double mx = 0, my = 0, mz = 0;
@@ -420,6 +429,8 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
 template <int KCAP, bool EXACT>
 __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __restrict__ q, int nq, int k,
                                                    int* __restrict__ out_idx, float* __restrict__ out_d) {
+  __shared__ WaveLds lds[4];
+  WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
   const int ngroups = (nq + 63) >> 6;
@@ -436,7 +447,7 @@ __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __r
     const float sx = uniform_f(p.x), sy = uniform_f(p.y), sz = uniform_f(p.z);
     const int pos = wave_lower_bound(c.keys, c.n, morton_key(sx, sy, sz, c.quant));
     const int leaf = min(pos, c.n - 1) / kLeafSize;
-    knn_search(c, vis, leaf - 1, leaf + 1);
+    knn_search(c, vis, leaf - 1, leaf + 1, L);
     if (!vis.active) continue;
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
@@ -670,6 +681,8 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
   const int lane = lane_id();
   const int wib = threadIdx.x >> 6;
   const int wave = blockIdx.x * kLinWaves + wib;
+  __shared__ WaveLds lds[kLinWaves];
+  WaveLds* L = &lds[wib];
   const int nwaves_total = gridDim.x * kLinWaves;
   const int ngroups = (src.n + 63) >> 6;
 
@@ -687,6 +700,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
     // pose when there is one (tight), else an optimistic radius kOptR.
     // Pass 2 (exact completion): lanes whose pass-1 radius was clipped to
     // kOptR and found nothing search again with the full max_corr bound.
+    const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const float opt2 = fminf(cap2, kOptR2);
     NN1Visitor vis;
     vis.qx = qx;
@@ -713,7 +727,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
     if (!(opt2 < cap2)) clipped = false;
     const unsigned long long skey = gp(src.keys)[active ? i : src.n - 1];
     const float ext0 = box_extent(make_wave_box(active, qx, qy, qz, vis.best));
-    split_search(tgt, vis, skey);
+    split_search(tgt, vis, skey, L);
     const bool again = clipped && vis.bestj < 0;
     if (__any(again)) {
       NN1Visitor v2;
@@ -725,7 +739,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       v2.bestj = -1;
       v2.skip_lo = 1;
       v2.skip_hi = 0;
-      split_search(tgt, v2, skey);
+      split_search(tgt, v2, skey, L);
       if (again) {
         vis.best = v2.best;
         vis.bestj = v2.bestj;
@@ -736,14 +750,14 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       vis.st_scan += v2.st_scan;
       vis.st_splits += v2.st_splits;
     }
+    const unsigned long long tm1 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     if (stats && lane == 0) {
       unsigned int* o = stats + (size_t)g * kStatFields;
       o[0] = vis.st_blocks;
       o[1] = vis.st_box;
       o[2] = vis.st_exact;
       o[3] = vis.st_scan;
-      o[4] = __float_as_uint(ext0);
-      o[5] = (unsigned)__popcll(__ballot(active && vis.bestj < 0));
+      o[4] = (unsigned)(tm1 - tm0);
       o[6] = (unsigned)__popcll(__ballot(again)) | (vis.st_splits << 16);
       o[7] = 1;
     }
@@ -802,6 +816,10 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
     acc0 += final_pair(treduce<5, 0>(C));
     acc1 += final_pair(treduce<5, 1>(C));
     acc2 += final_pair(treduce<5, 2>(C));
+    if (stats && lane == 0) {
+      const unsigned long long tm2 = __builtin_amdgcn_s_memtime();
+      stats[(size_t)g * kStatFields + 5] = (unsigned)(tm2 - tm1);
+    }
   }
 
   __shared__ double red[kLinWaves][kMomentSlots];
@@ -1167,6 +1185,8 @@ __global__ __launch_bounds__(256) void k_residuals(const AlignJob* __restrict__ 
   float Rf[9], tf[3];
   for (int e = 0; e < 9; ++e) Rf[e] = (float)st->last_lin_R[e];
   for (int e = 0; e < 3; ++e) tf[e] = (float)st->last_lin_t[e];
+  __shared__ WaveLds lds[4];
+  WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
   const int ngroups = (src.n + 63) >> 6;
@@ -1202,7 +1222,7 @@ __global__ __launch_bounds__(256) void k_residuals(const AlignJob* __restrict__ 
       vis.skip_lo = 1;
       vis.skip_hi = 0;
       vis.box = make_wave_box(need, vis.qx, vis.qy, vis.qz, vis.best);
-      traverse(tgt, vis);
+      traverse(tgt, vis, L);
       if (need) {
         d2 = vis.best;
         job->sqd[i] = d2;
@@ -1259,8 +1279,8 @@ void launch_bbox_final(hipStream_t s, const float* partial, int nparts, float* q
 void launch_morton(hipStream_t s, const float4* pts, int n, const float* quant, unsigned long long* keys, int* vals) {
   k_morton<<<cdiv(n, 256), 256, 0, s>>>(pts, n, quant, keys, vals);
 }
-void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, float4* sorted, int* inv_perm) {
-  k_gather<<<cdiv(n, 256), 256, 0, s>>>(raw, perm, n, sorted, inv_perm);
+void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, int npad, float4* sorted, int* inv_perm) {
+  k_gather<<<cdiv(npad, 256), 256, 0, s>>>(raw, perm, n, npad, sorted, inv_perm);
 }
 void launch_leaf_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float4* lo, float4* hi) {
   k_leaf_boxes<<<cdiv(nleaves, 8), 256, 0, s>>>(pts, n, nleaves, lo, hi);

@@ -55,15 +55,17 @@ __device__ __forceinline__ float uniform_f(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 
+// wave-wide min/max; the result is uniform but deliberately left in a VGPR
+// (SGPRs are the scarce resource in the traversal kernels)
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = fminf(v, __shfl_xor(v, m));
-  return uniform_f(v);
+  return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
-  return uniform_f(v);
+  return v;
 }
 
 // squared distance, nanoflann L2_Simple_Adaptor order (no contraction)
@@ -137,7 +139,7 @@ __device__ __forceinline__ int wave_lower_bound_lane(const unsigned long long* k
 // ---------------------------------------------------------------------------
 // Wave box: union over active lanes of the AABB of each lane's search ball.
 struct WaveBox {
-  float lx, ly, lz, hx, hy, hz;  // uniform
+  float lx, ly, lz, hx, hy, hz;  // uniform values held in VGPRs
 };
 
 __device__ __forceinline__ float ball_radius(float bound2) {
@@ -164,29 +166,55 @@ __device__ __forceinline__ bool box_overlap(const WaveBox& w, float4 lo, float4 
 }
 
 // ---------------------------------------------------------------------------
+// Per-wavefront LDS slice used by the leaf machinery.  Boxes of the current
+// leaf block and the points of the leaf being scanned are broadcast to all
+// lanes with ds_read_b128 (every lane reads the same address: conflict-free),
+// which keeps the uniform data in VGPRs instead of SGPRs.
+struct WaveLds {
+  f4v blo[kFanout];          // leaf-block boxes
+  f4v bhi[kFanout];
+  float px[kLeafSize];       // current leaf, SoA
+  float py[kLeafSize];
+  float pz[kLeafSize];
+};
+constexpr int kWaveLdsBytes = sizeof(WaveLds);
+
+// ---------------------------------------------------------------------------
 // Generic cooperative traversal.  Visitor V provides:
-//   WaveBox box;                                  current wave box (uniform)
+//   WaveBox box;                                  current wave box (VGPR-uniform)
 //   bool need(float4 lo, float4 hi)               per-lane exact leaf test
-//   void process(const CloudDev&, int start, int cnt, float4 p)
-//                                                 scan one leaf whose points
-//                                                 lanes 0..cnt-1 hold in p
+//   void process(const WaveLds*, int start)       scan the 32 staged points
 //   float bound()                                 per-lane squared bound
 //   bool active; float qx, qy, qz; int skip_lo, skip_hi;
 //
 // Leaves are handled a block at a time (the <= 64 children of one level-1
-// node): lane c holds leaf c's box, the wave-box filter and then the EXACT
-// per-lane filter run on registers only (boxes broadcast with readlane), and
-// the surviving leaves are scanned with the next leaf's points prefetched, so
-// a wavefront keeps one global load in flight instead of a dependent chain.
+// node): lane c loads leaf c's box into LDS, the wave-box filter and then the
+// EXACT per-lane filter run on the staged boxes, and the surviving leaves are
+// scanned with the next leaf's points prefetched into registers, so a
+// wavefront keeps one global load in flight instead of a dependent chain.
+// Clouds are padded to a multiple of 32 with far sentinel points, so a scan
+// never needs a per-point bound check.
 template <class V>
-__device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt, V& vis) {
+__device__ __forceinline__ void stage_points(WaveLds* L, float4 p) {
   const int lane = lane_id();
-  float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
-  if (lane < cnt) {
-    lo = ldg4(c.box_lo, base + lane);
-    hi = ldg4(c.box_hi, base + lane);
+  if (lane < kLeafSize) {
+    L->px[lane] = p.x;
+    L->py[lane] = p.y;
+    L->pz[lane] = p.z;
   }
-  const bool ov = lane < cnt && box_overlap(vis.box, lo, hi) && !(base + lane >= vis.skip_lo && base + lane <= vis.skip_hi);
+}
+
+template <class V>
+__device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt, V& vis, WaveLds* L) {
+  const int lane = lane_id();
+  bool ov = false;
+  if (lane < cnt) {
+    const float4 lo = ldg4(c.box_lo, base + lane);
+    const float4 hi = ldg4(c.box_hi, base + lane);
+    L->blo[lane] = f4v{lo.x, lo.y, lo.z, 0.f};
+    L->bhi[lane] = f4v{hi.x, hi.y, hi.z, 0.f};
+    ov = box_overlap(vis.box, lo, hi) && !(base + lane >= vis.skip_lo && base + lane <= vis.skip_hi);
+  }
   unsigned long long mask = __ballot(ov);
   vis.st_blocks += 1;
   vis.st_box += __popcll(mask);
@@ -194,50 +222,45 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
   while (mask) {
     const int b = __builtin_ctzll(mask);
     mask &= mask - 1;
-    const float4 blo = make_float4(readlane_f(lo.x, b), readlane_f(lo.y, b), readlane_f(lo.z, b), 0.f);
-    const float4 bhi = make_float4(readlane_f(hi.x, b), readlane_f(hi.y, b), readlane_f(hi.z, b), 0.f);
-    if (__any(vis.active && vis.need(blo, bhi))) ex |= 1ull << b;
+    const f4v blo = L->blo[b], bhi = L->bhi[b];
+    if (__any(vis.active && vis.need(make_float4(blo.x, blo.y, blo.z, 0.f), make_float4(bhi.x, bhi.y, bhi.z, 0.f))))
+      ex |= 1ull << b;
   }
   vis.st_exact += __popcll(ex);
   if (!ex) return;
-  int cur = __builtin_ctzll(ex);
+  // Rotated software pipeline: at the top of each step the only load in flight
+  // is the one being consumed (so its wait is exact), the next leaf's load is
+  // issued before the scan, and the scan works on registers/LDS only.
+  int nxt = __builtin_ctzll(ex);
   ex &= ex - 1;
-  int start = (base + cur) * kLeafSize;
-  int n_in = min(kLeafSize, c.n - start);
-  float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (lane < n_in) p = ldg4(c.pts, start + lane);
+  float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lane < kLeafSize) pn = ldg4(c.pts, (base + nxt) * kLeafSize + lane);
   bool improved = false;
-  for (;;) {
-    int nxt = -1, nstart = 0, nn = 0;
-    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
+  while (nxt >= 0) {
+    const int cur = nxt;
+    const float4 p = pn;
+    nxt = -1;
     if (ex) {
       nxt = __builtin_ctzll(ex);
       ex &= ex - 1;
-      nstart = (base + nxt) * kLeafSize;
-      nn = min(kLeafSize, c.n - nstart);
-      if (lane < nn) pn = ldg4(c.pts, nstart + lane);
+      if (lane < kLeafSize) pn = ldg4(c.pts, (base + nxt) * kLeafSize + lane);
     }
     // re-check with the bounds tightened by the leaves scanned so far
-    const float4 blo = make_float4(readlane_f(lo.x, cur), readlane_f(lo.y, cur), readlane_f(lo.z, cur), 0.f);
-    const float4 bhi = make_float4(readlane_f(hi.x, cur), readlane_f(hi.y, cur), readlane_f(hi.z, cur), 0.f);
-    if (__any(vis.active && vis.need(blo, bhi))) {
+    const f4v blo = L->blo[cur], bhi = L->bhi[cur];
+    if (__any(vis.active && vis.need(make_float4(blo.x, blo.y, blo.z, 0.f), make_float4(bhi.x, bhi.y, bhi.z, 0.f)))) {
       const float before = vis.bound();
       vis.st_scan += 1;
-      vis.process(c, start, n_in, p);
+      stage_points<V>(L, p);
+      vis.process(L, (base + cur) * kLeafSize);
       improved |= __any(vis.bound() < before);
     }
-    if (nxt < 0) break;
-    cur = nxt;
-    start = nstart;
-    n_in = nn;
-    p = pn;
   }
   if (improved) vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
 }
 
 template <int LV, class V>
-__device__ __forceinline__ void trav_level(const CloudDev& c, int base, unsigned long long mask, V& vis) {
-  // LV >= 2: mask selects nodes of level LV; their children are at LV-1
+__device__ __forceinline__ void trav_level(const CloudDev& c, int base, unsigned long long mask, V& vis, WaveLds* L) {
+  // mask selects nodes of level LV (>= 1); their children are at LV-1
   while (mask) {
     const int ci = __builtin_ctzll(mask);
     mask &= mask - 1;
@@ -245,7 +268,7 @@ __device__ __forceinline__ void trav_level(const CloudDev& c, int base, unsigned
     const int cb = node * kFanout;
     const int cnt = min(kFanout, lvl_cnt(c, LV - 1) - cb);
     if constexpr (LV == 1) {
-      leaf_block(c, cb, cnt, vis);
+      leaf_block(c, cb, cnt, vis, L);
     } else {
       const int lane = lane_id();
       bool ov = false;
@@ -253,32 +276,36 @@ __device__ __forceinline__ void trav_level(const CloudDev& c, int base, unsigned
         const int o = lvl_off(c, LV - 1) + cb + lane;
         ov = box_overlap(vis.box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
       }
-      trav_level<LV - 1>(c, cb, __ballot(ov), vis);
+      trav_level<LV - 1>(c, cb, __ballot(ov), vis, L);
     }
   }
 }
 
 template <class V>
-__device__ __forceinline__ void traverse(const CloudDev& c, V& vis) {
+__device__ __forceinline__ void traverse(const CloudDev& c, V& vis, WaveLds* L) {
   const int T = c.nlevels - 1;
   if (T == 0) {  // the leaves are the top level
-    leaf_block(c, 0, c.cnt0, vis);
+    leaf_block(c, 0, c.cnt0, vis, L);
     return;
   }
   const int lane = lane_id();
   bool ov = false;
   if (lane < lvl_cnt(c, T)) {
     const int o = lvl_off(c, T) + lane;
-    ov = box_overlap(vis.box, c.box_lo[o], c.box_hi[o]);
+    ov = box_overlap(vis.box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
   }
   const unsigned long long m = __ballot(ov);
   switch (T) {
-    case 1: trav_level<1>(c, 0, m, vis); break;
-    case 2: trav_level<2>(c, 0, m, vis); break;
-    case 3: trav_level<3>(c, 0, m, vis); break;
-    default: trav_level<4>(c, 0, m, vis); break;
+    case 1: trav_level<1>(c, 0, m, vis, L); break;
+    case 2: trav_level<2>(c, 0, m, vis, L); break;
+    case 3: trav_level<3>(c, 0, m, vis, L); break;
+    default: trav_level<4>(c, 0, m, vis, L); break;
   }
 }
+
+struct VisitStats {
+  unsigned st_blocks = 0, st_box = 0, st_exact = 0, st_scan = 0, st_splits = 0;
+};
 
 // ---------------------------------------------------------------------------
 // Compact sub-groups.  A wavefront's 64 queries are consecutive in Morton
@@ -305,11 +332,11 @@ __device__ __forceinline__ int morton_jump_split(unsigned long long key, int lo,
 }
 
 template <class V>
-__device__ __forceinline__ void search_range(const CloudDev& c, V& vis, bool base_active, int lo, int hi) {
+__device__ __forceinline__ void search_range(const CloudDev& c, V& vis, bool base_active, int lo, int hi, WaveLds* L) {
   const int lane = lane_id();
   vis.active = base_active && lane >= lo && lane < hi;
   vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
-  traverse(c, vis);
+  traverse(c, vis, L);
 }
 
 __device__ __forceinline__ float box_extent(const WaveBox& b) {
@@ -317,12 +344,12 @@ __device__ __forceinline__ float box_extent(const WaveBox& b) {
 }
 
 template <class V>
-__device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned long long key) {
+__device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned long long key, WaveLds* L) {
   const bool base_active = vis.active;
   const WaveBox whole = make_wave_box(base_active, vis.qx, vis.qy, vis.qz, vis.bound());
   if (!(box_extent(whole) > kSplitExtent)) {
     vis.box = whole;
-    traverse(c, vis);
+    traverse(c, vis, L);
     return;
   }
   vis.st_splits += 1;
@@ -338,12 +365,12 @@ __device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned
     if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
       vis.st_splits += 1;
       const int s2 = morton_jump_split(key, lo, hi);
-      search_range(c, vis, base_active, lo, s2);
-      search_range(c, vis, base_active, s2, hi);
+      search_range(c, vis, base_active, lo, s2, L);
+      search_range(c, vis, base_active, s2, hi, L);
     } else if (__any(act)) {
       vis.active = act;
       vis.box = hb;
-      traverse(c, vis);
+      traverse(c, vis, L);
     }
   }
   vis.active = base_active;
@@ -351,9 +378,15 @@ __device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned
 
 // ---------------------------------------------------------------------------
 // 1-NN visitor: per-lane (best, bestj); bound == best.
-struct VisitStats {
-  unsigned st_blocks = 0, st_box = 0, st_exact = 0, st_scan = 0, st_splits = 0;
-};
+
+// (squared distance, sorted position) as one order-preserving 64-bit key:
+// non-negative fp32 bit patterns sort like their values, so the exact
+// lexicographic rule (d < b) || (d == b && j < bj) is one u64 compare.
+__device__ __forceinline__ unsigned long long dkey(float d, int j) {
+  return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)j;
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 struct NN1Visitor : VisitStats {
   WaveBox box;
@@ -366,32 +399,41 @@ struct NN1Visitor : VisitStats {
   __device__ __forceinline__ float bound() const { return best; }
   __device__ __forceinline__ bool need(float4 lo, float4 hi) const { return box_dist2(qx, qy, qz, lo, hi) <= best; }
 
-  __device__ __forceinline__ void process(const CloudDev& c, int start, int cnt, float4 p) {
-    float b = best;
-    int bj = bestj;
+  __device__ __forceinline__ void process(const WaveLds* L, int start) {
+    unsigned long long bk = dkey(best, bestj);
+    const f4v* X = reinterpret_cast<const f4v*>(L->px);
+    const f4v* Y = reinterpret_cast<const f4v*>(L->py);
+    const f4v* Z = reinterpret_cast<const f4v*>(L->pz);
+    const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
 #pragma unroll
-    for (int j = 0; j < kLeafSize; ++j) {
-      if (j < cnt) {
-        const float d = dist2(qx, qy, qz, readlane_f(p.x, j), readlane_f(p.y, j), readlane_f(p.z, j));
-        const int pj = start + j;
-        const bool take = (d < b) || (d == b && (unsigned)pj < (unsigned)bj);
-        b = take ? d : b;
-        bj = take ? pj : bj;
+    for (int g = 0; g < kLeafSize / 4; ++g) {
+      const f4v x = X[g], y = Y[g], z = Z[g];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // two points at once (v_pk_* ops), same IEEE ops as dist2()
+        const f2v dx = qx2 - f2v{x[2 * h], x[2 * h + 1]};
+        const f2v dy = qy2 - f2v{y[2 * h], y[2 * h + 1]};
+        const f2v dz = qz2 - f2v{z[2 * h], z[2 * h + 1]};
+        const f2v d = (dx * dx + dy * dy) + dz * dz;
+        const int pj = start + 4 * g + 2 * h;
+        const unsigned long long k0 = dkey(d.x, pj), k1 = dkey(d.y, pj + 1);
+        bk = k0 < bk ? k0 : bk;
+        bk = k1 < bk ? k1 : bk;
       }
     }
     if (active) {
-      best = b;
-      bestj = bj;
+      best = __uint_as_float((unsigned)(bk >> 32));
+      bestj = (int)(unsigned)bk;
     }
   }
 
-  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf) {
-    const int start = leaf * kLeafSize;
-    const int cnt = min(kLeafSize, c.n - start);
+  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane_id() < cnt) p = ldg4(c.pts, start + lane_id());
-    process(c, start, cnt, p);
+    if (lane_id() < kLeafSize) p = ldg4(c.pts, leaf * kLeafSize + lane_id());
+    stage_points<NN1Visitor>(L, p);
+    process(L, leaf * kLeafSize);
   }
 };
+
 
 }  // namespace ddlo
