@@ -287,7 +287,7 @@ class Context:
         if not read:
             self._check(self.L.gicp_debug_stats(self.h, int(enable), None, 0, None))
             return None
-        n = (self.size(SOURCE) + 63) // 64
+        n = self.size(SOURCE)  # upper bound on the number of query groups
         out = np.zeros((n, 8), np.uint32)
         nw = C.c_size_t()
         self._check(self.L.gicp_debug_stats(self.h, int(enable), _ptr(out), out.size, C.byref(nw)))

@@ -279,7 +279,7 @@ gicp_status prepare_align(gicp_ctx* c) {
   HIP_TRY(c->corr.ensure(sizeof(int) * ns));
   HIP_TRY(c->sqd.ensure(sizeof(float) * ns));
   HIP_TRY(c->slab.ensure(sizeof(double) * kSlabStride * linearize_blocks(ns)));
-  if (c->stats_on) HIP_TRY(c->stats.ensure(sizeof(unsigned int) * kStatFields * ((ns + 63) / 64)));
+  if (c->stats_on) HIP_TRY(c->stats.ensure(sizeof(unsigned int) * kStatFields * (ns + 15)));
   return GICP_OK;
 }
 
@@ -290,7 +290,7 @@ gicp_status capture_chunk(gicp_ctx* c, bool with_init, int nblocks, hipGraph_t* 
   HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
   if (with_init) launch_align_init(c->stream, jd);
   for (int i = 0; i < kChunk; ++i) {
-    launch_linearize(c->stream, jd, nblocks);
+    launch_linearize(c->stream, jd, c->src.cloud->n, nblocks);
     launch_lm_step(c->stream, jd);
   }
   // publish {iter, done} to pinned host memory at the end of the chunk
@@ -364,7 +364,7 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
   launch_align_init(c->stream, jd);
   for (int i = 0; i < max_it; ++i) {
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i], c->stream));
-    launch_linearize(c->stream, jd, nblocks);
+    launch_linearize(c->stream, jd, c->src.cloud->n, nblocks);
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i + 1], c->stream));
     launch_lm_step(c->stream, jd);
   }
@@ -729,7 +729,7 @@ gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, doubl
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   const AlignJob* jd = c->job_dev.as<AlignJob>();
   launch_align_init(c->stream, jd);
-  launch_linearize(c->stream, jd, nblocks);
+  launch_linearize(c->stream, jd, c->src.cloud->n, nblocks);
   launch_lm_step(c->stream, jd);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
@@ -783,7 +783,8 @@ gicp_status gicp_debug_stats(gicp_ctx* c, int enable, unsigned int* out, size_t 
   if (!c) return fail(GICP_EINVAL, "null ctx");
   c->stats_on = enable != 0;
   if (out && c->src.cloud && c->stats.p) {
-    const size_t words = std::min(max_words, (size_t)kStatFields * ((c->src.cloud->n + 63) / 64));
+    const int q = search_queries_per_wave();
+    const size_t words = std::min(max_words, (size_t)kStatFields * ((c->src.cloud->n + q - 1) / q));
     HIP_TRY(hipMemcpy(out, c->stats.p, sizeof(unsigned int) * words, hipMemcpyDeviceToHost));
     if (nwords) *nwords = words;
   }

@@ -635,8 +635,9 @@ __device__ __forceinline__ void load_sym6(const __attribute__((address_space(1))
   c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y; c[4] = d.x; c[5] = d.y;
 }
 
-constexpr int kLinWaves = 4;   // waves per linearize block
-constexpr float kOptR2 = 0.25f;  // optimistic first-pass radius^2 (0.5 m)
+constexpr int kLinWaves = 4;      // waves per block (search and moment kernels)
+constexpr float kOptR2 = 0.25f;     // optimistic first-pass radius^2 (0.5 m)
+constexpr int kSearchQ = 16;        // queries per wavefront in the correspondence search
 
 __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
@@ -656,53 +657,48 @@ __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ job) {
+// K3a: exact bounded 1-NN correspondence search, Q queries per wavefront.
+// Pass 1: bound = distance to the previous correspondence at the new pose
+// when there is one (tight), else an optimistic radius kOptR.  Pass 2
+// (exact completion): queries whose pass-1 radius was clipped to kOptR and
+// found nothing search again with the full max_corr bound.  Writes corr/sqd
+// (update_correspondences, nano_gicp_impl.hpp:249-258).
+template <int Q>
+__global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
   const CloudDev src = job->src;
   const CloudDev tgt = job->tgt;
-  const auto src_cov = gp(job->src_cov);
-  const auto tgt_cov = gp(job->tgt_cov);
   const auto corr = gpw(job->corr);
   const auto sqd = gpw(job->sqd);
-  const auto slab = gpw(job->slab);
   unsigned int* const stats = job->stats;
   const float cap2 = job->cap2;
   const double max_corr2 = job->max_corr2;
   const int have_prev = st->have_prev;
-
-  double R[9], t[3];
-  for (int e = 0; e < 9; ++e) R[e] = st->R[e];
-  for (int e = 0; e < 3; ++e) t[e] = st->t[e];
   float Rf[9], tf[3];
-  for (int e = 0; e < 9; ++e) Rf[e] = (float)R[e];
-  for (int e = 0; e < 3; ++e) tf[e] = (float)t[e];
+  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
+  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
 
   const int lane = lane_id();
+  const int qi = lane % Q;
   const int wib = threadIdx.x >> 6;
-  const int wave = blockIdx.x * kLinWaves + wib;
   __shared__ WaveLds lds[kLinWaves];
   WaveLds* L = &lds[wib];
+  const int wave = blockIdx.x * kLinWaves + wib;
   const int nwaves_total = gridDim.x * kLinWaves;
-  const int ngroups = (src.n + 63) >> 6;
-
-  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  const int ngroups = (src.n + Q - 1) / Q;
   for (int g = wave; g < ngroups; g += nwaves_total) {
-    const int i = g * 64 + lane;
+    const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    const int i = g * Q + qi;
     const bool active = i < src.n;
-    const float4 a = ldg4(src.pts, active ? i : src.n - 1);
+    const int ic = active ? i : src.n - 1;
+    const float4 a = ldg4(src.pts, ic);
     // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
-
-    // Pass 1: bound = distance to the previous correspondence at the new
-    // pose when there is one (tight), else an optimistic radius kOptR.
-    // Pass 2 (exact completion): lanes whose pass-1 radius was clipped to
-    // kOptR and found nothing search again with the full max_corr bound.
-    const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const float opt2 = fminf(cap2, kOptR2);
-    NN1Visitor vis;
+    NNVisitor<Q> vis;
     vis.qx = qx;
     vis.qy = qy;
     vis.qz = qz;
@@ -711,7 +707,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
     vis.bestj = -1;
     vis.skip_lo = 1;
     vis.skip_hi = 0;
-    bool clipped = active;   // pass-1 bound below cap2 without a candidate
+    bool clipped = active && opt2 < cap2;
     if (have_prev && active) {
       const int j = corr[i];
       if (j >= 0) {
@@ -724,13 +720,11 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
         }
       }
     }
-    if (!(opt2 < cap2)) clipped = false;
-    const unsigned long long skey = gp(src.keys)[active ? i : src.n - 1];
-    const float ext0 = box_extent(make_wave_box(active, qx, qy, qz, vis.best));
-    split_search(tgt, vis, skey, L);
+    const unsigned long long skey = gp(src.keys)[ic];
+    split_search<NNVisitor<Q>, Q>(tgt, vis, skey, L);
     const bool again = clipped && vis.bestj < 0;
     if (__any(again)) {
-      NN1Visitor v2;
+      NNVisitor<Q> v2;
       v2.qx = qx;
       v2.qy = qy;
       v2.qz = qz;
@@ -739,7 +733,7 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       v2.bestj = -1;
       v2.skip_lo = 1;
       v2.skip_hi = 0;
-      split_search(tgt, v2, skey, L);
+      split_search<NNVisitor<Q>, Q>(tgt, v2, skey, L);
       if (again) {
         vis.best = v2.best;
         vis.bestj = v2.bestj;
@@ -750,27 +744,54 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
       vis.st_scan += v2.st_scan;
       vis.st_splits += v2.st_splits;
     }
-    const unsigned long long tm1 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
+    if (active && lane < Q) {
+      corr[i] = valid ? vis.bestj : -1;
+      sqd[i] = vis.bestj >= 0 ? vis.best : INFINITY;
+    }
     if (stats && lane == 0) {
+      const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
       unsigned int* o = stats + (size_t)g * kStatFields;
       o[0] = vis.st_blocks;
       o[1] = vis.st_box;
       o[2] = vis.st_exact;
       o[3] = vis.st_scan;
       o[4] = (unsigned)(tm1 - tm0);
+      o[5] = 0;
       o[6] = (unsigned)__popcll(__ballot(again)) | (vis.st_splits << 16);
       o[7] = 1;
     }
+  }
+}
 
-    const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
-    if (active) {
-      corr[i] = valid ? vis.bestj : -1;
-      sqd[i] = vis.bestj >= 0 ? vis.best : INFINITY;
-    }
-
+// K3b: Mahalanobis + normal-equation moments of the matched pairs
+// (update_correspondences :265-273 + linearize :292-328), 64 points per
+// wavefront, in-register transpose reduction, one slab row per block.
+__global__ __launch_bounds__(256) void k_moments(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  const CloudDev src = job->src;
+  const CloudDev tgt = job->tgt;
+  const auto src_cov = gp(job->src_cov);
+  const auto tgt_cov = gp(job->tgt_cov);
+  const auto corr = gp((const int*)job->corr);
+  const auto slab = gpw(job->slab);
+  double R[9], t[3];
+  for (int e = 0; e < 9; ++e) R[e] = st->R[e];
+  for (int e = 0; e < 3; ++e) t[e] = st->t[e];
+  const int lane = lane_id();
+  const int wib = threadIdx.x >> 6;
+  const int wave = blockIdx.x * kLinWaves + wib;
+  const int nwaves_total = gridDim.x * kLinWaves;
+  const int ngroups = (src.n + 63) >> 6;
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  for (int g = wave; g < ngroups; g += nwaves_total) {
+    const int i = g * 64 + lane;
+    const bool active = i < src.n;
+    const int j = active ? corr[i] : -1;
     Contrib C;
-    if (valid) {
-      const int j = vis.bestj;
+    if (j >= 0) {
+      const float4 a = ldg4(src.pts, i);
       const float4 b = ldg4(tgt.pts, j);
       double ca[6], cb[6];
       load_sym6(src_cov + 6 * (size_t)i, ca);
@@ -812,16 +833,10 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
     }
     C.qq[0] = C.q[0] * C.q[0]; C.qq[1] = C.q[0] * C.q[1]; C.qq[2] = C.q[0] * C.q[2];
     C.qq[3] = C.q[1] * C.q[1]; C.qq[4] = C.q[1] * C.q[2]; C.qq[5] = C.q[2] * C.q[2];
-
     acc0 += final_pair(treduce<5, 0>(C));
     acc1 += final_pair(treduce<5, 1>(C));
     acc2 += final_pair(treduce<5, 2>(C));
-    if (stats && lane == 0) {
-      const unsigned long long tm2 = __builtin_amdgcn_s_memtime();
-      stats[(size_t)g * kStatFields + 5] = (unsigned)(tm2 - tm1);
-    }
   }
-
   __shared__ double red[kLinWaves][kMomentSlots];
   if ((lane & 1) == 0) {
     const int base = moment_base(lane);
@@ -831,10 +846,10 @@ __global__ __launch_bounds__(256) void k_linearize(const AlignJob* __restrict__ 
   }
   __syncthreads();
   if (threadIdx.x < kSlabStride) {
-    double s = 0.0;
+    double sum = 0.0;
     if (threadIdx.x < kMoments)
-      for (int w = 0; w < kLinWaves; ++w) s += red[w][threadIdx.x];
-    slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = s;
+      for (int w = 0; w < kLinWaves; ++w) sum += red[w][threadIdx.x];
+    slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = sum;
   }
 }
 
@@ -1317,9 +1332,13 @@ void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, con
   k_cov_export<<<cdiv(n, 256), 256, 0, s>>>(cov6, layout, n, perm, out);
 }
 void launch_align_init(hipStream_t s, const AlignJob* job) { k_align_init<<<1, 64, 0, s>>>(job); }
-void launch_linearize(hipStream_t s, const AlignJob* job, int nblocks) {
-  k_linearize<<<nblocks, 64 * kLinWaves, 0, s>>>(job);
+void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks) {
+  const int search_groups = (nsrc + kSearchQ - 1) / kSearchQ;
+  const int sb = std::max(1, std::min((search_groups + kLinWaves - 1) / kLinWaves, 8192));
+  k_nn_search<kSearchQ><<<sb, 64 * kLinWaves, 0, s>>>(job);
+  k_moments<<<nblocks, 64 * kLinWaves, 0, s>>>(job);
 }
+int search_queries_per_wave() { return kSearchQ; }
 void launch_lm_step(hipStream_t s, const AlignJob* job) { k_lm_step<<<1, kLmThreads, 0, s>>>(job); }
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out) {
   k_residuals<<<group_blocks(nsrc), 256, 0, s>>>(job, out);

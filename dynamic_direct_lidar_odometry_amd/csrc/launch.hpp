@@ -21,7 +21,8 @@ bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq,
 void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6);
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);
 void launch_align_init(hipStream_t s, const AlignJob* job);
-void launch_linearize(hipStream_t s, const AlignJob* job, int nblocks);
+void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks);
+int search_queries_per_wave();
 void launch_lm_step(hipStream_t s, const AlignJob* job);
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out);
 void launch_transform(hipStream_t s, const float4* pts, int n, const int* perm, const float* T16, float* out,

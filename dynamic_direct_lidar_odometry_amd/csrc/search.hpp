@@ -318,12 +318,14 @@ struct VisitStats {
 // query cloud's own quantisation (rigid transforms keep the geometry).
 constexpr float kSplitExtent = 3.0f;
 
+template <int Q = 64>
 __device__ __forceinline__ int morton_jump_split(unsigned long long key, int lo, int hi) {
-  // lane with the largest (key ^ previous key) in (lo, hi); returns split lane
+  // query index (lane % Q) with the largest (key ^ previous key) in (lo, hi)
   const int lane = lane_id();
+  const int qi = lane % Q;
   const unsigned long long prev = __shfl_up(key, 1);
   int score = -1;
-  if (lane > lo && lane < hi) score = (64 - __clzll(key ^ prev)) * 64 + lane;
+  if (lane < Q && qi > lo && qi < hi) score = (64 - __clzll(key ^ prev)) * 64 + qi;
   int best = score;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) best = max(best, __shfl_xor(best, m));
@@ -331,10 +333,10 @@ __device__ __forceinline__ int morton_jump_split(unsigned long long key, int lo,
   return best < 0 ? (lo + hi) / 2 : (best & 63);
 }
 
-template <class V>
+template <int Q, class V>
 __device__ __forceinline__ void search_range(const CloudDev& c, V& vis, bool base_active, int lo, int hi, WaveLds* L) {
-  const int lane = lane_id();
-  vis.active = base_active && lane >= lo && lane < hi;
+  const int qi = lane_id() % Q;
+  vis.active = base_active && qi >= lo && qi < hi;
   vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
   traverse(c, vis, L);
 }
@@ -343,7 +345,7 @@ __device__ __forceinline__ float box_extent(const WaveBox& b) {
   return fmaxf(fmaxf(b.hx - b.lx, b.hy - b.ly), b.hz - b.lz);
 }
 
-template <class V>
+template <class V, int Q = 64>
 __device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned long long key, WaveLds* L) {
   const bool base_active = vis.active;
   const WaveBox whole = make_wave_box(base_active, vis.qx, vis.qy, vis.qz, vis.bound());
@@ -353,20 +355,19 @@ __device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned
     return;
   }
   vis.st_splits += 1;
-  const int s = morton_jump_split(key, 0, 64);
-  // each half: split once more if still extended
+  const int s = morton_jump_split<Q>(key, 0, Q);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int lo = h == 0 ? 0 : s, hi = h == 0 ? s : 64;
+    const int lo = h == 0 ? 0 : s, hi = h == 0 ? s : Q;
     if (lo >= hi) continue;
-    const int lane = lane_id();
-    const bool act = base_active && lane >= lo && lane < hi;
+    const int qi = lane_id() % Q;
+    const bool act = base_active && qi >= lo && qi < hi;
     const WaveBox hb = make_wave_box(act, vis.qx, vis.qy, vis.qz, vis.bound());
     if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
       vis.st_splits += 1;
-      const int s2 = morton_jump_split(key, lo, hi);
-      search_range(c, vis, base_active, lo, s2, L);
-      search_range(c, vis, base_active, s2, hi, L);
+      const int s2 = morton_jump_split<Q>(key, lo, hi);
+      search_range<Q>(c, vis, base_active, lo, s2, L);
+      search_range<Q>(c, vis, base_active, s2, hi, L);
     } else if (__any(act)) {
       vis.active = act;
       vis.box = hb;
@@ -375,9 +376,6 @@ __device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned
   }
   vis.active = base_active;
 }
-
-// ---------------------------------------------------------------------------
-// 1-NN visitor: per-lane (best, bestj); bound == best.
 
 // (squared distance, sorted position) as one order-preserving 64-bit key:
 // non-negative fp32 bit patterns sort like their values, so the exact
@@ -388,7 +386,14 @@ __device__ __forceinline__ unsigned long long dkey(float d, int j) {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-struct NN1Visitor : VisitStats {
+// 1-NN visitor for Q queries per wavefront: lane = (query lane % Q, slice
+// lane / Q); each of the S = 64/Q slices scans 32/S of a leaf's points and
+// the per-query partial minima are merged after every leaf, so every lane of
+// a query always holds the query's exact running (best, bestj).
+template <int Q>
+struct NNVisitor : VisitStats {
+  static constexpr int S = 64 / Q;
+  static constexpr int P = kLeafSize / S;   // points per lane per leaf
   WaveBox box;
   float qx, qy, qz;
   float best;   // squared distance bound (strict <, ties by position)
@@ -401,12 +406,13 @@ struct NN1Visitor : VisitStats {
 
   __device__ __forceinline__ void process(const WaveLds* L, int start) {
     unsigned long long bk = dkey(best, bestj);
-    const f4v* X = reinterpret_cast<const f4v*>(L->px);
-    const f4v* Y = reinterpret_cast<const f4v*>(L->py);
-    const f4v* Z = reinterpret_cast<const f4v*>(L->pz);
+    const int off = (lane_id() / Q) * P;
+    const f4v* X = reinterpret_cast<const f4v*>(L->px + off);
+    const f4v* Y = reinterpret_cast<const f4v*>(L->py + off);
+    const f4v* Z = reinterpret_cast<const f4v*>(L->pz + off);
     const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
 #pragma unroll
-    for (int g = 0; g < kLeafSize / 4; ++g) {
+    for (int g = 0; g < P / 4; ++g) {
       const f4v x = X[g], y = Y[g], z = Z[g];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -415,11 +421,16 @@ struct NN1Visitor : VisitStats {
         const f2v dy = qy2 - f2v{y[2 * h], y[2 * h + 1]};
         const f2v dz = qz2 - f2v{z[2 * h], z[2 * h + 1]};
         const f2v d = (dx * dx + dy * dy) + dz * dz;
-        const int pj = start + 4 * g + 2 * h;
+        const int pj = start + off + 4 * g + 2 * h;
         const unsigned long long k0 = dkey(d.x, pj), k1 = dkey(d.y, pj + 1);
         bk = k0 < bk ? k0 : bk;
         bk = k1 < bk ? k1 : bk;
       }
+    }
+#pragma unroll
+    for (int m = Q; m < 64; m <<= 1) {
+      const unsigned long long o = __shfl_xor(bk, m);
+      bk = o < bk ? o : bk;
     }
     if (active) {
       best = __uint_as_float((unsigned)(bk >> 32));
@@ -430,10 +441,11 @@ struct NN1Visitor : VisitStats {
   __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
     if (lane_id() < kLeafSize) p = ldg4(c.pts, leaf * kLeafSize + lane_id());
-    stage_points<NN1Visitor>(L, p);
+    stage_points<NNVisitor>(L, p);
     process(L, leaf * kLeafSize);
   }
 };
+using NN1Visitor = NNVisitor<64>;
 
 
 }  // namespace ddlo
