@@ -258,10 +258,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   return GICP_OK;
 }
 
-int linearize_blocks(int nsrc) {
-  const int groups = (nsrc + 63) / 64;
-  return std::max(1, std::min((groups + 3) / 4, 1024));
-}
+int linearize_blocks(int nsrc) { return moment_blocks(nsrc); }
 
 gicp_status prepare_align(gicp_ctx* c) {
   if (!c->src.cloud) return fail(GICP_ENOSOURCE, "no source cloud");

@@ -64,12 +64,29 @@ __global__ __launch_bounds__(256) void k_pack_bbox(const unsigned char* __restri
 
 __global__ __launch_bounds__(256) void k_bbox_final(const float* __restrict__ partial, int nparts,
                                                     float* __restrict__ quant) {
-  // one block; thread a reduces component a
+  // one block of 256 threads: strided partial min/max, then wave + LDS reduce
+  __shared__ float red[6][4];
   __shared__ float bb[6];
+  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int k = threadIdx.x; k < nparts; k += blockDim.x) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      v[a] = fminf(v[a], partial[k * 6 + a]);
+      v[a + 3] = fmaxf(v[a + 3], partial[k * 6 + a + 3]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    v[a] = wave_min(v[a]);
+    v[a + 3] = wave_max(v[a + 3]);
+  }
+  if (lane_id() == 0)
+    for (int a = 0; a < 6; ++a) red[a][threadIdx.x >> 6] = v[a];
+  __syncthreads();
   if (threadIdx.x < 6) {
     const int a = threadIdx.x;
-    float r = a < 3 ? INFINITY : -INFINITY;
-    for (int k = 0; k < nparts; ++k) r = a < 3 ? fminf(r, partial[k * 6 + a]) : fmaxf(r, partial[k * 6 + a]);
+    float r = red[a][0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = a < 3 ? fminf(r, red[a][w]) : fmaxf(r, red[a][w]);
     bb[a] = r;
   }
   __syncthreads();
@@ -344,6 +361,9 @@ struct KnnVisitor : VisitStats {
     if (lane_id() < kLeafSize) p = ldg4(c.pts, leaf * kLeafSize + lane_id());
     stage_points<KnnVisitor>(L, p);
     process(L, leaf * kLeafSize);
+  }
+  __device__ __forceinline__ bool scan_leaves(const CloudDev& c, int base, unsigned long long ex, WaveLds* L) {
+    return scan_leaves_lds(c, base, ex, *this, L);
   }
 };
 
@@ -697,17 +717,16 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
-    const float opt2 = fminf(cap2, kOptR2);
     NNVisitor<Q> vis;
     vis.qx = qx;
     vis.qy = qy;
     vis.qz = qz;
     vis.active = active;
-    vis.best = active ? opt2 : -1.f;
+    vis.best = active ? cap2 : -1.f;
     vis.bestj = -1;
     vis.skip_lo = 1;
     vis.skip_hi = 0;
-    bool clipped = active && opt2 < cap2;
+    bool seeded = false;
     if (have_prev && active) {
       const int j = corr[i];
       if (j >= 0) {
@@ -716,34 +735,34 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
         if (d < cap2) {
           vis.best = d;
           vis.bestj = j;
-          clipped = false;
+          seeded = true;
         }
       }
     }
+    // Exact seeding for queries without a usable previous correspondence:
+    // the real target points around the query's Morton position give an
+    // upper bound, so the single search below stays exact.
+    const bool need_seed = active && !seeded;
+    bool again = false;
+    if (__any(need_seed)) {
+      const int pos = group_lower_bound<Q>(tgt.keys, tgt.n, morton_key(qx, qy, qz, tgt.quant));
+      const int s = lane / Q;
+      const int cand = min(max(pos - (64 / Q) / 2 + s, 0), tgt.n - 1);
+      const float4 p = ldg4(tgt.pts, cand);
+      const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
+      unsigned long long bk = need_seed ? dkey(d, cand) : dkey(vis.best, vis.bestj);
+      vis.merge_slices(bk);
+      if (need_seed) {
+        const float bd = __uint_as_float((unsigned)(bk >> 32));
+        if (bd < cap2) {
+          vis.best = bd;
+          vis.bestj = (int)(unsigned)bk;
+        }
+      }
+      again = need_seed;
+    }
     const unsigned long long skey = gp(src.keys)[ic];
     split_search<NNVisitor<Q>, Q>(tgt, vis, skey, L);
-    const bool again = clipped && vis.bestj < 0;
-    if (__any(again)) {
-      NNVisitor<Q> v2;
-      v2.qx = qx;
-      v2.qy = qy;
-      v2.qz = qz;
-      v2.active = again;
-      v2.best = again ? cap2 : -1.f;
-      v2.bestj = -1;
-      v2.skip_lo = 1;
-      v2.skip_hi = 0;
-      split_search<NNVisitor<Q>, Q>(tgt, v2, skey, L);
-      if (again) {
-        vis.best = v2.best;
-        vis.bestj = v2.bestj;
-      }
-      vis.st_blocks += v2.st_blocks;
-      vis.st_box += v2.st_box;
-      vis.st_exact += v2.st_exact;
-      vis.st_scan += v2.st_scan;
-      vis.st_splits += v2.st_splits;
-    }
     const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
     if (active && lane < Q) {
       corr[i] = valid ? vis.bestj : -1;
@@ -767,7 +786,9 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
 // K3b: Mahalanobis + normal-equation moments of the matched pairs
 // (update_correspondences :265-273 + linearize :292-328), 64 points per
 // wavefront, in-register transpose reduction, one slab row per block.
-__global__ __launch_bounds__(256) void k_moments(const AlignJob* __restrict__ job) {
+constexpr int kMomWaves = 16;   // waves per moment block (1024 threads)
+
+__global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
   const CloudDev src = job->src;
@@ -781,8 +802,8 @@ __global__ __launch_bounds__(256) void k_moments(const AlignJob* __restrict__ jo
   for (int e = 0; e < 3; ++e) t[e] = st->t[e];
   const int lane = lane_id();
   const int wib = threadIdx.x >> 6;
-  const int wave = blockIdx.x * kLinWaves + wib;
-  const int nwaves_total = gridDim.x * kLinWaves;
+  const int wave = blockIdx.x * kMomWaves + wib;
+  const int nwaves_total = gridDim.x * kMomWaves;
   const int ngroups = (src.n + 63) >> 6;
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   for (int g = wave; g < ngroups; g += nwaves_total) {
@@ -837,7 +858,7 @@ __global__ __launch_bounds__(256) void k_moments(const AlignJob* __restrict__ jo
     acc1 += final_pair(treduce<5, 1>(C));
     acc2 += final_pair(treduce<5, 2>(C));
   }
-  __shared__ double red[kLinWaves][kMomentSlots];
+  __shared__ double red[kMomWaves][kMomentSlots];
   if ((lane & 1) == 0) {
     const int base = moment_base(lane);
     red[wib][base + 0] = acc0;
@@ -848,7 +869,7 @@ __global__ __launch_bounds__(256) void k_moments(const AlignJob* __restrict__ jo
   if (threadIdx.x < kSlabStride) {
     double sum = 0.0;
     if (threadIdx.x < kMoments)
-      for (int w = 0; w < kLinWaves; ++w) sum += red[w][threadIdx.x];
+      for (int w = 0; w < kMomWaves; ++w) sum += red[w][threadIdx.x];
     slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = sum;
   }
 }
@@ -878,53 +899,85 @@ __device__ void so3_exp_d(const double w[3], double R[9]) {  // gicp/so3.hpp:101
   R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
 
-// Eigen::LDLT<Matrix6d>(A).solve(rhs), pivoted (restated, see oracle)
+// Eigen::LDLT<Matrix6d>(A).solve(rhs), pivoted (restated, see oracle).
+// Every array index is a compile-time constant (pivot swaps go through
+// select chains), so the 36 entries stay in registers (no scratch).
 __device__ void ldlt_solve6_d(const double* A_in, const double* rhs, double* x) {
-  const int n = 6;
+  constexpr int n = 6;
   double m[36];
+#pragma unroll
   for (int i = 0; i < 36; ++i) m[i] = A_in[i];
   int tr[6];
-  double temp[6];
+#pragma unroll
   for (int k = 0; k < n; ++k) {
     int big = k;
     double bigv = fabs(m[k * n + k]);
+#pragma unroll
     for (int i = k + 1; i < n; ++i)
       if (fabs(m[i * n + i]) > bigv) { bigv = fabs(m[i * n + i]); big = i; }
     tr[k] = big;
-    if (k != big) {
-      for (int j = 0; j < k; ++j) { double s = m[k * n + j]; m[k * n + j] = m[big * n + j]; m[big * n + j] = s; }
-      for (int i = big + 1; i < n; ++i) { double s = m[i * n + k]; m[i * n + k] = m[i * n + big]; m[i * n + big] = s; }
-      { double s = m[k * n + k]; m[k * n + k] = m[big * n + big]; m[big * n + big] = s; }
-      for (int i = k + 1; i < big; ++i) {
-        double s = m[i * n + k];
-        m[i * n + k] = m[big * n + i];
-        m[big * n + i] = s;
+#pragma unroll
+    for (int r = k + 1; r < n; ++r) {
+      if (big == r) {
+        // swap k <-> r on the lower triangle, as Eigen's ldlt_inplace
+#pragma unroll
+        for (int j = 0; j < k; ++j) { const double t = m[k * n + j]; m[k * n + j] = m[r * n + j]; m[r * n + j] = t; }
+#pragma unroll
+        for (int i = r + 1; i < n; ++i) { const double t = m[i * n + k]; m[i * n + k] = m[i * n + r]; m[i * n + r] = t; }
+        { const double t = m[k * n + k]; m[k * n + k] = m[r * n + r]; m[r * n + r] = t; }
+#pragma unroll
+        for (int i = k + 1; i < r; ++i) { const double t = m[i * n + k]; m[i * n + k] = m[r * n + i]; m[r * n + i] = t; }
       }
     }
+    double temp[6];
     if (k > 0) {
+#pragma unroll
       for (int j = 0; j < k; ++j) temp[j] = m[j * n + j] * m[k * n + j];
       double s = 0;
+#pragma unroll
       for (int j = 0; j < k; ++j) s += m[k * n + j] * temp[j];
       m[k * n + k] -= s;
+#pragma unroll
       for (int i = k + 1; i < n; ++i) {
         double a = 0;
+#pragma unroll
         for (int j = 0; j < k; ++j) a += m[i * n + j] * temp[j];
         m[i * n + k] -= a;
       }
     }
     const double akk = m[k * n + k];
-    if (k < n - 1 && fabs(akk) > 0.0)
+    if (k < n - 1 && fabs(akk) > 0.0) {
+#pragma unroll
       for (int i = k + 1; i < n; ++i) m[i * n + k] /= akk;
+    }
   }
   double y[6];
+#pragma unroll
   for (int i = 0; i < n; ++i) y[i] = rhs[i];
-  for (int k = 0; k < n; ++k) { double s = y[k]; y[k] = y[tr[k]]; y[tr[k]] = s; }
+  // y = P y (transpositions in order)
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+#pragma unroll
+    for (int r = k + 1; r < n; ++r)
+      if (tr[k] == r) { const double t = y[k]; y[k] = y[r]; y[r] = t; }
+  }
+#pragma unroll
   for (int i = 0; i < n; ++i)
+#pragma unroll
     for (int j = 0; j < i; ++j) y[i] -= m[i * n + j] * y[j];
+#pragma unroll
   for (int i = 0; i < n; ++i) y[i] = (fabs(m[i * n + i]) > 2.2250738585072014e-308) ? y[i] / m[i * n + i] : 0.0;
+#pragma unroll
   for (int i = n - 1; i >= 0; --i)
+#pragma unroll
     for (int j = i + 1; j < n; ++j) y[i] -= m[j * n + i] * y[j];
-  for (int k = n - 1; k >= 0; --k) { double s = y[k]; y[k] = y[tr[k]]; y[tr[k]] = s; }
+#pragma unroll
+  for (int k = n - 1; k >= 0; --k) {
+#pragma unroll
+    for (int r = k + 1; r < n; ++r)
+      if (tr[k] == r) { const double t = y[k]; y[k] = y[r]; y[r] = t; }
+  }
+#pragma unroll
   for (int i = 0; i < n; ++i) x[i] = y[i];
 }
 
@@ -1037,6 +1090,8 @@ __device__ void compose(const double Rd[9], const double td[3], const double R[9
 
 constexpr int kLmThreads = 512;
 constexpr int kMaxTrials = 64;
+constexpr int kMomBlocksMax = 128;                      // moment-kernel blocks (slab rows)
+constexpr int kLmRowsPerPart = (kMomBlocksMax + 5) / 6;  // slab rows per reducer thread
 
 // One workgroup: (1) fixed-order reduction of the linearize partials,
 // (2) H and b one entry per thread, (3) every LM trial in its own thread —
@@ -1058,9 +1113,17 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
   const int nb = job->nblocks;
   const auto slab = gp(job->slab);
   if (tid < 6 * kSlabStride) {
+    // issue every load before summing (fixed order => deterministic)
     const int v = tid % kSlabStride, p = tid / kSlabStride;
+    double vals[kLmRowsPerPart];
+#pragma unroll
+    for (int r = 0; r < kLmRowsPerPart; ++r) {
+      const int b = p + 6 * r;
+      vals[r] = b < nb ? slab[(size_t)b * kSlabStride + v] : 0.0;
+    }
     double s = 0.0;
-    for (int b = p; b < nb; b += 6) s += slab[(size_t)b * kSlabStride + v];
+#pragma unroll
+    for (int r = 0; r < kLmRowsPerPart; ++r) s += vals[r];
     part[p][v] = s;
   }
   __syncthreads();
@@ -1289,7 +1352,7 @@ void launch_pack_bbox(hipStream_t s, const unsigned char* raw, size_t stride, in
   k_pack_bbox<<<nblocks, 256, 0, s>>>(raw, stride, n, out, partial, nonfinite);
 }
 void launch_bbox_final(hipStream_t s, const float* partial, int nparts, float* quant) {
-  k_bbox_final<<<1, 64, 0, s>>>(partial, nparts, quant);
+  k_bbox_final<<<1, 256, 0, s>>>(partial, nparts, quant);
 }
 void launch_morton(hipStream_t s, const float4* pts, int n, const float* quant, unsigned long long* keys, int* vals) {
   k_morton<<<cdiv(n, 256), 256, 0, s>>>(pts, n, quant, keys, vals);
@@ -1336,9 +1399,13 @@ void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks)
   const int search_groups = (nsrc + kSearchQ - 1) / kSearchQ;
   const int sb = std::max(1, std::min((search_groups + kLinWaves - 1) / kLinWaves, 8192));
   k_nn_search<kSearchQ><<<sb, 64 * kLinWaves, 0, s>>>(job);
-  k_moments<<<nblocks, 64 * kLinWaves, 0, s>>>(job);
+  k_moments<<<nblocks, 64 * kMomWaves, 0, s>>>(job);
 }
 int search_queries_per_wave() { return kSearchQ; }
+int moment_blocks(int nsrc) {
+  const int groups = (nsrc + 63) / 64;
+  return std::max(1, std::min((groups + kMomWaves - 1) / kMomWaves, kMomBlocksMax));
+}
 void launch_lm_step(hipStream_t s, const AlignJob* job) { k_lm_step<<<1, kLmThreads, 0, s>>>(job); }
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out) {
   k_residuals<<<group_blocks(nsrc), 256, 0, s>>>(job, out);

@@ -23,6 +23,7 @@ void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, con
 void launch_align_init(hipStream_t s, const AlignJob* job);
 void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks);
 int search_queries_per_wave();
+int moment_blocks(int nsrc);  // slab rows written by the moment kernel
 void launch_lm_step(hipStream_t s, const AlignJob* job);
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out);
 void launch_transform(hipStream_t s, const float4* pts, int n, const int* perm, const float* T16, float* out,

@@ -136,6 +136,34 @@ __device__ __forceinline__ int wave_lower_bound_lane(const unsigned long long* k
   return lo;
 }
 
+// Per-query lower_bound for Q-query groups: the S = 64/Q lanes of a query
+// test S pivots per step ((S+1)-ary search), ~log_{S+1}(n) dependent loads.
+template <int Q>
+__device__ __forceinline__ int group_lower_bound(const unsigned long long* keys, int n, unsigned long long key) {
+  constexpr int S = 64 / Q;
+  const int lane = lane_id();
+  const int s = lane / Q, qi = lane % Q;
+  int lo = 0, hi = n;  // answer in [lo, hi]
+  while (__any(hi - lo > 0)) {
+    const int len = hi - lo;
+    // pivots lo + (t+1)*len/(S+1), t = 0..S-1
+    const int piv = lo + (int)(((long long)(s + 1) * len) / (S + 1));
+    const bool less = len > 0 && gp(keys)[min(piv, n - 1)] < key && piv < hi;
+    const unsigned long long bal = __ballot(less);
+    int cnt = 0;
+#pragma unroll
+    for (int t = 0; t < S; ++t) cnt += (int)((bal >> (qi + t * Q)) & 1ull);
+    if (len > 0) {
+      const int nlo = cnt == 0 ? lo : lo + (int)(((long long)cnt * len) / (S + 1)) + 1;
+      const int nhi = cnt == S ? hi : lo + (int)(((long long)(cnt + 1) * len) / (S + 1));
+      lo = nlo;
+      hi = max(nhi, nlo);
+      if (hi - lo <= 0) hi = lo;
+    }
+  }
+  return lo;
+}
+
 // ---------------------------------------------------------------------------
 // Wave box: union over active lanes of the AABB of each lane's search ball.
 struct WaveBox {
@@ -228,9 +256,16 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
   }
   vis.st_exact += __popcll(ex);
   if (!ex) return;
-  // Rotated software pipeline: at the top of each step the only load in flight
-  // is the one being consumed (so its wait is exact), the next leaf's load is
-  // issued before the scan, and the scan works on registers/LDS only.
+  if (vis.scan_leaves(c, base, ex, L)) vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
+}
+
+// Generic LDS-staged, prefetching scan of the leaves in `ex` (bit b = leaf
+// base + b) used by visitors whose process() reads the staged SoA points.
+// Rotated pipeline: at the top of each step the only load in flight is the
+// one being consumed, the next leaf's load is issued before the scan.
+template <class V>
+__device__ __forceinline__ bool scan_leaves_lds(const CloudDev& c, int base, unsigned long long ex, V& vis, WaveLds* L) {
+  const int lane = lane_id();
   int nxt = __builtin_ctzll(ex);
   ex &= ex - 1;
   float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -245,7 +280,6 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
       ex &= ex - 1;
       if (lane < kLeafSize) pn = ldg4(c.pts, (base + nxt) * kLeafSize + lane);
     }
-    // re-check with the bounds tightened by the leaves scanned so far
     const f4v blo = L->blo[cur], bhi = L->bhi[cur];
     if (__any(vis.active && vis.need(make_float4(blo.x, blo.y, blo.z, 0.f), make_float4(bhi.x, bhi.y, bhi.z, 0.f)))) {
       const float before = vis.bound();
@@ -255,7 +289,7 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
       improved |= __any(vis.bound() < before);
     }
   }
-  if (improved) vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
+  return improved;
 }
 
 template <int LV, class V>
@@ -390,6 +424,37 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // lane / Q); each of the S = 64/Q slices scans 32/S of a leaf's points and
 // the per-query partial minima are merged after every leaf, so every lane of
 // a query always holds the query's exact running (best, bestj).
+// u64 min across lanes l and l ^ 32 / l ^ 16 with the gfx950 permlane swaps
+// (register-only; no LDS round trip)
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+template <int M>
+__device__ __forceinline__ unsigned long long xor_min64(unsigned long long v) {
+  const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+  unsigned a0, a1, b0, b1;
+  if constexpr (M == 32) {
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a0 = rl[0]; b0 = rl[1]; a1 = rh[0]; b1 = rh[1];
+  } else if constexpr (M == 16) {
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a0 = rl[0]; b0 = rl[1]; a1 = rh[0]; b1 = rh[1];
+  } else {
+    return umin64(v, __shfl_xor(v, M));
+  }
+  return umin64(((unsigned long long)a1 << 32) | a0, ((unsigned long long)b1 << 32) | b0);
+}
+
+typedef float f3v __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ f3v ldg3(const float4* p, long i) {
+  return ((const __attribute__((address_space(1))) f3v*)(p + i))[0];
+}
+
+// 1-NN visitor for Q queries per wavefront: lane = (query lane % Q, slice
+// lane / Q); each of the S = 64/Q slices loads and scans 32/S of a leaf's
+// points straight into registers (next leaf prefetched), and the per-query
+// partial minima are merged after every leaf with permlane swaps, so every
+// lane of a query always holds the query's exact running (best, bestj).
 template <int Q>
 struct NNVisitor : VisitStats {
   static constexpr int S = 64 / Q;
@@ -404,45 +469,72 @@ struct NNVisitor : VisitStats {
   __device__ __forceinline__ float bound() const { return best; }
   __device__ __forceinline__ bool need(float4 lo, float4 hi) const { return box_dist2(qx, qy, qz, lo, hi) <= best; }
 
-  __device__ __forceinline__ void process(const WaveLds* L, int start) {
+  __device__ __forceinline__ void merge_slices(unsigned long long& bk) const {
+    if constexpr (Q <= 16) bk = xor_min64<16>(bk);
+    if constexpr (Q <= 32) bk = xor_min64<32>(bk);
+    if constexpr (Q < 16) {
+#pragma unroll
+      for (int m = Q; m < 16; m <<= 1) bk = umin64(bk, __shfl_xor(bk, m));
+    }
+  }
+
+  __device__ __forceinline__ void scan_regs(const f3v (&pt)[P], int start) {
     unsigned long long bk = dkey(best, bestj);
     const int off = (lane_id() / Q) * P;
-    const f4v* X = reinterpret_cast<const f4v*>(L->px + off);
-    const f4v* Y = reinterpret_cast<const f4v*>(L->py + off);
-    const f4v* Z = reinterpret_cast<const f4v*>(L->pz + off);
     const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
 #pragma unroll
-    for (int g = 0; g < P / 4; ++g) {
-      const f4v x = X[g], y = Y[g], z = Z[g];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        // two points at once (v_pk_* ops), same IEEE ops as dist2()
-        const f2v dx = qx2 - f2v{x[2 * h], x[2 * h + 1]};
-        const f2v dy = qy2 - f2v{y[2 * h], y[2 * h + 1]};
-        const f2v dz = qz2 - f2v{z[2 * h], z[2 * h + 1]};
-        const f2v d = (dx * dx + dy * dy) + dz * dz;
-        const int pj = start + off + 4 * g + 2 * h;
-        const unsigned long long k0 = dkey(d.x, pj), k1 = dkey(d.y, pj + 1);
-        bk = k0 < bk ? k0 : bk;
-        bk = k1 < bk ? k1 : bk;
-      }
+    for (int h = 0; h < P; h += 2) {
+      // two points at once (v_pk_* ops), same IEEE ops as dist2()
+      const f2v dx = qx2 - f2v{pt[h].x, pt[h + 1].x};
+      const f2v dy = qy2 - f2v{pt[h].y, pt[h + 1].y};
+      const f2v dz = qz2 - f2v{pt[h].z, pt[h + 1].z};
+      const f2v d = (dx * dx + dy * dy) + dz * dz;
+      const int pj = start + off + h;
+      bk = umin64(bk, dkey(d.x, pj));
+      bk = umin64(bk, dkey(d.y, pj + 1));
     }
-#pragma unroll
-    for (int m = Q; m < 64; m <<= 1) {
-      const unsigned long long o = __shfl_xor(bk, m);
-      bk = o < bk ? o : bk;
-    }
+    merge_slices(bk);
     if (active) {
       best = __uint_as_float((unsigned)(bk >> 32));
       bestj = (int)(unsigned)bk;
     }
   }
 
-  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane_id() < kLeafSize) p = ldg4(c.pts, leaf * kLeafSize + lane_id());
-    stage_points<NNVisitor>(L, p);
-    process(L, leaf * kLeafSize);
+  __device__ __forceinline__ void load_leaf(const CloudDev& c, int leaf, f3v (&pt)[P]) const {
+    const long b = (long)leaf * kLeafSize + (lane_id() / Q) * P;
+#pragma unroll
+    for (int h = 0; h < P; ++h) pt[h] = ldg3(c.pts, b + h);
+  }
+
+  __device__ __forceinline__ bool scan_leaves(const CloudDev& c, int base, unsigned long long ex, WaveLds*) {
+    int nxt = base + __builtin_ctzll(ex);
+    ex &= ex - 1;
+    f3v pn[P];
+    load_leaf(c, nxt, pn);
+    bool improved = false;
+    while (nxt >= 0) {
+      const int cur = nxt;
+      f3v p[P];
+#pragma unroll
+      for (int h = 0; h < P; ++h) p[h] = pn[h];
+      nxt = -1;
+      if (ex) {
+        nxt = base + __builtin_ctzll(ex);
+        ex &= ex - 1;
+        load_leaf(c, nxt, pn);
+      }
+      const float before = best;
+      st_scan += 1;
+      scan_regs(p, cur * kLeafSize);
+      improved |= __any(best < before);
+    }
+    return improved;
+  }
+
+  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds*) {
+    f3v p[P];
+    load_leaf(c, leaf, p);
+    scan_regs(p, leaf * kLeafSize);
   }
 };
 using NN1Visitor = NNVisitor<64>;
