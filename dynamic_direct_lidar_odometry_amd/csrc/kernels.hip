@@ -703,7 +703,9 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
   const int qi = lane % Q;
   const int wib = threadIdx.x >> 6;
   __shared__ WaveLds lds[kLinWaves];
+  __shared__ CollectLds clds[kLinWaves];
   WaveLds* L = &lds[wib];
+  CollectLds* CL = &clds[wib];
   const int wave = blockIdx.x * kLinWaves + wib;
   const int nwaves_total = gridDim.x * kLinWaves;
   const int ngroups = (src.n + Q - 1) / Q;
@@ -762,7 +764,17 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
       again = need_seed;
     }
     const unsigned long long skey = gp(src.keys)[ic];
-    split_search<NNVisitor<Q>, Q>(tgt, vis, skey, L);
+    unsigned cst[5] = {0, 0, 0, 0, 0};
+    collect_scan_nn<Q>(tgt, CL, qx, qy, qz, active, vis.best, vis.bestj, skey, cst);
+    if (cst[1]) {  // leaf list overflow: per-leaf traversal (exact, slower)
+      split_search<NNVisitor<Q>, Q>(tgt, vis, skey, L);
+    } else {
+      vis.st_blocks = cst[0];
+      vis.st_box = cst[1];
+      vis.st_exact = cst[2];
+      vis.st_scan = cst[3];
+      vis.st_splits = cst[4];
+    }
     const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
     if (active && lane < Q) {
       corr[i] = valid ? vis.bestj : -1;

@@ -541,3 +541,226 @@ using NN1Visitor = NNVisitor<64>;
 
 
 }  // namespace ddlo
+
+namespace ddlo {
+
+// ===========================================================================
+// Collect-then-scan exact 1-NN for Q-query groups (the correspondence search
+// of the GICP loop).
+//
+// The per-leaf traversal above pays one dependent global round trip per
+// leaf.  Here a wavefront first COLLECTS every leaf that any of its queries
+// may need (upper levels by the union box; then, per candidate level-1 node,
+// lane c loads leaf c's box and tests it exactly against all Q queries, which
+// are broadcast from LDS), and then SCANS the collected list in batches of 8
+// leaves streamed into LDS with global_load_lds (one instruction moves two
+// leaves, one wait per batch).  Exactness is unchanged: a leaf is skipped
+// only if its box is farther than the query's bound, and the bounds only
+// shrink while scanning.
+// ===========================================================================
+constexpr int kListMax = 512;       // leaf list capacity per wavefront
+constexpr int kBatch = 8;           // leaves per LDS-DMA batch
+
+struct CollectLds {
+  f4v q[64];                        // per query lane: x, y, z, bound (bound < 0: inactive)
+  int leaves[kListMax];
+  int nleaves;
+  int overflow;
+  int pad[2];
+  f4v pts[kBatch * kLeafSize];      // batch of streamed leaves (AoS float4)
+};
+constexpr int kCollectLdsBytes = sizeof(CollectLds);
+
+template <int Q>
+struct NNCollector {
+  static constexpr int S = 64 / Q;
+  static constexpr int P = kLeafSize / S;
+  CollectLds* L;
+  WaveBox box;
+  unsigned st_blocks = 0, st_box = 0, st_exact = 0, st_scan = 0, st_splits = 0;
+
+  // candidate level-1 node: exact per-leaf filter against all queries
+  __device__ __forceinline__ void block(const CloudDev& c, int base, int cnt) {
+    const int lane = lane_id();
+    st_blocks += 1;
+    bool need = false;
+    if (lane < cnt) {
+      const float4 lo = ldg4(c.box_lo, base + lane);
+      const float4 hi = ldg4(c.box_hi, base + lane);
+#pragma unroll 4
+      for (int k = 0; k < Q; ++k) {
+        const f4v qk = L->q[k];
+        need |= qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, lo, hi) <= qk.w;
+      }
+    }
+    const unsigned long long m = __ballot(need);
+    st_exact += __popcll(m);
+    const int n0 = L->nleaves;   // uniform (single wave owns L)
+    const int cntm = __popcll(m);
+    if (n0 + cntm > kListMax) {
+      if (lane == 0) L->overflow = 1;
+      return;
+    }
+    if (need) {
+      const int slot = n0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      L->leaves[slot] = base + lane;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) L->nleaves = n0 + cntm;
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  template <int LV>
+  __device__ __forceinline__ void walk(const CloudDev& c, int base, unsigned long long mask) {
+    while (mask) {
+      const int ci = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const int node = base + ci;
+      const int cb = node * kFanout;
+      const int cnt = min(kFanout, lvl_cnt(c, LV - 1) - cb);
+      if constexpr (LV == 1) {
+        block(c, cb, cnt);
+      } else {
+        const int lane = lane_id();
+        bool ov = false;
+        if (lane < cnt) {
+          const int o = lvl_off(c, LV - 1) + cb + lane;
+          ov = box_overlap(box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
+        }
+        walk<LV - 1>(c, cb, __ballot(ov));
+      }
+    }
+  }
+
+  __device__ __forceinline__ void collect(const CloudDev& c) {
+    const int T = c.nlevels - 1;
+    if (T == 0) {
+      block(c, 0, c.cnt0);
+      return;
+    }
+    const int lane = lane_id();
+    bool ov = false;
+    if (lane < lvl_cnt(c, T)) {
+      const int o = lvl_off(c, T) + lane;
+      ov = box_overlap(box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
+    }
+    const unsigned long long m = __ballot(ov);
+    switch (T) {
+      case 1: walk<1>(c, 0, m); break;
+      case 2: walk<2>(c, 0, m); break;
+      case 3: walk<3>(c, 0, m); break;
+      default: walk<4>(c, 0, m); break;
+    }
+  }
+
+  // Stream the collected leaves through LDS and scan them.  (best, bestj) is
+  // the query's running minimum, identical in all S lanes of the query.
+  __device__ __forceinline__ void scan(const CloudDev& c, float qx, float qy, float qz, bool active, float& best,
+                                       int& bestj) {
+    const int lane = lane_id();
+    const int n = L->nleaves;
+    unsigned long long bk = dkey(best, bestj);
+    const int s = lane / Q;
+    const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+    for (int b0 = 0; b0 < n; b0 += kBatch) {
+      const int nb = min(kBatch, n - b0);
+      // one global_load_lds_dwordx4 moves two leaves: lanes 0-31 -> leaf 2t, 32-63 -> leaf 2t+1
+#pragma unroll
+      for (int t = 0; t < kBatch / 2; ++t) {
+        if (2 * t < nb) {
+          const int lf = L->leaves[b0 + min(2 * t + (lane >> 5), nb - 1)];
+          const float4* src = c.pts + (size_t)lf * kLeafSize + (lane & 31);
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)&L->pts[2 * t * kLeafSize], 16, 0, 0);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the batch has landed in LDS
+      __builtin_amdgcn_wave_barrier();
+      for (int t = 0; t < nb; ++t) {
+        const int start = L->leaves[b0 + t] * kLeafSize + s * P;
+        const f4v* pp = &L->pts[t * kLeafSize + s * P];
+#pragma unroll
+        for (int h = 0; h < P; h += 2) {
+          const f4v p0 = pp[h], p1 = pp[h + 1];
+          const f2v dx = qx2 - f2v{p0.x, p1.x};
+          const f2v dy = qy2 - f2v{p0.y, p1.y};
+          const f2v dz = qz2 - f2v{p0.z, p1.z};
+          const f2v d = (dx * dx + dy * dy) + dz * dz;
+          bk = umin64(bk, dkey(d.x, start + h));
+          bk = umin64(bk, dkey(d.y, start + h + 1));
+        }
+      }
+      st_scan += nb;
+      __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (Q <= 16) bk = xor_min64<16>(bk);
+    if constexpr (Q <= 32) bk = xor_min64<32>(bk);
+    if (active) {
+      best = __uint_as_float((unsigned)(bk >> 32));
+      bestj = (int)(unsigned)bk;
+    }
+  }
+};
+
+// Full exact bounded 1-NN for a Q-query group: split the group at Morton
+// jumps (<= 4 compact sub-ranges), collect per sub-range, scan once.
+template <int Q>
+__device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L, float qx, float qy, float qz,
+                                                bool active, float& best, int& bestj, unsigned long long key,
+                                                unsigned (&st)[5]) {
+  const int lane = lane_id();
+  const int qi = lane % Q;
+  if (lane < Q) L->q[lane] = f4v{qx, qy, qz, active ? best : -1.f};
+  if (lane == 0) {
+    L->nleaves = 0;
+    L->overflow = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  NNCollector<Q> col;
+  col.L = L;
+  const WaveBox whole = make_wave_box(active, qx, qy, qz, best);
+  if (!(box_extent(whole) > kSplitExtent)) {
+    col.box = whole;
+    col.collect(c);
+  } else {
+    col.st_splits += 1;
+    const int sp = morton_jump_split<Q>(key, 0, Q);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int lo = h == 0 ? 0 : sp, hi = h == 0 ? sp : Q;
+      if (lo >= hi) continue;
+      const bool act = active && qi >= lo && qi < hi;
+      const WaveBox hb = make_wave_box(act, qx, qy, qz, best);
+      if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
+        col.st_splits += 1;
+        const int s2 = morton_jump_split<Q>(key, lo, hi);
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int l2 = h2 == 0 ? lo : s2, r2 = h2 == 0 ? s2 : hi;
+          const bool a2 = active && qi >= l2 && qi < r2;
+          if (!__any(a2)) continue;
+          col.box = make_wave_box(a2, qx, qy, qz, best);
+          col.collect(c);
+        }
+      } else if (__any(act)) {
+        col.box = hb;
+        col.collect(c);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  st[0] = col.st_blocks;
+  st[2] = col.st_exact;
+  st[4] = col.st_splits;
+  if (L->overflow) {
+    st[1] = 1;  // caller falls back to the per-leaf traversal
+    return;
+  }
+  st[1] = 0;
+  // the same leaf may have been collected by two sub-ranges: harmless (the
+  // min is idempotent), so no de-duplication
+  col.scan(c, qx, qy, qz, active, best, bestj);
+  st[3] = col.st_scan;
+}
+
+}  // namespace ddlo
