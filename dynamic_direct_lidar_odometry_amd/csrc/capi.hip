@@ -74,6 +74,9 @@ struct CloudData {
   int nlevels = 0;
   int lvl_off[kMaxLevels] = {0};
   int lvl_cnt[kMaxLevels] = {0};
+  int upper_count() const {
+    return nlevels <= 1 ? 0 : lvl_off[nlevels - 1] + lvl_cnt[nlevels - 1] - lvl_off[1];
+  }
   CloudDev dev() const {
     CloudDev c;
     c.pts = pts.as<float4>();
@@ -160,6 +163,8 @@ gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, 
   cd->n = N;
   cd->nlevels = levels_for(N, cd->lvl_cnt, cd->lvl_off);
   if (cd->nlevels < 0) return fail(GICP_EINVAL, "cloud too large for the search hierarchy");
+  if (cd->upper_count() > 2048)  // LDS cache of levels >= 1 (64 KB): <= 4.2M points
+    return fail(GICP_EINVAL, "cloud too large for the search hierarchy's LDS cache (max ~4.2M points)");
   const int total_boxes = cd->lvl_off[cd->nlevels - 1] + cd->lvl_cnt[cd->nlevels - 1];
   hipStream_t s = c->stream;
   const size_t raw_sz = (n - 1) * stride + 12;
@@ -287,7 +292,7 @@ gicp_status capture_chunk(gicp_ctx* c, bool with_init, int nblocks, hipGraph_t* 
   HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
   if (with_init) launch_align_init(c->stream, jd);
   for (int i = 0; i < kChunk; ++i) {
-    launch_linearize(c->stream, jd, c->src.cloud->n, nblocks);
+    launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
     launch_lm_step(c->stream, jd);
   }
   // publish {iter, done} to pinned host memory at the end of the chunk
@@ -361,7 +366,7 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
   launch_align_init(c->stream, jd);
   for (int i = 0; i < max_it; ++i) {
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i], c->stream));
-    launch_linearize(c->stream, jd, c->src.cloud->n, nblocks);
+    launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i + 1], c->stream));
     launch_lm_step(c->stream, jd);
   }
@@ -726,7 +731,7 @@ gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, doubl
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   const AlignJob* jd = c->job_dev.as<AlignJob>();
   launch_align_init(c->stream, jd);
-  launch_linearize(c->stream, jd, c->src.cloud->n, nblocks);
+  launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
   launch_lm_step(c->stream, jd);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));

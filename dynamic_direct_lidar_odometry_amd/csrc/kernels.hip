@@ -684,7 +684,7 @@ __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__
 // found nothing search again with the full max_corr bound.  Writes corr/sqd
 // (update_correspondences, nano_gicp_impl.hpp:249-258).
 template <int Q>
-__global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ job) {
+__global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
   const CloudDev src = job->src;
@@ -702,13 +702,19 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
   const int lane = lane_id();
   const int qi = lane % Q;
   const int wib = threadIdx.x >> 6;
-  __shared__ WaveLds lds[kLinWaves];
-  __shared__ CollectLds clds[kLinWaves];
-  WaveLds* L = &lds[wib];
-  CollectLds* CL = &clds[wib];
+  // dynamic LDS: [kLinWaves x CollectLds][upper-level box cache]
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  CollectLds* CL = reinterpret_cast<CollectLds*>(dsm) + wib;
+  f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kCollectLdsBytes);
+  fill_upper(tgt, upper);
+  __syncthreads();
   const int wave = blockIdx.x * kLinWaves + wib;
   const int nwaves_total = gridDim.x * kLinWaves;
   const int ngroups = (src.n + Q - 1) / Q;
+  // previous linearization pose (for the triangle-inequality bound)
+  float Rp[9], tp[3];
+  for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
+  for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const int i = g * Q + qi;
@@ -732,11 +738,17 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
     if (have_prev && active) {
       const int j = corr[i];
       if (j >= 0) {
-        const float4 p = ldg4(tgt.pts, j);
-        const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
-        if (d < cap2) {
-          vis.best = d;
-          vis.bestj = j;
+        // NN(q) <= |q - p_prev| <= sqrt(sqd_prev) + |q - q_prev| (triangle
+        // inequality; fp64 with an upward margin covers fp32 rounding), so
+        // the bound needs no load of the previous match.
+        const float qpx = (Rp[0] * a.x + Rp[1] * a.y) + (Rp[2] * a.z + tp[0]);
+        const float qpy = (Rp[3] * a.x + Rp[4] * a.y) + (Rp[5] * a.z + tp[1]);
+        const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
+        const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
+        const double r = sqrt((double)sqd[i]) + sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
+        const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
+        if (b2 < (double)cap2) {
+          vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
           seeded = true;
         }
       }
@@ -764,17 +776,13 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
       again = need_seed;
     }
     const unsigned long long skey = gp(src.keys)[ic];
-    unsigned cst[5] = {0, 0, 0, 0, 0};
-    collect_scan_nn<Q>(tgt, CL, qx, qy, qz, active, vis.best, vis.bestj, skey, cst);
-    if (cst[1]) {  // leaf list overflow: per-leaf traversal (exact, slower)
-      split_search<NNVisitor<Q>, Q>(tgt, vis, skey, L);
-    } else {
-      vis.st_blocks = cst[0];
-      vis.st_box = cst[1];
-      vis.st_exact = cst[2];
-      vis.st_scan = cst[3];
-      vis.st_splits = cst[4];
-    }
+    unsigned cst[6] = {0, 0, 0, 0, 0, 0};
+    collect_scan_nn<Q>(tgt, CL, upper, qx, qy, qz, active, vis.best, vis.bestj, skey, cst);
+    vis.st_blocks = cst[0];
+    vis.st_box = cst[1];
+    vis.st_exact = cst[2];
+    vis.st_scan = cst[3];
+    vis.st_splits = cst[4];
     const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
     if (active && lane < Q) {
       corr[i] = valid ? vis.bestj : -1;
@@ -788,7 +796,7 @@ __global__ __launch_bounds__(256) void k_nn_search(const AlignJob* __restrict__ 
       o[2] = vis.st_exact;
       o[3] = vis.st_scan;
       o[4] = (unsigned)(tm1 - tm0);
-      o[5] = 0;
+      o[5] = cst[5] - (unsigned)tm0;  // cycles until the end of the collect phase
       o[6] = (unsigned)__popcll(__ballot(again)) | (vis.st_splits << 16);
       o[7] = 1;
     }
@@ -1407,10 +1415,13 @@ void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, con
   k_cov_export<<<cdiv(n, 256), 256, 0, s>>>(cov6, layout, n, perm, out);
 }
 void launch_align_init(hipStream_t s, const AlignJob* job) { k_align_init<<<1, 64, 0, s>>>(job); }
-void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks) {
+size_t search_lds_bytes(int upper_count) {
+  return (size_t)kLinWaves * kCollectLdsBytes + 2 * sizeof(f4v) * (size_t)upper_count;
+}
+void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int job_upper_count) {
   const int search_groups = (nsrc + kSearchQ - 1) / kSearchQ;
   const int sb = std::max(1, std::min((search_groups + kLinWaves - 1) / kLinWaves, 8192));
-  k_nn_search<kSearchQ><<<sb, 64 * kLinWaves, 0, s>>>(job);
+  k_nn_search<kSearchQ><<<sb, 64 * kLinWaves, search_lds_bytes(job_upper_count), s>>>(job);
   k_moments<<<nblocks, 64 * kMomWaves, 0, s>>>(job);
 }
 int search_queries_per_wave() { return kSearchQ; }

@@ -21,7 +21,8 @@ bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq,
 void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6);
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);
 void launch_align_init(hipStream_t s, const AlignJob* job);
-void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks);
+// tgt_upper: number of upper-level (>= 1) boxes of the target (LDS cache size)
+void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int tgt_upper);
 int search_queries_per_wave();
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
 void launch_lm_step(hipStream_t s, const AlignJob* job);

@@ -549,119 +549,81 @@ namespace ddlo {
 // of the GICP loop).
 //
 // The per-leaf traversal above pays one dependent global round trip per
-// leaf.  Here a wavefront first COLLECTS every leaf that any of its queries
-// may need (upper levels by the union box; then, per candidate level-1 node,
-// lane c loads leaf c's box and tests it exactly against all Q queries, which
-// are broadcast from LDS), and then SCANS the collected list in batches of 8
-// leaves streamed into LDS with global_load_lds (one instruction moves two
-// leaves, one wait per batch).  Exactness is unchanged: a leaf is skipped
-// only if its box is farther than the query's bound, and the bounds only
-// shrink while scanning.
+// node and per leaf.  Here a wavefront
+//   1. walks the upper levels (levels >= 1, cached in LDS per workgroup) with
+//      the union box of its queries' balls -> candidate level-1 blocks;
+//   2. loads the leaf boxes of up to 4 candidate blocks at once (lane = leaf)
+//      and tests every leaf EXACTLY against all Q queries (broadcast from
+//      LDS) -> per-wave leaf list;
+//   3. streams the listed leaves through LDS in batches with global_load_lds
+//      (one instruction moves two 32-point leaves), one wait per batch, and
+//      every lane scans its slice of each leaf.
+// Exactness: a leaf is dropped only if its box is farther than the query's
+// bound, and bounds only shrink while scanning.
 // ===========================================================================
-constexpr int kListMax = 512;       // leaf list capacity per wavefront
-constexpr int kBatch = 8;           // leaves per LDS-DMA batch
+constexpr int kListMax = 256;       // leaf list capacity per wavefront
+constexpr int kBlkMax = 32;         // candidate level-1 blocks per wavefront
+constexpr int kBatch = 4;           // leaves per LDS-DMA batch
+constexpr int kQMax = 16;           // queries per wavefront (collect path)
 
 struct CollectLds {
-  f4v q[64];                        // per query lane: x, y, z, bound (bound < 0: inactive)
+  f4v q[kQMax];                     // per query: x, y, z, bound (bound < 0: inactive)
   int leaves[kListMax];
-  int nleaves;
-  int overflow;
-  int pad[2];
-  f4v pts[kBatch * kLeafSize];      // batch of streamed leaves (AoS float4)
+  int blocks[kBlkMax];
+  int nleaves, nblocks, pad0, pad1;
+  f4v pts[kBatch * kLeafSize];      // streamed leaves (AoS float4)
 };
-constexpr int kCollectLdsBytes = sizeof(CollectLds);
+constexpr int kCollectLdsBytes = (int)sizeof(CollectLds);
+
+__device__ __forceinline__ int upper_count(const CloudDev& c) {
+  return c.nlevels <= 1 ? 0 : (lvl_off(c, c.nlevels - 1) + lvl_cnt(c, c.nlevels - 1) - c.off1);
+}
+
+// Upper-level box cache shared by a workgroup: boxes of levels >= 1 in the
+// cloud's level order (index = global box index - lvl_off(c, 1)); lo at
+// [0, n), hi at [n, 2n).  Cooperative fill by the whole workgroup.
+__device__ __forceinline__ void fill_upper(const CloudDev& c, f4v* U) {
+  const int n = upper_count(c);
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const float4 lo = ldg4(c.box_lo, c.off1 + k), hi = ldg4(c.box_hi, c.off1 + k);
+    U[k] = f4v{lo.x, lo.y, lo.z, 0.f};
+    U[n + k] = f4v{hi.x, hi.y, hi.z, 0.f};
+  }
+}
+
+__device__ __forceinline__ bool box_overlap_v(const WaveBox& w, f4v lo, f4v hi) {
+  return lo.x <= w.hx && hi.x >= w.lx && lo.y <= w.hy && hi.y >= w.ly && lo.z <= w.hz && hi.z >= w.lz;
+}
 
 template <int Q>
 struct NNCollector {
   static constexpr int S = 64 / Q;
   static constexpr int P = kLeafSize / S;
   CollectLds* L;
+  const f4v* U;     // upper-level cache
+  int nup;          // its size
   WaveBox box;
-  unsigned st_blocks = 0, st_box = 0, st_exact = 0, st_scan = 0, st_splits = 0;
+  // per-lane query state; bk = (best, bestj) key, identical in the S lanes of a query
+  float qx, qy, qz;
+  bool active;
+  unsigned long long bk;
+  unsigned st_blocks = 0, st_exact = 0, st_scan = 0, st_splits = 0;
 
-  // candidate level-1 node: exact per-leaf filter against all queries
-  __device__ __forceinline__ void block(const CloudDev& c, int base, int cnt) {
-    const int lane = lane_id();
-    st_blocks += 1;
-    bool need = false;
-    if (lane < cnt) {
-      const float4 lo = ldg4(c.box_lo, base + lane);
-      const float4 hi = ldg4(c.box_hi, base + lane);
-#pragma unroll 4
-      for (int k = 0; k < Q; ++k) {
-        const f4v qk = L->q[k];
-        need |= qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, lo, hi) <= qk.w;
-      }
-    }
-    const unsigned long long m = __ballot(need);
-    st_exact += __popcll(m);
-    const int n0 = L->nleaves;   // uniform (single wave owns L)
-    const int cntm = __popcll(m);
-    if (n0 + cntm > kListMax) {
-      if (lane == 0) L->overflow = 1;
-      return;
-    }
-    if (need) {
-      const int slot = n0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-      L->leaves[slot] = base + lane;
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) L->nleaves = n0 + cntm;
+  __device__ __forceinline__ float bound() const { return __uint_as_float((unsigned)(bk >> 32)); }
+
+  __device__ __forceinline__ void publish_bounds() {
+    if (lane_id() < Q) L->q[lane_id()].w = active ? bound() : -1.f;
     __builtin_amdgcn_wave_barrier();
   }
 
-  template <int LV>
-  __device__ __forceinline__ void walk(const CloudDev& c, int base, unsigned long long mask) {
-    while (mask) {
-      const int ci = __builtin_ctzll(mask);
-      mask &= mask - 1;
-      const int node = base + ci;
-      const int cb = node * kFanout;
-      const int cnt = min(kFanout, lvl_cnt(c, LV - 1) - cb);
-      if constexpr (LV == 1) {
-        block(c, cb, cnt);
-      } else {
-        const int lane = lane_id();
-        bool ov = false;
-        if (lane < cnt) {
-          const int o = lvl_off(c, LV - 1) + cb + lane;
-          ov = box_overlap(box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
-        }
-        walk<LV - 1>(c, cb, __ballot(ov));
-      }
-    }
-  }
-
-  __device__ __forceinline__ void collect(const CloudDev& c) {
-    const int T = c.nlevels - 1;
-    if (T == 0) {
-      block(c, 0, c.cnt0);
-      return;
-    }
-    const int lane = lane_id();
-    bool ov = false;
-    if (lane < lvl_cnt(c, T)) {
-      const int o = lvl_off(c, T) + lane;
-      ov = box_overlap(box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
-    }
-    const unsigned long long m = __ballot(ov);
-    switch (T) {
-      case 1: walk<1>(c, 0, m); break;
-      case 2: walk<2>(c, 0, m); break;
-      case 3: walk<3>(c, 0, m); break;
-      default: walk<4>(c, 0, m); break;
-    }
-  }
-
-  // Stream the collected leaves through LDS and scan them.  (best, bestj) is
-  // the query's running minimum, identical in all S lanes of the query.
-  __device__ __forceinline__ void scan(const CloudDev& c, float qx, float qy, float qz, bool active, float& best,
-                                       int& bestj) {
+  // Stream the listed leaves through LDS and scan them.
+  __device__ __forceinline__ void flush_leaves(const CloudDev& c) {
     const int lane = lane_id();
     const int n = L->nleaves;
-    unsigned long long bk = dkey(best, bestj);
+    if (n == 0) return;
     const int s = lane / Q;
     const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+    unsigned long long k = bk;
     for (int b0 = 0; b0 < n; b0 += kBatch) {
       const int nb = min(kBatch, n - b0);
       // one global_load_lds_dwordx4 moves two leaves: lanes 0-31 -> leaf 2t, 32-63 -> leaf 2t+1
@@ -686,42 +648,159 @@ struct NNCollector {
           const f2v dy = qy2 - f2v{p0.y, p1.y};
           const f2v dz = qz2 - f2v{p0.z, p1.z};
           const f2v d = (dx * dx + dy * dy) + dz * dz;
-          bk = umin64(bk, dkey(d.x, start + h));
-          bk = umin64(bk, dkey(d.y, start + h + 1));
+          k = umin64(k, dkey(d.x, start + h));
+          k = umin64(k, dkey(d.y, start + h + 1));
         }
       }
       st_scan += nb;
       __builtin_amdgcn_wave_barrier();
     }
-    if constexpr (Q <= 16) bk = xor_min64<16>(bk);
-    if constexpr (Q <= 32) bk = xor_min64<32>(bk);
-    if (active) {
-      best = __uint_as_float((unsigned)(bk >> 32));
-      bestj = (int)(unsigned)bk;
+    if constexpr (Q <= 16) k = xor_min64<16>(k);
+    if constexpr (Q <= 32) k = xor_min64<32>(k);
+    if (active) bk = k;
+    if (lane == 0) L->nleaves = 0;
+    __builtin_amdgcn_wave_barrier();
+    publish_bounds();
+  }
+
+  // exact leaf filter of the listed blocks (4 blocks per round trip)
+  __device__ __forceinline__ void flush_blocks(const CloudDev& c) {
+    const int lane = lane_id();
+    const int nb = L->nblocks;
+    for (int b0 = 0; b0 < nb; b0 += 4) {
+      float4 lo[4], hi[4];
+      int base[4], cnt[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int bi = min(b0 + u, nb - 1);
+        base[u] = L->blocks[bi] * kFanout;
+        cnt[u] = (b0 + u < nb) ? min(kFanout, c.cnt0 - base[u]) : 0;
+        const int li = min(base[u] + lane, c.cnt0 - 1);
+        lo[u] = ldg4(c.box_lo, li);
+        hi[u] = ldg4(c.box_hi, li);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (cnt[u] == 0) continue;
+        st_blocks += 1;
+        bool need = false;
+        if (lane < cnt[u]) {
+#pragma unroll 4
+          for (int q = 0; q < Q; ++q) {
+            const f4v qk = L->q[q];
+            need |= qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, lo[u], hi[u]) <= qk.w;
+          }
+        }
+        const unsigned long long m = __ballot(need);
+        const int cm = __popcll(m);
+        st_exact += cm;
+        if (L->nleaves + cm > kListMax) flush_leaves(c);  // tightens bounds; list empties
+        const int n0 = L->nleaves;
+        if (need) {
+          const int slot =
+              n0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+          L->leaves[slot] = base[u] + lane;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) L->nleaves = n0 + cm;
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (lane == 0) L->nblocks = 0;
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  __device__ __forceinline__ void push_block(const CloudDev& c, int node) {
+    if (L->nblocks >= kBlkMax) flush_blocks(c);
+    if (lane_id() == 0) {
+      const int n = L->nblocks;
+      L->blocks[n] = node;
+      L->nblocks = n + 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  __device__ __forceinline__ bool upper_ov(const CloudDev& c, int level, int idx) const {
+    const int k = lvl_off(c, level) - c.off1 + idx;
+    return box_overlap_v(box, U[k], U[nup + k]);
+  }
+
+  template <int LV>
+  __device__ __forceinline__ void walk(const CloudDev& c, int base, unsigned long long mask) {
+    // mask selects nodes of level LV (>= 2) overlapping the box
+    while (mask) {
+      const int ci = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const int node = base + ci;
+      const int cb = node * kFanout;
+      const int cnt = min(kFanout, lvl_cnt(c, LV - 1) - cb);
+      const int lane = lane_id();
+      const bool ov = lane < cnt && upper_ov(c, LV - 1, cb + lane);
+      unsigned long long m = __ballot(ov);
+      if constexpr (LV == 2) {
+        while (m) {
+          const int b = __builtin_ctzll(m);
+          m &= m - 1;
+          push_block(c, cb + b);
+        }
+      } else {
+        walk<LV - 1>(c, cb, m);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void collect_blocks(const CloudDev& c) {
+    const int T = c.nlevels - 1;
+    if (T == 0) {
+      push_block(c, 0);
+      return;
+    }
+    const int lane = lane_id();
+    const bool ov = lane < lvl_cnt(c, T) && upper_ov(c, T, lane);
+    unsigned long long m = __ballot(ov);
+    if (T == 1) {
+      while (m) {
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        push_block(c, b);
+      }
+      return;
+    }
+    switch (T) {
+      case 2: walk<2>(c, 0, m); break;
+      case 3: walk<3>(c, 0, m); break;
+      default: walk<4>(c, 0, m); break;
     }
   }
 };
 
 // Full exact bounded 1-NN for a Q-query group: split the group at Morton
-// jumps (<= 4 compact sub-ranges), collect per sub-range, scan once.
+// jumps (<= 4 compact sub-ranges), collect per sub-range, filter, scan.
 template <int Q>
-__device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L, float qx, float qy, float qz,
-                                                bool active, float& best, int& bestj, unsigned long long key,
-                                                unsigned (&st)[5]) {
+__device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L, const f4v* U, float qx, float qy,
+                                                float qz, bool active, float& best, int& bestj,
+                                                unsigned long long key, unsigned (&st)[6]) {
   const int lane = lane_id();
   const int qi = lane % Q;
   if (lane < Q) L->q[lane] = f4v{qx, qy, qz, active ? best : -1.f};
   if (lane == 0) {
     L->nleaves = 0;
-    L->overflow = 0;
+    L->nblocks = 0;
   }
   __builtin_amdgcn_wave_barrier();
   NNCollector<Q> col;
   col.L = L;
+  col.U = U;
+  col.nup = upper_count(c);
+  col.qx = qx;
+  col.qy = qy;
+  col.qz = qz;
+  col.active = active;
+  col.bk = dkey(best, bestj);
   const WaveBox whole = make_wave_box(active, qx, qy, qz, best);
   if (!(box_extent(whole) > kSplitExtent)) {
     col.box = whole;
-    col.collect(c);
+    col.collect_blocks(c);
   } else {
     col.st_splits += 1;
     const int sp = morton_jump_split<Q>(key, 0, Q);
@@ -730,7 +809,7 @@ __device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L
       const int lo = h == 0 ? 0 : sp, hi = h == 0 ? sp : Q;
       if (lo >= hi) continue;
       const bool act = active && qi >= lo && qi < hi;
-      const WaveBox hb = make_wave_box(act, qx, qy, qz, best);
+      const WaveBox hb = make_wave_box(act, qx, qy, qz, col.bound());
       if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
         col.st_splits += 1;
         const int s2 = morton_jump_split<Q>(key, lo, hi);
@@ -739,28 +818,29 @@ __device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L
           const int l2 = h2 == 0 ? lo : s2, r2 = h2 == 0 ? s2 : hi;
           const bool a2 = active && qi >= l2 && qi < r2;
           if (!__any(a2)) continue;
-          col.box = make_wave_box(a2, qx, qy, qz, best);
-          col.collect(c);
+          col.box = make_wave_box(a2, qx, qy, qz, col.bound());
+          col.collect_blocks(c);
         }
       } else if (__any(act)) {
         col.box = hb;
-        col.collect(c);
+        col.collect_blocks(c);
       }
     }
   }
-  __builtin_amdgcn_wave_barrier();
+  // a block listed by two sub-ranges is filtered twice: harmless (a leaf
+  // scanned twice leaves the minimum unchanged)
+  col.flush_blocks(c);
+  st[5] = (unsigned)__builtin_amdgcn_s_memtime();
+  col.flush_leaves(c);
   st[0] = col.st_blocks;
-  st[2] = col.st_exact;
-  st[4] = col.st_splits;
-  if (L->overflow) {
-    st[1] = 1;  // caller falls back to the per-leaf traversal
-    return;
-  }
   st[1] = 0;
-  // the same leaf may have been collected by two sub-ranges: harmless (the
-  // min is idempotent), so no de-duplication
-  col.scan(c, qx, qy, qz, active, best, bestj);
+  st[2] = col.st_exact;
   st[3] = col.st_scan;
+  st[4] = col.st_splits;
+  if (active) {
+    best = col.bound();
+    bestj = (int)(unsigned)col.bk;
+  }
 }
 
 }  // namespace ddlo

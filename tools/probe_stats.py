@@ -13,7 +13,7 @@ def summarize(tag, st):
         v = st[:, i]
         print(f"  {name:6s} mean {v.mean():8.1f} p50 {np.percentile(v,50):6.0f} p90 {np.percentile(v,90):6.0f} p99 {np.percentile(v,99):6.0f} max {v.max():6d} sum {v.sum()}")
     cyc = st[:, 4].astype(np.float64); mcyc = st[:, 5].astype(np.float64)
-    print(f"  search cycles mean {cyc.mean():.0f} p50 {np.percentile(cyc,50):.0f} p90 {np.percentile(cyc,90):.0f} max {cyc.max():.0f}; moment cycles mean {mcyc.mean():.0f} max {mcyc.max():.0f}")
+    print(f"  search cycles mean {cyc.mean():.0f} p50 {np.percentile(cyc,50):.0f} p90 {np.percentile(cyc,90):.0f} max {cyc.max():.0f}; collect-phase cycles mean {mcyc.mean():.0f} max {mcyc.max():.0f}")
     print(f"  cycles per scanned leaf {cyc.sum()/max(1,st[:,3].sum()):.0f}; corr(scan, cycles) {np.corrcoef(st[:,3], cyc)[0,1]:.2f} corr(box, cycles) {np.corrcoef(st[:,1], cyc)[0,1]:.2f}")
     print(f"  pass-2 lanes mean {(st[:,6]&0xffff).mean():.2f}; splits mean {(st[:,6]>>16).mean():.3f} max {(st[:,6]>>16).max()}")
     top = np.argsort(-st[:, 3])[:5]
