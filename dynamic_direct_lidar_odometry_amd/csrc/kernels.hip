@@ -745,11 +745,22 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
         const float qpy = (Rp[3] * a.x + Rp[4] * a.y) + (Rp[5] * a.z + tp[1]);
         const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
         const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
-        const double r = sqrt((double)sqd[i]) + sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
-        const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
-        if (b2 < (double)cap2) {
-          vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
-          seeded = true;
+        const double mv = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
+        if (mv < 0.02) {
+          const double r = sqrt((double)sqd[i]) + mv;
+          const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
+          if (b2 < (double)cap2) {
+            vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
+            seeded = true;
+          }
+        } else {  // large pose step: the exact distance to the previous match
+          const float4 p = ldg4(tgt.pts, j);
+          const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
+          if (d < cap2) {
+            vis.best = d;
+            vis.bestj = j;
+            seeded = true;
+          }
         }
       }
     }
