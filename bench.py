@@ -1,0 +1,216 @@
+"""Benchmark of the GICP hot path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], SURVEY.md §8(d) cfg 3): S2M GICP of a
+131,072-point 64x2048 scan against a 500,000-point fused submap of 4
+keyframes (target covariances per keyframe, k=10 PLANE, as
+odom.cc:1147-1149,1302-1310), reference S2M parameters (ddlo.yaml:196-201:
+maxCorr 2.0 m, maxIterations 32, transformationEpsilon 0.01, LM), initial
+guess = ground truth perturbed by t=(0.30,-0.20,0.05) m, yaw 2 deg,
+roll/pitch 0.5 deg.  Synthetic data (scene.py ray-caster, no datasets).
+
+One step = one align() (NanoGICP::computeTransformation), index build and
+covariances excluded (SURVEY.md §8(d) "ms/scan").  value = outer GICP
+iterations per second over the whole job (all ranks); ms_per_step = ms/scan.
+
+Multi-GPU (torchrun, one process per GPU): the path does not shard in this
+round (SURVEY.md §8(e) spatial sharding is future work), so every rank runs
+an independent replica on its own GPU (weak scaling, no data-path
+collective); torch.distributed is used for the barrier and max-time only.
+
+Roofline: the linearize step (k_nn_search + k_moments, launched back to back
+per outer iteration) timed with HIP events on the library's stream inside
+this process; algorithmic bytes per launch = 76 * N_s (SURVEY.md §8(d)
+B_lin), peak HBM 8 TB/s (MI355X_MICROARCH.md).  cpu_baseline = the C++/OpenMP
+oracle (oracle/cpu_ref.cpp, a restatement of the reference algorithm, "port")
+timed on this host on the same problem.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "GICP iters/sec + ms/scan, 131k-pt source → 500k-pt submap; pose Δ vs CPU ref"
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_problem():
+    from dynamic_direct_lidar_odometry_amd import scene
+    prob = scene.s2m_problem(64, 2048, 4, 500000, 3)
+    return prob
+
+
+def keyframe_covariances(ctx_factory, keyframes, k=10):
+    """Per-keyframe covariances on the GPU (odom.cc:1147-1149), concatenated (:1302-1310)."""
+    from dynamic_direct_lidar_odometry_amd import SOURCE, default_params
+    covs = []
+    c = ctx_factory()
+    c.set_params(default_params(k_correspondences=k))
+    for kf in keyframes:
+        c.set_source(kf)
+        c.compute_covariances(SOURCE)
+        covs.append(c.get_covariances(SOURCE))
+    c.close()
+    return np.concatenate(covs)
+
+
+def rot_err(A, B):
+    R = A[:3, :3].astype(np.float64).T @ B[:3, :3].astype(np.float64)
+    return float(math.acos(max(-1.0, min(1.0, (np.trace(R) - 1) / 2))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-runs", type=int, default=3, help="oracle align runs for cpu_baseline (median)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as td
+        torch.cuda.set_device(local_rank)
+        td.init_process_group(backend="nccl")
+        dist = td
+
+    from dynamic_direct_lidar_odometry_amd import Context, default_params, SOURCE, TARGET
+
+    t0 = time.time()
+    prob = build_problem()
+    sub = np.ascontiguousarray(np.concatenate(prob["keyframes"])[prob["subset"]])
+    src = prob["source"]
+    kcov_all = keyframe_covariances(lambda: Context(local_rank), prob["keyframes"], k=10)
+    tcov = np.ascontiguousarray(kcov_all[prob["subset"]])
+    params = default_params(k_correspondences=20, max_correspondence_distance=2.0, max_iterations=32,
+                            transformation_epsilon=0.01)
+    ctx = Context(local_rank)
+    # source covariances as the pipeline makes them: by the S2S instance, k=10
+    # (odom.cc:765 copies them into S2M; ddlo.yaml:188)
+    ctx.set_params(default_params(k_correspondences=10))
+    ctx.set_source(src)
+    ctx.compute_covariances(SOURCE)
+    scov = ctx.get_covariances(SOURCE)
+    ctx.set_params(params)
+    ctx.set_target(sub)
+    ctx.set_covariances(TARGET, tcov)
+    guess = prob["guess"].astype(np.float32)
+    log(f"[rank {rank}] setup {time.time() - t0:.1f}s: src {len(src)} tgt {len(sub)}")
+
+    # warmup
+    for _ in range(args.warmup):
+        out, res = ctx.align(guess)
+    ctx.synchronize()
+
+    # timed region: K aligns, barrier + sync on both sides, max over ranks
+    if dist:
+        dist.barrier()
+    ctx.synchronize()
+    t_start = time.perf_counter()
+    iters = 0
+    for _ in range(args.steps):
+        out, res = ctx.align(guess)
+        iters += res.iterations_run
+    ctx.synchronize()
+    t_end = time.perf_counter()
+    elapsed = t_end - t_start
+    if dist:
+        import torch
+        t = torch.tensor([elapsed, float(iters)], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        iters_total = float(tsum[1])
+    else:
+        iters_total = float(iters)
+    steps_total = args.steps * world
+    value = iters_total / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # roofline: linearize launches timed with HIP events on the library stream
+    ctx.set_profiling(True)
+    lin_ms, lin_launches = 0.0, 0
+    for _ in range(max(3, min(args.steps, 10))):
+        _, r = ctx.align(guess)
+        lin_ms += r.linearize_ms
+        lin_launches += r.iterations_run
+    ctx.set_profiling(False)
+    ctx.synchronize()
+    avg_launch_s = (lin_ms / max(lin_launches, 1)) * 1e-3
+    bytes_per_launch = 76.0 * len(src)   # SURVEY.md §8(d) B_lin = 76 * N_s
+    achieved_gbs = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GICP iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 search / f64 normal equations",
+        "data": "synthetic (ray-cast plaza, scene.py; no datasets)",
+        "config": {"workload": "cfg3 S2M GICP: 131,072-pt 64x2048 scan -> 500,000-pt 4-keyframe submap, "
+                               "LM, maxCorr 2.0 m, maxIter 32, transEps 0.01",
+                   "source_points": int(len(src)), "target_points": int(len(sub)),
+                   "iterations_per_scan": round(iters_total / steps_total, 3),
+                   "parallelism": f"replicas x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": None,
+                     "kernel": "linearize = k_nn_search + k_moments (per outer iteration)",
+                     "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                     "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+    }
+
+    if rank == 0 and not args.no_cpu:
+        from oracle import oracle as O
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+        g = O.Gicp(src, sub, O.as_params(params), threads=threads)
+        g.set_covariances(0, scov)
+        g.set_covariances(1, tcov)
+        times = []
+        oout = None
+        for _ in range(args.cpu_runs):
+            c0 = time.perf_counter()
+            oout, ores = g.align(guess)
+            times.append(time.perf_counter() - c0)
+        cpu_ms = 1e3 * float(np.median(times))
+        result["cpu_baseline"] = {"value": round(cpu_ms, 3), "unit": "ms/scan", "cores": threads, "kind": "port",
+                                  "sample": f"{args.cpu_runs} full S2M aligns of the same cfg3 problem "
+                                            f"(median; {ores.iterations_run} iters each), OpenMP oracle "
+                                            f"oracle/cpu_ref.cpp at -O2",
+                                  "speedup_gpu_vs_cpu": round(cpu_ms / ms_per_step, 2)}
+        result["pose_delta_vs_cpu"] = {"trans_m": float(np.abs(out[:3, 3] - oout[:3, 3]).max()),
+                                       "rot_rad": rot_err(out, oout)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -119,6 +119,7 @@ def load():
         "gicp_set_profiling": (I, [P, I]),
         "gicp_debug_stats": (I, [P, I, P, S, C.POINTER(S)]),
         "gicp_get_stream": (I, [P, C.POINTER(P)]),
+        "gicp_synchronize": (I, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -295,6 +296,9 @@ class Context:
 
     def set_profiling(self, on=True):
         self._check(self.L.gicp_set_profiling(self.h, int(on)))
+
+    def synchronize(self):
+        self._check(self.L.gicp_synchronize(self.h))
 
     def stream(self) -> int:
         s = C.c_void_p()

@@ -799,6 +799,15 @@ gicp_status gicp_set_profiling(gicp_ctx* c, int enable) {
   return GICP_OK;
 }
 
+gicp_status gicp_synchronize(gicp_ctx* c) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipStreamSynchronize(c->copy_stream));
+  return GICP_OK;
+}
+
 gicp_status gicp_get_stream(const gicp_ctx* c, void** stream) {
   if (!c || !stream) return fail(GICP_EINVAL, "null argument");
   *stream = (void*)c->stream;

@@ -191,6 +191,8 @@ gicp_status gicp_set_profiling(struct gicp_ctx* ctx, int enable);
 /* Diagnostics (development): enable per 64-query-group search counters for
  * subsequent linearize launches and/or read those of the last launch. */
 gicp_status gicp_debug_stats(struct gicp_ctx* ctx, int enable, unsigned int* out, size_t max_words, size_t* nwords);
+/* Blocks until all work queued on the ctx's stream(s) has finished. */
+gicp_status gicp_synchronize(struct gicp_ctx* ctx);
 /* The ctx's HIP stream (hipStream_t) for callers that interleave their own work. */
 gicp_status gicp_get_stream(const struct gicp_ctx* ctx, void** stream);
 
