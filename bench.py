@@ -67,8 +67,9 @@ def keyframe_covariances(ctx_factory, keyframes, k=10):
 
 
 def rot_err(A, B):
-    R = A[:3, :3].astype(np.float64).T @ B[:3, :3].astype(np.float64)
-    return float(math.acos(max(-1.0, min(1.0, (np.trace(R) - 1) / 2))))
+    """Rotation angle between A and B: 2*asin(|RA - RB|_F / sqrt(8)) (well conditioned at 0)."""
+    f = float(np.linalg.norm(A[:3, :3].astype(np.float64) - B[:3, :3].astype(np.float64)))
+    return 2.0 * math.asin(min(1.0, f / math.sqrt(8.0)))
 
 
 def main():
