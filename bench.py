@@ -66,6 +66,20 @@ def keyframe_covariances(ctx_factory, keyframes, k=10):
     return np.concatenate(covs)
 
 
+def reduce_over_ranks(dist, elapsed, iters, device):
+    """Job time = MAX over ranks of the timed region; work = SUM of iterations
+    (replicas: every rank aligns its own scan stream)."""
+    if dist is None:
+        return float(elapsed), float(iters)
+    import torch
+    t = torch.tensor([elapsed, float(iters)], dtype=torch.float64, device=device)
+    tmax = t.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tsum = t.clone()
+    dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+    return float(tmax[0]), float(tsum[1])
+
+
 def rot_err(A, B):
     """Rotation angle between A and B: 2*asin(|RA - RB|_F / sqrt(8)) (well conditioned at 0)."""
     f = float(np.linalg.norm(A[:3, :3].astype(np.float64) - B[:3, :3].astype(np.float64)))
@@ -131,18 +145,7 @@ def main():
         iters += res.iterations_run
     ctx.synchronize()
     t_end = time.perf_counter()
-    elapsed = t_end - t_start
-    if dist:
-        import torch
-        t = torch.tensor([elapsed, float(iters)], dtype=torch.float64, device=f"cuda:{local_rank}")
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
-        iters_total = float(tsum[1])
-    else:
-        iters_total = float(iters)
+    elapsed, iters_total = reduce_over_ranks(dist, t_end - t_start, iters, f"cuda:{local_rank}")
     steps_total = args.steps * world
     value = iters_total / elapsed
     ms_per_step = 1e3 * elapsed / args.steps

@@ -1,0 +1,254 @@
+"""GPU parity of the GICP path (covariances, correspondences, linearization,
+LM / GN alignment, residuals) through the C-ABI, against the oracle's golden
+vectors (tests/golden/gicp_*.npz) and the live oracle.
+
+Tolerances (floating point, stated per check):
+  covariances   |d| <= 1e-12 * max|C|   (fp64, different summation order)
+  H, b, cost    rel 1e-11               (fp64 moment reduction vs per-point sums)
+  correspondences / sq. distances       bit-exact
+  poses         |d| <= 1e-6             (fp32 output of an fp64 state)
+  iterations / convergence flags        exact
+"""
+import numpy as np
+import pytest
+
+import dynamic_direct_lidar_odometry_amd as P
+import np_gicp as NP
+from dynamic_direct_lidar_odometry_amd import SOURCE, TARGET
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+S2S = dict(k_correspondences=10, max_correspondence_distance=1.0, max_iterations=32, transformation_epsilon=5e-4)
+S2M = dict(k_correspondences=20, max_correspondence_distance=2.0, max_iterations=32, transformation_epsilon=0.01)
+
+
+def s2s_ctx(g, **kw):
+    c = P.Context(0)
+    c.set_params(P.default_params(**{**S2S, **kw}))
+    c.set_target(g["tgt"])
+    c.set_source(g["src"])
+    c.set_covariances(SOURCE, g["cov_src_PLANE"])
+    c.set_covariances(TARGET, g["cov_tgt"])
+    return c
+
+
+@pytest.mark.parametrize("reg", ["NONE", "MIN_EIG", "NORMALIZED_MIN_EIG", "PLANE", "FROBENIUS"])
+def test_covariances_all_regularizations(s2s_golden, reg):
+    g = s2s_golden
+    c = P.Context(0)
+    c.set_params(P.default_params(k_correspondences=10, regularization=O.REG[reg]))
+    c.set_source(g["src"])
+    assert not c.has_covariances(SOURCE)
+    c.compute_covariances(SOURCE)
+    assert c.has_covariances(SOURCE)
+    cov = c.get_covariances(SOURCE)
+    ref = g[f"cov_src_{reg}"]
+    np.testing.assert_allclose(cov, ref, rtol=0, atol=1e-12 * max(np.abs(ref).max(), 1.0))
+
+
+@pytest.mark.parametrize("k", [5, 20, 32, 64])
+def test_covariances_other_k_vs_oracle(s2s_golden, k):
+    src = s2s_golden["src"][:3000]
+    c = P.Context(0)
+    c.set_params(P.default_params(k_correspondences=k))
+    c.set_target(src)
+    c.compute_covariances(TARGET)
+    ref = O.covariances(src, k)
+    np.testing.assert_allclose(c.get_covariances(TARGET), ref, rtol=0, atol=1e-12)
+
+
+def test_covariance_layouts_roundtrip(s2s_golden):
+    g = s2s_golden
+    c = P.Context(0)
+    c.set_source(g["src"])
+    c.set_covariances(SOURCE, g["cov_src_PLANE"])
+    m = c.get_covariances(SOURCE, P.COV_MAT4D).reshape(-1, 4, 4)
+    np.testing.assert_array_equal(NP.mat_to_sym6(m[:, :3, :3]), g["cov_src_PLANE"])
+    assert np.all(m[:, 3, :] == 0) and np.all(m[:, :, 3] == 0)   # Matrix4d with zero 4th row/col (:438)
+    c.set_covariances(SOURCE, m.reshape(-1, 16))
+    np.testing.assert_array_equal(c.get_covariances(SOURCE), g["cov_src_PLANE"])
+    with pytest.raises(P.GicpError):
+        c.set_covariances(SOURCE, g["cov_src_PLANE"][:-1])
+    c.set_source(g["src"][:100])                                  # new cloud clears covariances
+    assert not c.has_covariances(SOURCE)
+
+
+def test_linearize_vs_golden(s2s_golden):
+    g = s2s_golden
+    c = s2s_ctx(g)
+    H, b, cost, nc = c.linearize(np.eye(4))
+    corr, sqd = c.correspondences()
+    np.testing.assert_array_equal(corr, g["lin_corr"])
+    np.testing.assert_array_equal(sqd, g["lin_sqd"])
+    assert nc == int(np.sum(g["lin_corr"] >= 0))
+    np.testing.assert_allclose(H, g["lin_H"], rtol=1e-11, atol=1e-11 * np.abs(g["lin_H"]).max())
+    np.testing.assert_allclose(b, g["lin_b"], rtol=1e-11, atol=1e-11 * np.abs(g["lin_b"]).max())
+    assert abs(cost - float(g["lin_cost"])) <= 1e-11 * abs(float(g["lin_cost"]))
+
+
+def test_linearize_random_poses_vs_oracle(s2s_golden):
+    g = s2s_golden
+    c = s2s_ctx(g)
+    o = O.Gicp(g["src"], g["tgt"], O.default_params(**S2S))
+    o.set_covariances(0, g["cov_src_PLANE"])
+    o.set_covariances(1, g["cov_tgt"])
+    rng = np.random.default_rng(2)
+    for _ in range(5):
+        T = np.eye(4)
+        T[:3, :3] = NP.so3_exp(rng.normal(0, 0.03, 3))
+        T[:3, 3] = rng.normal(0, 0.2, 3)
+        H, b, cost, nc = c.linearize(T)
+        Ho, bo, co, corr, sqd = o.linearize(T)
+        gc, gs = c.correspondences()
+        np.testing.assert_array_equal(gc, corr)
+        np.testing.assert_array_equal(gs, sqd)
+        np.testing.assert_allclose(H, Ho, rtol=1e-11, atol=1e-11 * np.abs(Ho).max())
+        np.testing.assert_allclose(b, bo, rtol=1e-11, atol=1e-11 * np.abs(bo).max())
+        assert abs(cost - co) <= 1e-11 * abs(co)
+
+
+def test_align_lm_s2s_vs_golden(s2s_golden):
+    g = s2s_golden
+    c = s2s_ctx(g)
+    pose, res = c.align()
+    assert res.iterations_run == int(g["lm_iters"])
+    assert res.nr_iterations == int(g["lm_nr"])
+    assert res.converged == int(g["lm_converged"]) and not res.lm_failed
+    assert res.lm_trials == int(g["lm_trials"])
+    np.testing.assert_allclose(pose, g["lm_pose"], atol=1e-6)
+    np.testing.assert_allclose(np.array(res.final_hessian).reshape(6, 6), g["lm_hessian"], rtol=1e-9,
+                               atol=1e-9 * np.abs(g["lm_hessian"]).max())
+    corr, sqd = c.correspondences()
+    np.testing.assert_array_equal(corr, g["lm_last_corr"])
+    np.testing.assert_array_equal(sqd, g["lm_last_sqd"])
+    r = c.residuals()                                   # getResiduals: sqrt of the last sq. distances (:225-232)
+    np.testing.assert_array_equal(r, np.sqrt(g["lm_last_sqd"].astype(np.float64)))
+
+
+def test_align_gn_fixed_vs_golden(s2s_golden):
+    g = s2s_golden
+    c = s2s_ctx(g, max_iterations=10, optimizer=P.GAUSS_NEWTON, fixed_iterations=10)
+    pose, res = c.align()
+    assert res.iterations_run == 10 == int(g["gn_iters"])
+    np.testing.assert_allclose(pose, g["gn_pose"], atol=1e-6)
+
+
+def test_align_s2m_vs_golden(s2m_golden):
+    g = s2m_golden
+    c = P.Context(0)
+    c.set_params(P.default_params(**S2M))
+    c.set_target(g["sub"])
+    c.set_covariances(TARGET, g["cov_sub"])
+    c.set_source(g["src"])
+    c.set_covariances(SOURCE, g["cov_src"])
+    pose, res = c.align(g["guess"])
+    assert res.iterations_run == int(g["iters"]) and res.converged == int(g["converged"])
+    np.testing.assert_allclose(pose, g["pose"], atol=1e-6)
+    # repeated aligns are deterministic
+    pose2, res2 = c.align(g["guess"])
+    np.testing.assert_array_equal(pose, pose2)
+
+
+def test_align_computes_missing_covariances(s2s_golden):
+    """computeTransformation computes covariances that were not supplied (nano_gicp_impl.hpp:186-193)."""
+    g = s2s_golden
+    c = P.Context(0)
+    c.set_params(P.default_params(**S2S))
+    c.set_target(g["tgt"])
+    c.set_source(g["src"])
+    pose, res = c.align()
+    assert c.has_covariances(SOURCE) and c.has_covariances(TARGET)
+    np.testing.assert_allclose(c.get_covariances(SOURCE), g["cov_src_PLANE"], atol=1e-12)
+    np.testing.assert_allclose(c.get_covariances(TARGET), g["cov_tgt"], atol=1e-12)
+    assert res.iterations_run == int(g["lm_iters"])
+    np.testing.assert_allclose(pose, g["lm_pose"], atol=1e-6)
+
+
+def test_align_with_guess_and_param_variants(s2s_golden):
+    g = s2s_golden
+    rng = np.random.default_rng(9)
+    for trial in range(3):
+        kw = dict(S2S)
+        kw["max_correspondence_distance"] = [0.5, 1.0, 3.0][trial]
+        kw["transformation_epsilon"] = [1e-3, 5e-4, 1e-2][trial]
+        guess = np.eye(4, dtype=np.float32)
+        guess[:3, :3] = NP.so3_exp(rng.normal(0, 0.01, 3))
+        guess[:3, 3] = rng.normal(0, 0.1, 3)
+        c = s2s_ctx(g, **kw)
+        o = O.Gicp(g["src"], g["tgt"], O.default_params(**kw))
+        o.set_covariances(0, g["cov_src_PLANE"])
+        o.set_covariances(1, g["cov_tgt"])
+        pose, res = c.align(guess)
+        opose, ores = o.align(guess)
+        assert (res.iterations_run, res.converged, res.lm_trials) == (ores.iterations_run, ores.converged, ores.lm_trials)
+        np.testing.assert_allclose(pose, opose, atol=1e-6)
+
+
+def test_align_no_correspondences(s2s_golden):
+    """Source far from the target: zero correspondences, pose stays at the guess (as the oracle)."""
+    g = s2s_golden
+    c = P.Context(0)
+    c.set_params(P.default_params(**S2S))
+    c.set_target(g["tgt"])
+    c.set_source(g["src"] + np.float32(1000.0))
+    pose, res = c.align()
+    o = O.Gicp(g["src"] + np.float32(1000.0), g["tgt"], O.default_params(**S2S))
+    opose, ores = o.align()
+    assert res.num_correspondences == 0
+    assert (res.iterations_run, res.converged) == (ores.iterations_run, ores.converged)
+    np.testing.assert_array_equal(pose, opose)
+
+
+def test_align_errors():
+    c = P.Context(0)
+    with pytest.raises(P.GicpError) as e:
+        c.align()
+    assert e.value.status in (2, 3)                     # ENOSOURCE / ENOTARGET
+    c.set_source(np.random.default_rng(0).standard_normal((50, 3)).astype(np.float32))
+    with pytest.raises(P.GicpError) as e:
+        c.align()
+    assert e.value.status == 2                          # ENOTARGET
+    with pytest.raises(P.GicpError) as e:
+        c.residuals()
+    assert e.value.status == 7                          # ESTATE (no linearization yet)
+    c.set_target(np.random.default_rng(1).standard_normal((5, 3)).astype(np.float32))
+    with pytest.raises(P.GicpError) as e:
+        c.align()                                       # default k=20 > 5 target points
+    assert e.value.status == 4                          # ETOOFEW
+    with pytest.raises(P.GicpError):
+        c.set_params(P.default_params(k_correspondences=0))
+
+
+def test_transform_source(s2s_golden):
+    g = s2s_golden
+    c = s2s_ctx(g)
+    pose, _ = c.align()
+    out = c.transform_source()
+    ref = (g["src"].astype(np.float64) @ pose[:3, :3].T.astype(np.float64) + pose[:3, 3]).astype(np.float32)
+    np.testing.assert_allclose(out, ref, atol=2e-5)
+
+
+def test_swap_and_share(s2s_golden):
+    g = s2s_golden
+    a = s2s_ctx(g)
+    pose, _ = a.align()
+    # swapSourceAndTarget: clouds and covariances trade places (nano_gicp_impl.hpp:97-106)
+    a.swap_source_target()
+    assert a.size(SOURCE) == len(g["tgt"]) and a.size(TARGET) == len(g["src"])
+    np.testing.assert_array_equal(a.get_covariances(SOURCE), g["cov_tgt"])
+    np.testing.assert_array_equal(a.get_covariances(TARGET), g["cov_src_PLANE"])
+    inv, _ = a.align(np.linalg.inv(pose.astype(np.float64)).astype(np.float32))
+    np.testing.assert_allclose(inv @ pose, np.eye(4), atol=5e-3)
+    # shareSourceFrom: S2M uses the S2S source cloud + covariances (odom.cc:530,765)
+    b = P.Context(0)
+    b.set_params(P.default_params(**S2S))
+    b.set_target(g["src"])
+    b.set_covariances(TARGET, g["cov_src_PLANE"])
+    b.share_source_from(a)
+    np.testing.assert_array_equal(b.get_covariances(SOURCE), g["cov_tgt"])
+    p2, _ = b.align(np.linalg.inv(pose.astype(np.float64)).astype(np.float32))
+    np.testing.assert_array_equal(p2, inv)
+    # copy-on-write: new covariances on b do not change a's
+    b.set_covariances(SOURCE, g["cov_tgt"] * 2.0)
+    np.testing.assert_array_equal(a.get_covariances(SOURCE), g["cov_tgt"])

@@ -1,0 +1,134 @@
+"""GPU parity of the exact nearest-neighbour search (HIP, through the C-ABI)
+against the reference nanoflann's golden vectors and the oracle.
+
+Bar: bit-exact indices and squared distances.  Exact distance ties (duplicate
+or equidistant points) are the one documented divergence: nanoflann keeps the
+first point its traversal meets, the GPU keeps the lowest Morton position; the
+returned squared distances stay bit-identical and each returned index is a
+point at exactly that distance (DESIGN.md "Tie rule")."""
+import numpy as np
+import pytest
+
+import dynamic_direct_lidar_odometry_amd as P
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx_with_target(pts):
+    c = P.Context(0)
+    c.set_target(pts)
+    return c
+
+
+def _assert_tie_aware(pts, q, idx, sqd, gidx, gsqd):
+    """Same sorted distances as nanoflann, and every returned index is a distinct
+    point at exactly its reported distance (which point among equals may differ)."""
+    np.testing.assert_array_equal(sqd, gsqd)
+    d = q[:, None, :] - pts[idx]
+    d_of_idx = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+    np.testing.assert_array_equal(d_of_idx.astype(np.float32), sqd)
+    for r in range(len(idx)):
+        assert len(set(idx[r].tolist())) == idx.shape[1]
+    # a row whose result has no repeated distance and whose k-th distance is
+    # not repeated just outside it has a unique answer: it must match exactly
+    for r in range(len(idx)):
+        dr = pts - q[r]
+        all_d = ((dr[:, 0] * dr[:, 0] + dr[:, 1] * dr[:, 1]) + dr[:, 2] * dr[:, 2]).astype(np.float32)
+        if np.sum(all_d <= gsqd[r, -1]) == idx.shape[1]:
+            assert set(idx[r].tolist()) == set(gidx[r].tolist())
+
+
+@pytest.mark.parametrize("k", [1, 10, 20])
+def test_knn_vs_reference_golden(knn_golden, k):
+    g = knn_golden
+    q = g["scan_q"] if k == 1 else g["scan_q"][::4]
+    c = _ctx_with_target(g["scan_pts"])
+    idx, sqd = c.knn_target(q, k)
+    np.testing.assert_array_equal(idx, g[f"scan_k{k}_idx"])
+    np.testing.assert_array_equal(sqd, g[f"scan_k{k}_sqd"])
+
+
+def test_knn_self_and_far_golden(knn_golden):
+    g = knn_golden
+    c = _ctx_with_target(g["scan_pts"][:2048])
+    idx, sqd = c.knn_target(g["scan_pts"][:2048], 10)
+    np.testing.assert_array_equal(idx, g["self_k10_idx"])
+    np.testing.assert_array_equal(sqd, g["self_k10_sqd"])
+    c = _ctx_with_target(g["scan_pts"])
+    idx, sqd = c.knn_target(g["far_q"], 10)
+    np.testing.assert_array_equal(idx, g["far_k10_idx"])
+    np.testing.assert_array_equal(sqd, g["far_k10_sqd"])
+
+
+@pytest.mark.parametrize("case,k", [("dup", 10), ("lat", 1), ("lat", 10)])
+def test_knn_ties_golden(knn_golden, case, k):
+    g = knn_golden
+    pts, q = g[f"{case}_pts"], g[f"{case}_q"]
+    c = _ctx_with_target(pts)
+    idx, sqd = c.knn_target(q, k)
+    _assert_tie_aware(pts, q, idx, sqd, g[f"{case}_k{k}_idx"], g[f"{case}_k{k}_sqd"])
+
+
+@pytest.mark.parametrize("n", [1, 5, 31, 32, 33, 63, 1000, 2049, 40000])
+@pytest.mark.parametrize("k", [1, 3, 10, 16, 20, 32, 64])
+def test_knn_ragged_sizes_vs_oracle(n, k):
+    if k > n:
+        pytest.skip("k > n covered by test_knn_too_few")
+    rng = np.random.default_rng(n * 100 + k)
+    pts = (rng.standard_normal((n, 3)) * [20, 20, 3]).astype(np.float32)
+    q = (rng.standard_normal((777, 3)) * [22, 22, 4]).astype(np.float32)
+    c = _ctx_with_target(pts)
+    idx, sqd = c.knn_target(q, k)
+    oi, od = O.knn(pts, q, k)
+    np.testing.assert_array_equal(sqd, od)
+    np.testing.assert_array_equal(idx, oi)
+
+
+def test_knn_strided_pointxyzi_input(knn_golden):
+    """32-byte pcl::PointXYZI records (x, y, z, pad, intensity, pad[3]) are read in place."""
+    g = knn_golden
+    rec = np.zeros((len(g["scan_pts"]), 8), np.float32)
+    rec[:, :3] = g["scan_pts"]
+    rec[:, 3] = 1.0
+    rec[:, 4] = 7.0
+    c = _ctx_with_target(rec)
+    qrec = np.zeros((len(g["scan_q"]), 8), np.float32)
+    qrec[:, :3] = g["scan_q"]
+    idx, sqd = c.knn_target(qrec, 1)
+    np.testing.assert_array_equal(idx, g["scan_k1_idx"])
+    np.testing.assert_array_equal(sqd, g["scan_k1_sqd"])
+
+
+def test_knn_too_few_and_errors():
+    c = P.Context(0)
+    with pytest.raises(P.GicpError) as e:
+        c.knn_target(np.zeros((4, 3), np.float32), 1)
+    assert e.value.status == 2                                 # ENOTARGET
+    c.set_target(np.random.default_rng(0).standard_normal((5, 3)).astype(np.float32))
+    with pytest.raises(P.GicpError) as e:
+        c.knn_target(np.zeros((4, 3), np.float32), 10)
+    assert e.value.status == 4                                 # ETOOFEW
+    with pytest.raises(P.GicpError) as e:
+        c.knn_target(np.zeros((4, 3), np.float32), 65)
+    assert e.value.status == 1                                 # EINVAL
+    bad = np.zeros((100, 3), np.float32)
+    bad[17, 1] = np.nan
+    with pytest.raises(P.GicpError) as e:
+        c.set_target(bad)
+    assert e.value.status == 8                                 # ENONFINITE
+    with pytest.raises(P.GicpError) as e:
+        c.set_target(np.zeros((0, 3), np.float32))
+    assert e.value.status == 1
+
+
+def test_knn_large_cloud_property():
+    """500k-point target (cfg 3 size): GPU 1-NN equals the oracle on a 20k query sample."""
+    rng = np.random.default_rng(11)
+    pts = (rng.standard_normal((500_000, 3)) * [30, 30, 3]).astype(np.float32)
+    q = (rng.standard_normal((20_000, 3)) * [30, 30, 3]).astype(np.float32)
+    c = _ctx_with_target(pts)
+    idx, sqd = c.knn_target(q, 1)
+    oi, od = O.knn(pts, q, 1)
+    np.testing.assert_array_equal(sqd, od)
+    np.testing.assert_array_equal(idx, oi)
