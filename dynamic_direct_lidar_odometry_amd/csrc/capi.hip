@@ -671,6 +671,10 @@ gicp_status gicp_get_correspondences(gicp_ctx* c, int32_t* corr, float* sq_dist,
   HIP_TRY(c->tmp_out.ensure((sizeof(int) + sizeof(float)) * n + 64));
   int* dcorr = c->tmp_out.as<int>();
   float* dsqd = reinterpret_cast<float*>(c->tmp_out.as<char>() + ((sizeof(int) * n + 63) / 64) * 64);
+  // sq_distances_ holds the unbounded 1-NN distance of EVERY point
+  // (nano_gicp_impl.hpp:255-257); the bounded search left +inf for points
+  // without a match, so complete those first (same kernel as getResiduals)
+  if (sq_dist && c->tgt.cloud) launch_residuals(c->stream, c->job_dev.as<AlignJob>(), (int)n, nullptr);
   launch_export_corr(c->stream, c->job_dev.as<AlignJob>(), (int)n, dcorr, dsqd);
   HIP_TRY(hipGetLastError());
   if (corr) HIP_TRY(hipMemcpyAsync(corr, dcorr, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));

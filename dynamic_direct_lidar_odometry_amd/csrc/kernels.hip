@@ -1337,7 +1337,7 @@ __global__ __launch_bounds__(256) void k_residuals(const AlignJob* __restrict__ 
         job->sqd[i] = d2;
       }
     }
-    if (active) out[src.perm[i]] = sqrt((double)d2);
+    if (active && out) out[src.perm[i]] = sqrt((double)d2);
   }
 }
 

@@ -166,7 +166,8 @@ gicp_status gicp_align(struct gicp_ctx* ctx, const float* guess16, float* out16,
 gicp_status gicp_get_residuals(struct gicp_ctx* ctx, double* out, size_t n);
 /* correspondences_ / sq_distances_ of the last linearization, original
  * indices (-1 = no correspondence within max_correspondence_distance).
- * Unmatched points report sq_dist = +inf unless gicp_get_residuals ran. */
+ * sq_dist is the unbounded 1-NN squared distance of every point, as
+ * sq_distances_ (nano_gicp_impl.hpp:255-257), matched or not. */
 gicp_status gicp_get_correspondences(struct gicp_ctx* ctx, int32_t* corr, float* sq_dist, size_t n);
 /* pcl::transformPointCloud(*input_, output, final_transformation_)
  * (lsq_registration_impl.hpp:125); writes xyz with the given stride. */
