@@ -16,6 +16,7 @@ import dynamic_direct_lidar_odometry_amd as P
 import np_gicp as NP
 from dynamic_direct_lidar_odometry_amd import SOURCE, TARGET
 from oracle import oracle as O
+from parity import assert_cov_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -43,8 +44,7 @@ def test_covariances_all_regularizations(s2s_golden, reg):
     c.compute_covariances(SOURCE)
     assert c.has_covariances(SOURCE)
     cov = c.get_covariances(SOURCE)
-    ref = g[f"cov_src_{reg}"]
-    np.testing.assert_allclose(cov, ref, rtol=0, atol=1e-12 * max(np.abs(ref).max(), 1.0))
+    assert_cov_parity(g["src"], 10, cov, g[f"cov_src_{reg}"])
 
 
 @pytest.mark.parametrize("k", [5, 20, 32, 64])
@@ -54,8 +54,7 @@ def test_covariances_other_k_vs_oracle(s2s_golden, k):
     c.set_params(P.default_params(k_correspondences=k))
     c.set_target(src)
     c.compute_covariances(TARGET)
-    ref = O.covariances(src, k)
-    np.testing.assert_allclose(c.get_covariances(TARGET), ref, rtol=0, atol=1e-12)
+    assert_cov_parity(src, k, c.get_covariances(TARGET), O.covariances(src, k))
 
 
 def test_covariance_layouts_roundtrip(s2s_golden):

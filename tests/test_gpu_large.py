@@ -6,6 +6,7 @@ import pytest
 import dynamic_direct_lidar_odometry_amd as P
 from dynamic_direct_lidar_odometry_amd import SOURCE, TARGET, scene
 from oracle import oracle as O
+from parity import assert_cov_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -32,11 +33,11 @@ def test_cfg3_covariances_vs_oracle(cfg3):
     c.set_params(P.default_params(k_correspondences=10))
     c.set_source(cfg3["source"])
     c.compute_covariances(SOURCE)
-    np.testing.assert_allclose(c.get_covariances(SOURCE), O.covariances(cfg3["source"], 10), rtol=0, atol=1e-12)
-    for kf, lo in zip(cfg3["keyframes"][:1], [0]):
-        c.set_source(kf)
-        c.compute_covariances(SOURCE)
-        np.testing.assert_allclose(c.get_covariances(SOURCE), O.covariances(kf, 10), rtol=0, atol=1e-12)
+    assert_cov_parity(cfg3["source"], 10, c.get_covariances(SOURCE), O.covariances(cfg3["source"], 10))
+    kf = cfg3["keyframes"][0]
+    c.set_source(kf)
+    c.compute_covariances(SOURCE)
+    assert_cov_parity(kf, 10, c.get_covariances(SOURCE), O.covariances(kf, 10))
 
 
 @pytest.mark.parametrize("optimizer", ["LM", "GN20"])
