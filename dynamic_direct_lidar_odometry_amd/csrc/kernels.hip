@@ -1,14 +1,18 @@
 // kernels.hip — hand-written gfx950 kernels of the GICP hot path.
 //
 //   K1 index build      k_pack_bbox, k_bbox_final, k_morton, k_gather,
-//                       k_leaf_boxes, k_level_boxes   (radix sort: index_build.hip)
+//                       k_leaf_boxes, k_level_boxes   (radix sort: hipcub, capi.hip)
 //   K2 kNN-k covariance k_covariances<KCAP,EXACT>        calculate_covariances
 //                                                       nano_gicp_impl.hpp:373-441
-//   K3 linearize        k_linearize                     update_correspondences +
-//                                                       linearize :234-342
+//   K3 correspondences  k_nn_search<Q>                  update_correspondences
+//                                                       :234-275 (1-NN part)
+//   K4 moments          k_moments                       update_correspondences
+//                                                       (M) + linearize :277-336
 //   K5 LM / GN step     k_lm_step                       lsq_registration_impl.hpp:95-232
-//   K6 outputs          k_residuals, k_transform        getResiduals :225-232,
-//                                                       transformPointCloud lsq:125
+//                                                       (+ compute_error :339-383
+//                                                       evaluated from the moments)
+//   K6 outputs          k_residuals, k_transform,       getResiduals :225-232,
+//                       k_export_corr                   transformPointCloud lsq:125
 // Compiled with -ffp-contract=off: fp32 distance / transform arithmetic must
 // not be contracted into FMAs so that correspondences equal the oracle's.
 #include <hip/hip_runtime.h>
