@@ -86,6 +86,90 @@ def rot_err(A, B):
     return 2.0 * math.asin(min(1.0, f / math.sqrt(8.0)))
 
 
+def sharded_leg(dist, rank, world, local_rank, args):
+    """BASELINE.json configs[3] / SURVEY.md §8(e): 262,144-pt 128x2048 scan vs
+    a 2,000,000-pt 8-keyframe submap, spatially sharded over the job's GPUs
+    (slab + 2 m halo per rank, one RCCL all-reduce of the 80 moment doubles
+    per outer iteration inside the align graph).  With one GPU it is the same
+    code path with a one-rank communicator.  Reported next to the replica
+    metric; strong scaling (fixed problem), so compare across n_gpus."""
+    import dynamic_direct_lidar_odometry_amd as P
+    from dynamic_direct_lidar_odometry_amd import scene, SOURCE
+    from dynamic_direct_lidar_odometry_amd.shard import ShardedGicp
+
+    t0 = time.time()
+    prob = scene.s2m_problem(128, 2048, 8, 2000000, 4)
+    sub = np.ascontiguousarray(np.concatenate(prob["keyframes"])[prob["subset"]])
+    src = prob["source"]
+    kcov = keyframe_covariances(lambda: P.Context(local_rank), prob["keyframes"], k=10)
+    tcov = np.ascontiguousarray(kcov[prob["subset"]])
+    c = P.Context(local_rank)
+    c.set_params(P.default_params(k_correspondences=10))
+    c.set_source(src)
+    c.compute_covariances(SOURCE)
+    scov = c.get_covariances(SOURCE)
+    c.close()
+    params = P.default_params(k_correspondences=20, max_correspondence_distance=2.0, max_iterations=32,
+                              transformation_epsilon=0.01)
+    # unique id from rank 0, broadcast over the job's process group
+    uid = P.comm_unique_id() if rank == 0 else bytes(128)
+    if dist is not None:
+        obj = [uid]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
+    sh = ShardedGicp(local_rank, rank, world, uid, params)
+    slab = sh.set_target(sub, tcov)
+    sh.set_source(src, scov)
+    guess = prob["guess"].astype(np.float32)
+    log(f"[rank {rank}] sharded setup {time.time() - t0:.1f}s: src {len(src)} tgt {len(sub)} "
+        f"local {len(sh.local_index)} slab axis {slab.axis} [{slab.lo:.2f}, {slab.hi:.2f})")
+    for _ in range(2):
+        out, res = sh.align(guess)
+    sh.ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t_start = time.perf_counter()
+    iters = 0
+    for _ in range(args.sharded_steps):
+        out, res = sh.align(guess)
+        iters += res.iterations_run
+    sh.ctx.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    local_pts = len(sh.local_index)
+    graphs = sh.ctx.comm_info()[2]
+    sh.close()
+    out_leg = {"workload": "cfg4 S2M: 262,144-pt 128x2048 scan -> 2,000,000-pt 8-keyframe submap, LM, maxCorr 2.0 m",
+               "n_gpus": world, "ms_per_scan": round(1e3 * elapsed / args.sharded_steps, 4),
+               "iters_per_s": round(iters / elapsed, 2), "iterations_per_scan": res.iterations_run,
+               "converged": bool(res.converged), "target_points_per_rank_max": None,
+               "collective": "RCCL all-reduce, 80 fp64 per outer iteration" + (" (in graph)" if graphs else " (eager)"),
+               "scaling": "strong"}
+    if dist is not None:
+        import torch
+        t = torch.tensor([local_pts], dtype=torch.int64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        local_pts = int(t[0])
+    out_leg["target_points_per_rank_max"] = local_pts
+    if rank == 0:
+        # pose parity of the sharded result against the unsharded align on one GPU
+        c = P.Context(local_rank)
+        c.set_params(params)
+        c.set_target(sub)
+        c.set_covariances(1, tcov)
+        c.set_source(src)
+        c.set_covariances(0, scov)
+        ref, _ = c.align(guess)
+        c.close()
+        out_leg["pose_delta_vs_1gpu"] = {"trans_m": float(np.abs(out[:3, 3] - ref[:3, 3]).max()),
+                                         "rot_rad": rot_err(out, ref)}
+    return out_leg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,6 +177,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-runs", type=int, default=3, help="oracle align runs for cpu_baseline (median)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the spatially sharded cfg4 leg")
+    ap.add_argument("--sharded-steps", type=int, default=10)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -208,9 +294,11 @@ def main():
                                   "speedup_gpu_vs_cpu": round(cpu_ms / ms_per_step, 2)}
         result["pose_delta_vs_cpu"] = {"trans_m": float(np.abs(out[:3, 3] - oout[:3, 3]).max()),
                                        "rot_rad": rot_err(out, oout)}
+    ctx.close()
+    if not args.no_sharded:
+        result["sharded_s2m"] = sharded_leg(dist, rank, world, local_rank, args)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ctx.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

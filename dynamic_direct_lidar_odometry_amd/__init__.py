@@ -29,7 +29,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
 STATUS = {0: "GICP_OK", 1: "GICP_EINVAL", 2: "GICP_ENOTARGET", 3: "GICP_ENOSOURCE", 4: "GICP_ETOOFEW",
-          5: "GICP_EHIP", 6: "GICP_ENOMEM", 7: "GICP_ESTATE", 8: "GICP_ENONFINITE"}
+          5: "GICP_EHIP", 6: "GICP_ENOMEM", 7: "GICP_ESTATE", 8: "GICP_ENONFINITE", 9: "GICP_ECOMM"}
 
 
 class GicpError(RuntimeError):
@@ -120,6 +120,10 @@ def load():
         "gicp_debug_stats": (I, [P, I, P, S, C.POINTER(S)]),
         "gicp_get_stream": (I, [P, C.POINTER(P)]),
         "gicp_synchronize": (I, [P]),
+        "gicp_set_shard": (I, [P, I, C.c_float, C.c_float]),
+        "gicp_comm_unique_id": (I, [P, S]),
+        "gicp_set_comm": (I, [P, P, S, I, I]),
+        "gicp_get_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -147,6 +151,16 @@ def _xyz(points):
         return a, a.strides[0]
     a = np.ascontiguousarray(np.asarray(points, dtype=np.float32).reshape(-1, 3))
     return a, 12
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (128 bytes) for gicp_set_comm; make it on one rank and broadcast."""
+    L = load()
+    buf = (C.c_uint8 * 128)()
+    rc = L.gicp_comm_unique_id(C.cast(buf, C.c_void_p), 128)
+    if rc != 0:
+        raise GicpError(rc, L.gicp_last_error().decode())
+    return bytes(buf)
 
 
 class Context:
@@ -299,6 +313,22 @@ class Context:
 
     def synchronize(self):
         self._check(self.L.gicp_synchronize(self.h))
+
+    # ---- spatial sharding
+    def set_shard(self, axis: int, lo: float = -np.inf, hi: float = np.inf):
+        self._check(self.L.gicp_set_shard(self.h, int(axis), float(lo), float(hi)))
+
+    def set_comm(self, unique_id: bytes | None, nranks: int, rank: int):
+        buf = None
+        if unique_id is not None:
+            buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._check(self.L.gicp_set_comm(self.h, None if buf is None else C.cast(buf, C.c_void_p), 128,
+                                         int(nranks), int(rank)))
+
+    def comm_info(self):
+        n, r, g = C.c_int(), C.c_int(), C.c_int()
+        self._check(self.L.gicp_get_comm_info(self.h, C.byref(n), C.byref(r), C.byref(g)))
+        return n.value, r.value, bool(g.value)
 
     def stream(self) -> int:
         s = C.c_void_p()

@@ -8,6 +8,9 @@
 #include <hip/hip_runtime.h>
 
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>  // types only: RCCL is dlopen'ed on first gicp_set_comm
+
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <cfloat>
@@ -120,6 +123,49 @@ int levels_for(int n, int* cnt, int* off) {
   return L;
 }
 
+// RCCL entry points, resolved at run time so the single-GPU library carries
+// no link dependency on RCCL.  dlopen by soname: in a process that already
+// loaded torch, this returns torch's RCCL, which shares torch's HIP runtime
+// with this library (same libamdhip64.so.7 soname), so streams are compatible.
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  bool ok = false;
+  std::string why;
+};
+
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char* e = dlerror();
+      x.why = std::string("cannot load RCCL: ") + (e ? e : "?");
+      return x;
+    }
+    x.get_unique_id = (decltype(x.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    x.comm_init_rank = (decltype(x.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
+    x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
+    x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+    x.ok = x.get_unique_id && x.comm_init_rank && x.comm_destroy && x.all_reduce && x.error_string;
+    if (!x.ok) x.why = "RCCL is missing an entry point";
+    return x;
+  }();
+  return r;
+}
+
+#define NCCL_TRY(expr)                                                                      \
+  do {                                                                                      \
+    ncclResult_t _r = (expr);                                                               \
+    if (_r != ncclSuccess)                                                                  \
+      return fail(GICP_ECOMM, std::string(#expr) + ": " + rccl().error_string(_r));         \
+  } while (0)
+
 }  // namespace
 
 struct gicp_ctx {
@@ -146,6 +192,13 @@ struct gicp_ctx {
   bool profiling = false;
   std::vector<hipEvent_t> prof_ev;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // spatial sharding: ownership slab + RCCL communicator
+  int own_axis = -1;
+  float own_lo = -INFINITY, own_hi = INFINITY;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  DevBuf mom;          // [kSlabStride] reduced moments, all-reduced in place
+  bool comm_graphs = true;  // RCCL captured into the chunk graphs (else eager chunks)
 };
 
 namespace {
@@ -259,6 +312,11 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.lm_init_lambda_factor = c->params.lm_init_lambda_factor;
   j.transformation_epsilon = c->params.transformation_epsilon;
   j.rotation_epsilon = c->params.rotation_epsilon;
+  j.own_axis = c->own_axis;
+  j.own_lo = c->own_lo;
+  j.own_hi = c->own_hi;
+  j.premom = c->comm ? 1 : 0;
+  j.mom = c->mom.as<double>();
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   return GICP_OK;
 }
@@ -281,26 +339,58 @@ gicp_status prepare_align(gicp_ctx* c) {
   HIP_TRY(c->corr.ensure(sizeof(int) * ns));
   HIP_TRY(c->sqd.ensure(sizeof(float) * ns));
   HIP_TRY(c->slab.ensure(sizeof(double) * kSlabStride * linearize_blocks(ns)));
+  HIP_TRY(c->mom.ensure(sizeof(double) * kSlabStride));
   if (c->stats_on) HIP_TRY(c->stats.ensure(sizeof(unsigned int) * kStatFields * (ns + 15)));
   return GICP_OK;
 }
 
 constexpr int kChunk = 4;  // outer iterations per graph launch
 
-gicp_status capture_chunk(gicp_ctx* c, bool with_init, int nblocks, hipGraph_t* g, hipGraphExec_t* ge) {
+// One outer iteration: linearize (search + moments), then — on a sharded ctx —
+// this rank's reduced moments all-reduced across ranks (80 doubles over
+// RCCL: H, b, cost and the LM trial-cost moments in one collective), then
+// the LM/GN step, replicated bit-identically on every rank.
+gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks) {
+  launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
+  if (c->comm) {
+    launch_mom_reduce(c->stream, jd);
+    NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
+  }
+  launch_lm_step(c->stream, jd);
+  return GICP_OK;
+}
+
+gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int nblocks) {
   const AlignJob* jd = c->job_dev.as<AlignJob>();
-  HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
   if (with_init) launch_align_init(c->stream, jd);
   for (int i = 0; i < kChunk; ++i) {
-    launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
-    launch_lm_step(c->stream, jd);
+    gicp_status s = enqueue_iteration(c, jd, nblocks);
+    if (s) return s;
   }
   // publish {iter, done} to pinned host memory at the end of the chunk
-  (void)hipMemcpyAsync(c->flag_host, &c->state_dev.as<AlignState>()->iter, 2 * sizeof(int), hipMemcpyDeviceToHost,
-                       c->stream);
-  HIP_TRY(hipStreamEndCapture(c->stream, g));
+  HIP_TRY(hipMemcpyAsync(c->flag_host, &c->state_dev.as<AlignState>()->iter, 2 * sizeof(int), hipMemcpyDeviceToHost,
+                         c->stream));
+  return GICP_OK;
+}
+
+gicp_status capture_chunk(gicp_ctx* c, bool with_init, int nblocks, hipGraph_t* g, hipGraphExec_t* ge) {
+  HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  const gicp_status s = enqueue_chunk(c, with_init, nblocks);
+  const hipError_t e = hipStreamEndCapture(c->stream, g);  // always leave capture mode
+  if (s) return s;
+  HIP_TRY(e);
   HIP_TRY(hipGraphInstantiate(ge, *g, nullptr, nullptr, 0));
   return GICP_OK;
+}
+
+void drop_graphs(gicp_ctx* c) {
+  if (c->g_first) (void)hipGraphExecDestroy(c->g_first);
+  if (c->g_rest) (void)hipGraphExecDestroy(c->g_rest);
+  if (c->gg_first) (void)hipGraphDestroy(c->gg_first);
+  if (c->gg_rest) (void)hipGraphDestroy(c->gg_rest);
+  c->g_first = c->g_rest = nullptr;
+  c->gg_first = c->gg_rest = nullptr;
+  c->graph_key = std::make_tuple(-1, -1, nullptr);
 }
 
 // Launch chunks of kChunk iterations, keeping one chunk queued ahead while the
@@ -309,20 +399,29 @@ gicp_status capture_chunk(gicp_ctx* c, bool with_init, int nblocks, hipGraph_t* 
 // Returns the index of the chunk after which the state is final.
 gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chunk) {
   const void* jd = c->job_dev.p;
-  auto key = std::make_tuple(kChunk, nblocks, jd);
-  if (!c->g_first || c->graph_key != key) {
-    if (c->g_first) (void)hipGraphExecDestroy(c->g_first);
-    if (c->g_rest) (void)hipGraphExecDestroy(c->g_rest);
-    if (c->gg_first) (void)hipGraphDestroy(c->gg_first);
-    if (c->gg_rest) (void)hipGraphDestroy(c->gg_rest);
-    c->g_first = c->g_rest = nullptr;
-    c->gg_first = c->gg_rest = nullptr;
+  // key: chunk length, grid, job buffer and whether RCCL is in the chunk
+  auto key = std::make_tuple(kChunk * (c->comm ? -1 : 1), nblocks, jd);
+  const bool use_graph = !c->comm || c->comm_graphs;
+  if (use_graph && (!c->g_first || c->graph_key != key)) {
+    drop_graphs(c);
     gicp_status s = capture_chunk(c, true, nblocks, &c->gg_first, &c->g_first);
-    if (s) return s;
-    s = capture_chunk(c, false, nblocks, &c->gg_rest, &c->g_rest);
-    if (s) return s;
+    if (!s) s = capture_chunk(c, false, nblocks, &c->gg_rest, &c->g_rest);
+    if (s) {
+      drop_graphs(c);
+      (void)hipGetLastError();
+      if (!c->comm) return s;
+      c->comm_graphs = false;  // RCCL refused stream capture: launch chunks eagerly
+      return run_align_graph(c, max_it, nblocks, final_chunk);
+    }
     c->graph_key = key;
   }
+  auto launch_chunk = [&](bool first) -> gicp_status {
+    if (use_graph) {
+      HIP_TRY(hipGraphLaunch(first ? c->g_first : c->g_rest, c->stream));
+      return GICP_OK;
+    }
+    return enqueue_chunk(c, first, nblocks);
+  };
   const int nchunks = (max_it + kChunk - 1) / kChunk;
   while ((int)c->chunk_ev.size() < nchunks) {
     hipEvent_t e;
@@ -331,21 +430,27 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   }
   c->flag_host[0] = 0;
   c->flag_host[1] = 0;
-  HIP_TRY(hipGraphLaunch(c->g_first, c->stream));
+  gicp_status s = launch_chunk(true);
+  if (s) return s;
   HIP_TRY(hipEventRecord(c->chunk_ev[0], c->stream));
   int launched = 1;
   if (nchunks > 1) {
-    HIP_TRY(hipGraphLaunch(c->g_rest, c->stream));
+    s = launch_chunk(false);
+    if (s) return s;
     HIP_TRY(hipEventRecord(c->chunk_ev[1], c->stream));
     launched = 2;
   }
+  // The number of chunks launched depends only on the done flags, which the
+  // replicated LM step makes identical on every rank of a sharded align, so
+  // every rank issues the same sequence of collectives.
   int k = 0;
   for (;;) {
     HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
     const volatile int* fl = c->flag_host;
     if (fl[1] || k == nchunks - 1) break;
     if (launched < nchunks) {
-      HIP_TRY(hipGraphLaunch(c->g_rest, c->stream));
+      s = launch_chunk(false);
+      if (s) return s;
       HIP_TRY(hipEventRecord(c->chunk_ev[launched], c->stream));
       ++launched;
     }
@@ -368,6 +473,10 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i], c->stream));
     launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i + 1], c->stream));
+    if (c->comm) {
+      launch_mom_reduce(c->stream, jd);
+      NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
+    }
     launch_lm_step(c->stream, jd);
   }
   HIP_TRY(hipGetLastError());
@@ -426,10 +535,8 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   if (!c) return GICP_OK;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  if (c->g_first) (void)hipGraphExecDestroy(c->g_first);
-  if (c->g_rest) (void)hipGraphExecDestroy(c->g_rest);
-  if (c->gg_first) (void)hipGraphDestroy(c->gg_first);
-  if (c->gg_rest) (void)hipGraphDestroy(c->gg_rest);
+  drop_graphs(c);
+  if (c->comm) (void)rccl().comm_destroy(c->comm);
   for (auto e : c->prof_ev) (void)hipEventDestroy(e);
   for (auto e : c->chunk_ev) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -657,6 +764,12 @@ gicp_status gicp_get_residuals(gicp_ctx* c, double* out, size_t n) {
   HIP_TRY(c->tmp_out.ensure(sizeof(double) * n));
   launch_residuals(c->stream, c->job_dev.as<AlignJob>(), (int)n, c->tmp_out.as<double>());
   HIP_TRY(hipGetLastError());
+  // sharded: every rank holds the exact nearest distance within its tile +
+  // halo for every source point (owned matches, unbounded search otherwise);
+  // the tiles cover the whole target, so the minimum over ranks is the
+  // global 1-NN distance (nano_gicp_impl.hpp:255-257,225-232)
+  if (c->comm)
+    NCCL_TRY(rccl().all_reduce(c->tmp_out.p, c->tmp_out.p, n, ncclFloat64, ncclMin, c->comm, c->stream));
   HIP_TRY(hipMemcpyAsync(out, c->tmp_out.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return GICP_OK;
@@ -735,8 +848,8 @@ gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, doubl
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   const AlignJob* jd = c->job_dev.as<AlignJob>();
   launch_align_init(c->stream, jd);
-  launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
-  launch_lm_step(c->stream, jd);
+  s = enqueue_iteration(c, jd, nblocks);
+  if (s) return s;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -809,6 +922,63 @@ gicp_status gicp_synchronize(gicp_ctx* c) {
   if (s) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipStreamSynchronize(c->copy_stream));
+  return GICP_OK;
+}
+
+gicp_status gicp_set_shard(gicp_ctx* c, int axis, float lo, float hi) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  if (axis < -1 || axis > 2) return fail(GICP_EINVAL, "shard axis must be -1 (none), 0, 1 or 2");
+  if (axis >= 0 && !(lo < hi)) return fail(GICP_EINVAL, "empty shard range");
+  c->own_axis = axis;
+  c->own_lo = axis >= 0 ? lo : -INFINITY;
+  c->own_hi = axis >= 0 ? hi : INFINITY;
+  invalidate_align(c);
+  return GICP_OK;
+}
+
+gicp_status gicp_comm_unique_id(uint8_t* out, size_t nbytes) {
+  if (!out || nbytes < sizeof(ncclUniqueId)) return fail(GICP_EINVAL, "unique id buffer must hold 128 bytes");
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(GICP_ECOMM, r.why);
+  ncclUniqueId id;
+  NCCL_TRY(r.get_unique_id(&id));
+  std::memcpy(out, &id, sizeof(id));
+  return GICP_OK;
+}
+
+gicp_status gicp_set_comm(gicp_ctx* c, const uint8_t* id, size_t nbytes, int nranks, int rank) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->comm) {
+    (void)rccl().comm_destroy(c->comm);
+    c->comm = nullptr;
+  }
+  drop_graphs(c);
+  c->nranks = 1;
+  c->rank = 0;
+  c->comm_graphs = true;
+  if (nranks == 0) return GICP_OK;  // detach
+  if (!id || nbytes < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(GICP_EINVAL, "invalid communicator arguments");
+  const Rccl& r = rccl();
+  if (!r.ok) return fail(GICP_ECOMM, r.why);
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCL_TRY(r.comm_init_rank(&c->comm, nranks, uid, rank));
+  HIP_TRY(c->mom.ensure(sizeof(double) * kSlabStride));
+  c->nranks = nranks;
+  c->rank = rank;
+  invalidate_align(c);
+  return GICP_OK;
+}
+
+gicp_status gicp_get_comm_info(const gicp_ctx* c, int* nranks, int* rank, int* graphs) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  if (nranks) *nranks = c->comm ? c->nranks : 0;
+  if (rank) *rank = c->rank;
+  if (graphs) *graphs = (!c->comm || c->comm_graphs) ? 1 : 0;
   return GICP_OK;
 }
 

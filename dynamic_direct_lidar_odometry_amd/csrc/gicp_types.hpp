@@ -91,6 +91,16 @@ struct AlignJob {
   double lm_init_lambda_factor;
   double transformation_epsilon;
   double rotation_epsilon;
+  // Spatial sharding: this rank owns the source points
+  // whose transformed coordinate q[own_axis] lies in [own_lo, own_hi); its
+  // target holds that slab plus a max_corr halo.  own_axis < 0: unsharded.
+  int own_axis;
+  float own_lo, own_hi;
+  // premom = 1: k_mom_reduce writes this rank's reduced moments to mom, the
+  // host's collective sums them across ranks in place, and k_lm_step reads
+  // mom instead of reducing the slab itself.
+  int premom;
+  double* mom;             // [kSlabStride]
 };
 
 }  // namespace ddlo

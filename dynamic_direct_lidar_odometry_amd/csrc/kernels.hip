@@ -699,6 +699,8 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
   const float cap2 = job->cap2;
   const double max_corr2 = job->max_corr2;
   const int have_prev = st->have_prev;
+  const int own_axis = job->own_axis;
+  const float own_lo = job->own_lo, own_hi = job->own_hi;
   float Rf[9], tf[3];
   for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
   for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
@@ -722,13 +724,27 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const int i = g * Q + qi;
-    const bool active = i < src.n;
-    const int ic = active ? i : src.n - 1;
+    const bool inrange = i < src.n;
+    const int ic = inrange ? i : src.n - 1;
     const float4 a = ldg4(src.pts, ic);
     // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
+    // spatial sharding: search only the queries this rank owns
+    const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
+    const bool active = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi));
+    if (!__any(active)) {
+      if (inrange && lane < Q) {
+        corr[i] = -1;
+        sqd[i] = INFINITY;
+      }
+      if (stats && lane == 0) {
+        unsigned int* o = stats + (size_t)g * kStatFields;
+        for (int f = 0; f < kStatFields; ++f) o[f] = 0;
+      }
+      continue;
+    }
     NNVisitor<Q> vis;
     vis.qx = qx;
     vis.qy = qy;
@@ -799,9 +815,9 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
     vis.st_scan = cst[3];
     vis.st_splits = cst[4];
     const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
-    if (active && lane < Q) {
+    if (inrange && lane < Q) {
       corr[i] = valid ? vis.bestj : -1;
-      sqd[i] = vis.bestj >= 0 ? vis.best : INFINITY;
+      sqd[i] = active && vis.bestj >= 0 ? vis.best : INFINITY;
     }
     if (stats && lane == 0) {
       const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
@@ -1128,22 +1144,9 @@ constexpr int kMaxTrials = 64;
 constexpr int kMomBlocksMax = 128;                      // moment-kernel blocks (slab rows)
 constexpr int kLmRowsPerPart = (kMomBlocksMax + 5) / 6;  // slab rows per reducer thread
 
-// One workgroup: (1) fixed-order reduction of the linearize partials,
-// (2) H and b one entry per thread, (3) every LM trial in its own thread —
-// the reference's trial sequence is fully determined up front (lambda_i =
-// nu_{i-1} lambda_{i-1}, nu doubling: lsq_registration_impl.hpp:187-223), so
-// trial i is evaluated with exactly the lambda the sequential loop would use,
-// (4) thread 0 replays the sequential accept/reject decisions.
-__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job) {
-  AlignState* st = job->state;
-  if (__builtin_amdgcn_readfirstlane(st->done)) return;
-  __shared__ double part[6][kSlabStride];
-  __shared__ double mom[kSlabStride];
-  __shared__ double Hs[36], bs[6];
-  __shared__ double tr_rho[kMaxTrials], tr_lambda[kMaxTrials];
-  __shared__ double tr_R[kMaxTrials][9], tr_t[kMaxTrials][3];
-  __shared__ int tr_conv[kMaxTrials];
-  __shared__ double lambda0_s;
+// Fixed-order reduction of the linearize slab (nblocks x kSlabStride) into
+// mom[kSlabStride] by one workgroup of >= 6 * kSlabStride threads.
+__device__ __forceinline__ void reduce_slab(const AlignJob* job, double (*part)[kSlabStride], double* mom) {
   const int tid = threadIdx.x;
   const int nb = job->nblocks;
   const auto slab = gp(job->slab);
@@ -1168,6 +1171,42 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
     mom[tid] = s;
   }
   __syncthreads();
+}
+
+// K5a (sharded align only): this rank's reduced moments -> job->mom, which
+// the host's all-reduce then sums across ranks before k_lm_step.
+__global__ __launch_bounds__(kLmThreads) void k_mom_reduce(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  __shared__ double part[6][kSlabStride];
+  __shared__ double mom[kSlabStride];
+  reduce_slab(job, part, mom);
+  if (threadIdx.x < kSlabStride) gpw(job->mom)[threadIdx.x] = mom[threadIdx.x];
+}
+
+// One workgroup: (1) fixed-order reduction of the linearize partials,
+// (2) H and b one entry per thread, (3) every LM trial in its own thread —
+// the reference's trial sequence is fully determined up front (lambda_i =
+// nu_{i-1} lambda_{i-1}, nu doubling: lsq_registration_impl.hpp:187-223), so
+// trial i is evaluated with exactly the lambda the sequential loop would use,
+// (4) thread 0 replays the sequential accept/reject decisions.
+__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  __shared__ double part[6][kSlabStride];
+  __shared__ double mom[kSlabStride];
+  __shared__ double Hs[36], bs[6];
+  __shared__ double tr_rho[kMaxTrials], tr_lambda[kMaxTrials];
+  __shared__ double tr_R[kMaxTrials][9], tr_t[kMaxTrials][3];
+  __shared__ int tr_conv[kMaxTrials];
+  __shared__ double lambda0_s;
+  const int tid = threadIdx.x;
+  if (job->premom) {  // moments already reduced (and summed across shards)
+    if (tid < kSlabStride) mom[tid] = gp((const double*)job->mom)[tid];
+    __syncthreads();
+  } else {
+    reduce_slab(job, part, mom);
+  }
   const Moments mo{mom};
   if (tid < 42) {
     const double v = normal_eq_entry(mo, tid);
@@ -1445,6 +1484,7 @@ int moment_blocks(int nsrc) {
   return std::max(1, std::min((groups + kMomWaves - 1) / kMomWaves, kMomBlocksMax));
 }
 void launch_lm_step(hipStream_t s, const AlignJob* job) { k_lm_step<<<1, kLmThreads, 0, s>>>(job); }
+void launch_mom_reduce(hipStream_t s, const AlignJob* job) { k_mom_reduce<<<1, kLmThreads, 0, s>>>(job); }
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out) {
   k_residuals<<<group_blocks(nsrc), 256, 0, s>>>(job, out);
 }

@@ -26,6 +26,7 @@ void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks,
 int search_queries_per_wave();
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
 void launch_lm_step(hipStream_t s, const AlignJob* job);
+void launch_mom_reduce(hipStream_t s, const AlignJob* job);  // sharded align: slab -> job->mom
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out);
 void launch_transform(hipStream_t s, const float4* pts, int n, const int* perm, const float* T16, float* out,
                       size_t stride_floats);

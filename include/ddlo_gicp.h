@@ -40,7 +40,8 @@ typedef enum gicp_status {
   GICP_ENOMEM = 6,      /* device allocation failed                          */
   GICP_ESTATE = 7,      /* call not valid in the current state (e.g. residuals
                            requested before any align)                       */
-  GICP_ENONFINITE = 8   /* cloud contains NaN/Inf coordinates                 */
+  GICP_ENONFINITE = 8,  /* cloud contains NaN/Inf coordinates                 */
+  GICP_ECOMM = 9        /* RCCL missing or a collective failed (sharded align) */
 } gicp_status;
 
 /* Same order as nano_gicp::RegularizationMethod (gicp/gicp_settings.hpp:47-54). */
@@ -196,6 +197,29 @@ gicp_status gicp_debug_stats(struct gicp_ctx* ctx, int enable, unsigned int* out
 gicp_status gicp_synchronize(struct gicp_ctx* ctx);
 /* The ctx's HIP stream (hipStream_t) for callers that interleave their own work. */
 gicp_status gicp_get_stream(const struct gicp_ctx* ctx, void** stream);
+
+/* ---- spatially sharded align (no reference counterpart:
+ * the reference aligns on one host, nano_gicp_impl.hpp:277-342 summing
+ * per-thread H/b partials, which here become per-GPU partials) ------------
+ * Rank r of N holds the target points of its slab [lo, hi) along `axis`
+ * plus a halo of max_correspondence_distance on both sides (and their
+ * covariances, computed on the full cloud), and the whole source.  Each
+ * outer iteration it searches only the source points whose transformed
+ * coordinate falls in its slab, reduces their moments, all-reduces the 80
+ * moment doubles over RCCL (ncclSum, fp64) and runs the identical LM step,
+ * so every rank returns the same pose.  Exact: any target point within
+ * max_corr of an owned query lies in the slab + halo. */
+/* Ownership slab of this ctx; axis -1 removes it. */
+gicp_status gicp_set_shard(struct gicp_ctx* ctx, int axis, float lo, float hi);
+/* ncclGetUniqueId (128 bytes) — call on one rank and broadcast. */
+gicp_status gicp_comm_unique_id(uint8_t* out, size_t nbytes);
+/* ncclCommInitRank on the ctx's device (collective over the nranks ranks);
+ * nranks = 0 detaches.  With a communicator, align / linearize all-reduce
+ * the moments and get_residuals all-reduces (min) the residuals. */
+gicp_status gicp_set_comm(struct gicp_ctx* ctx, const uint8_t* id, size_t nbytes, int nranks, int rank);
+/* nranks (0 = no communicator), rank, and whether the collective is captured
+ * in the align graphs (1) or launched eagerly (0). */
+gicp_status gicp_get_comm_info(const struct gicp_ctx* ctx, int* nranks, int* rank, int* graphs);
 
 #ifdef __cplusplus
 }

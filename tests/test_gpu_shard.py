@@ -1,0 +1,111 @@
+"""GPU parity of the spatially sharded S2M path through the C-ABI.
+
+One GPU cannot host two RCCL ranks, so the multi-rank logic and the RCCL
+plumbing are checked separately:
+  * N shard contexts on one device (no communicator): their linearize
+    moments add up to the unsharded moments (fp64, rel 1e-10: only the
+    summation order differs), matched counts exactly, and every owned
+    query's correspondence equals the unsharded one (same squared distance,
+    bit-exact; same target point up to exact-distance ties);
+  * a one-rank RCCL communicator: the align graph with the all-reduce
+    inside returns the bit-identical pose, iteration count and residuals
+    of the plain align.
+"""
+import numpy as np
+import pytest
+
+import dynamic_direct_lidar_odometry_amd as P
+from conftest import load_golden
+from dynamic_direct_lidar_odometry_amd import SOURCE, TARGET
+from dynamic_direct_lidar_odometry_amd.shard import ShardedGicp, halo_indices, owner_of, plan_slabs
+import np_gicp as NP
+
+pytestmark = pytest.mark.gpu
+
+S2M = dict(k_correspondences=20, max_correspondence_distance=2.0, max_iterations=32, transformation_epsilon=0.01)
+
+
+def full_ctx(g):
+    c = P.Context(0)
+    c.set_params(P.default_params(**S2M))
+    c.set_target(g["sub"])
+    c.set_source(g["src"])
+    c.set_covariances(SOURCE, g["cov_src"])
+    c.set_covariances(TARGET, g["cov_sub"])
+    return c
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_shard_moments_add_up(world):
+    g = load_golden("gicp_s2m.npz")
+    pose = g["guess"].astype(np.float64)
+    full = full_ctx(g)
+    H, b, cost, nc = full.linearize(pose)
+    mom = full.moments()
+    fcorr, fsqd = full.correspondences()
+    slabs = plan_slabs(g["sub"], world)
+    own = owner_of(NP.transform_f32(pose, g["src"]), slabs)
+    tot = np.zeros(80)
+    ntot = 0
+    for r, s in enumerate(slabs):
+        idx = halo_indices(g["sub"], s, S2M["max_correspondence_distance"])
+        c = P.Context(0)
+        c.set_params(P.default_params(**S2M))
+        c.set_target(g["sub"][idx])
+        c.set_source(g["src"])
+        c.set_covariances(SOURCE, g["cov_src"])
+        c.set_covariances(TARGET, g["cov_sub"][idx])
+        c.set_shard(s.axis, s.lo, s.hi)
+        _, _, _, n_r = c.linearize(pose)
+        tot += c.moments()
+        ntot += n_r
+        corr, sqd = c.correspondences()
+        mine = own == r
+        # owned queries: same exact distance; same point unless an exact tie
+        np.testing.assert_array_equal(sqd[mine], fsqd[mine])
+        gc = np.where(corr >= 0, idx[np.maximum(corr, 0)], -1)
+        diff = mine & (gc != fcorr)
+        if diff.any():
+            q = NP.transform_f32(pose, g["src"][diff])
+            d_alt = NP.nanoflann_sqd(q, g["sub"][gc[diff]])
+            np.testing.assert_array_equal(d_alt, fsqd[diff])
+        c.close()
+    assert ntot == nc
+    np.testing.assert_allclose(tot[:74], mom[:74], rtol=1e-10, atol=1e-10 * np.abs(mom[:74]).max())
+    full.close()
+
+
+def test_comm1_align_identical_to_plain():
+    g = load_golden("gicp_s2m.npz")
+    plain = full_ctx(g)
+    out0, r0 = plain.align(g["guess"])
+    res0 = plain.residuals()
+    uid = P.comm_unique_id()
+    sh = ShardedGicp(0, 0, 1, uid, P.default_params(**S2M))
+    assert sh.ctx.comm_info()[0] == 1
+    sh.set_target(g["sub"], g["cov_sub"])
+    assert sh.slab.lo == -np.inf and sh.slab.hi == np.inf
+    sh.set_source(g["src"], g["cov_src"])
+    out1, r1 = sh.align(g["guess"])
+    np.testing.assert_array_equal(out1, out0)
+    assert (r1.iterations_run, r1.converged, r1.lm_trials) == (r0.iterations_run, r0.converged, r0.lm_trials)
+    np.testing.assert_array_equal(np.array(r1.final_hessian), np.array(r0.final_hessian))
+    np.testing.assert_array_equal(sh.residuals(), res0)
+    # a second align reuses the captured graphs
+    out2, _ = sh.align(g["guess"])
+    np.testing.assert_array_equal(out2, out0)
+    print("comm graphs:", sh.ctx.comm_info())
+    sh.close()
+    plain.close()
+
+
+def test_shard_arguments_rejected():
+    c = P.Context(0)
+    with pytest.raises(P.GicpError):
+        c.set_shard(3, 0.0, 1.0)
+    with pytest.raises(P.GicpError):
+        c.set_shard(0, 1.0, 1.0)
+    c.set_shard(-1)
+    with pytest.raises(P.GicpError):
+        c.set_comm(b"\0" * 128, 2, 5)
+    c.close()

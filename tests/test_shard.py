@@ -1,0 +1,121 @@
+"""Spatial sharding of the S2M align — host logic on CPU.
+
+* slab planning is a partition of the line (every fp32 query has exactly one
+  owner) and count-balanced;
+* the halo makes every bounded 1-NN of an owned query local to its rank;
+* the per-rank moment sums of a 2-rank gloo job add up to the unsharded
+  linearization (np_gicp restatement of nano_gicp_impl.hpp:234-342):
+  H, b, cost within rel 1e-9 (fp64, different summation order), matched
+  counts exact.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import np_gicp as NP
+from conftest import load_golden
+from dynamic_direct_lidar_odometry_amd.shard import halo_indices, owner_of, plan_slabs
+
+
+def test_plan_slabs_partition_and_balance():
+    rng = np.random.default_rng(0)
+    pts = (rng.standard_normal((10007, 3)) * [30, 10, 2]).astype(np.float32)
+    for n in (1, 2, 3, 8):
+        slabs = plan_slabs(pts, n)
+        assert all(s.axis == 0 for s in slabs)
+        assert slabs[0].lo == -np.inf and slabs[-1].hi == np.inf
+        for a, b in zip(slabs, slabs[1:]):
+            assert a.hi == b.lo and np.float32(a.hi) == a.hi
+        own = owner_of(pts, slabs)
+        counts = np.bincount(own, minlength=n)
+        assert counts.sum() == len(pts)
+        assert counts.max() - counts.min() <= 2
+        # boundary values belong to exactly one slab (half-open ranges)
+        q = np.array([[s.lo, 0, 0] for s in slabs[1:]], np.float32)
+        if len(q):
+            np.testing.assert_array_equal(owner_of(q, slabs), np.arange(1, n))
+
+
+def test_halo_contains_every_bounded_neighbour():
+    g = load_golden("gicp_s2m.npz")
+    sub, src = g["sub"], g["src"]
+    max_corr = 2.0
+    q = NP.transform_f32(g["guess"], src)
+    for n in (2, 4, 8):
+        slabs = plan_slabs(sub, n)
+        own = owner_of(q, slabs)
+        for r, s in enumerate(slabs):
+            idx = set(halo_indices(sub, s, max_corr).tolist())
+            qs = q[own == r]
+            d = NP.nanoflann_sqd(qs[:, None, :], sub[None, :, :])
+            ii, jj = np.nonzero(d.astype(np.float64) < max_corr ** 2)
+            assert set(jj.tolist()) <= idx
+
+
+def _shard_moments(g, rank, world, pose, max_corr):
+    src, sub = g["src"], g["sub"]
+    ca, cb = NP.sym6_to_mat(g["cov_src"]), NP.sym6_to_mat(g["cov_sub"])
+    slabs = plan_slabs(sub, world)
+    idx = halo_indices(sub, slabs[rank], max_corr)
+    own = owner_of(NP.transform_f32(pose, src), slabs) == rank
+    prob = NP.Problem(src[own], sub[idx], ca[own], cb[idx], max_corr)
+    H, b, cost = prob.linearize(pose)
+    return np.concatenate([H.ravel(), b, [cost, float((prob.corr >= 0).sum())]])
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = load_golden("gicp_s2m.npz")
+    v = torch.from_numpy(_shard_moments(g, rank, world, g["guess"], 2.0))
+    dist.all_reduce(v)          # the one collective of a sharded iteration
+    q.put((rank, v.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_linearize_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = load_golden("gicp_s2m.npz")
+    full = NP.Problem(g["src"], g["sub"], NP.sym6_to_mat(g["cov_src"]), NP.sym6_to_mat(g["cov_sub"]), 2.0)
+    H, b, cost = full.linearize(g["guess"])
+    for r in (0, 1):
+        v = res[r]
+        np.testing.assert_allclose(v[:36].reshape(6, 6), H, rtol=1e-9, atol=1e-9 * np.abs(H).max())
+        np.testing.assert_allclose(v[36:42], b, rtol=1e-9, atol=1e-9 * np.abs(b).max())
+        assert v[42] == pytest.approx(cost, rel=1e-9)
+        assert v[43] == (full.corr >= 0).sum()
+    np.testing.assert_array_equal(res[0], res[1])   # every rank sees the same sums
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_sharded_linearize_sum_more_ranks(world):
+    g = load_golden("gicp_s2m.npz")
+    pose = g["guess"]
+    tot = sum(_shard_moments(g, r, world, pose, 2.0) for r in range(world))
+    full = NP.Problem(g["src"], g["sub"], NP.sym6_to_mat(g["cov_src"]), NP.sym6_to_mat(g["cov_sub"]), 2.0)
+    H, b, cost = full.linearize(pose)
+    np.testing.assert_allclose(tot[:36].reshape(6, 6), H, rtol=1e-9, atol=1e-9 * np.abs(H).max())
+    assert tot[43] == (full.corr >= 0).sum()
