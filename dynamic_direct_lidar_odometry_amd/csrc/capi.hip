@@ -16,6 +16,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -198,6 +199,7 @@ struct gicp_ctx {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   DevBuf mom;          // [kSlabStride] reduced moments, all-reduced in place
+  DevBuf unres;        // phase-B search state: [defer_key u64 x n][defer_mask u64 x groups]
   bool comm_graphs = true;  // RCCL captured into the chunk graphs (else eager chunks)
 };
 
@@ -283,6 +285,17 @@ gicp_status compute_cov(gicp_ctx* c, Side& side) {
 
 void invalidate_align(gicp_ctx* c) { c->have_align = false; }
 
+// Tuning knobs of the tile search (development; defaults are the tuned values)
+constexpr float kTileR0Default = 0.25f;
+constexpr float kSplitExtentDefault = 3.0f;
+float env_float(const char* name, float dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  const float f = std::strtof(v, &end);
+  return (end && end != v && f > 0.f) ? f : dflt;
+}
+
 gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   AlignJob& j = *c->job_host;
   std::memset(&j, 0, sizeof(j));
@@ -315,8 +328,16 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.own_axis = c->own_axis;
   j.own_lo = c->own_lo;
   j.own_hi = c->own_hi;
+  j.tile_r0 = env_float("DDLO_TILE_R0", kTileR0Default);
+  j.split_extent = env_float("DDLO_SPLIT_EXTENT", kSplitExtentDefault);
   j.premom = c->comm ? 1 : 0;
   j.mom = c->mom.as<double>();
+  {
+    const size_t ns = (size_t)c->src.cloud->n;
+    char* u = c->unres.as<char>();
+    j.defer_key = reinterpret_cast<unsigned long long*>(u);
+    j.defer_mask = reinterpret_cast<unsigned long long*>(u + sizeof(unsigned long long) * ns);
+  }
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   return GICP_OK;
 }
@@ -340,7 +361,11 @@ gicp_status prepare_align(gicp_ctx* c) {
   HIP_TRY(c->sqd.ensure(sizeof(float) * ns));
   HIP_TRY(c->slab.ensure(sizeof(double) * kSlabStride * linearize_blocks(ns)));
   HIP_TRY(c->mom.ensure(sizeof(double) * kSlabStride));
-  if (c->stats_on) HIP_TRY(c->stats.ensure(sizeof(unsigned int) * kStatFields * (ns + 15)));
+  HIP_TRY(c->unres.ensure(sizeof(unsigned long long) * ((size_t)ns + (size_t)ns / 64 + 2)));
+  if (c->stats_on) {
+    HIP_TRY(c->stats.ensure(sizeof(unsigned int) * kStatFields * (ns + 15)));
+    HIP_TRY(hipMemsetAsync(c->stats.p, 0, c->stats.bytes, c->stream));
+  }
   return GICP_OK;
 }
 
@@ -903,7 +928,8 @@ gicp_status gicp_debug_stats(gicp_ctx* c, int enable, unsigned int* out, size_t 
   c->stats_on = enable != 0;
   if (out && c->src.cloud && c->stats.p) {
     const int q = search_queries_per_wave();
-    const size_t words = std::min(max_words, (size_t)kStatFields * ((c->src.cloud->n + q - 1) / q));
+    const size_t groups = (c->src.cloud->n + q - 1) / q;
+    const size_t words = std::min(max_words, (size_t)kStatFields * (groups + (groups + 3) / 4));  // phase A + B rows
     HIP_TRY(hipMemcpy(out, c->stats.p, sizeof(unsigned int) * words, hipMemcpyDeviceToHost));
     if (nwords) *nwords = words;
   }

@@ -101,6 +101,12 @@ struct AlignJob {
   // mom instead of reducing the slab itself.
   int premom;
   double* mom;             // [kSlabStride]
+  // phase B of the correspondence search: per 64-query group, the mask of
+  // lanes phase A could not resolve; per source point, their (best, bestj)
+  float tile_r0;           // phase-A radius of the tile search (m)
+  float split_extent;      // sub-range split threshold of a wave's union box (m)
+  unsigned long long* defer_mask;  // [ceil(n_src / 64)]
+  unsigned long long* defer_key;   // [n_src]
 };
 
 }  // namespace ddlo

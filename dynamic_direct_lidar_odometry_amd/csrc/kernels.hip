@@ -17,8 +17,12 @@
 // not be contracted into FMAs so that correspondences equal the oracle's.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "gicp_types.hpp"
 #include "search.hpp"
+#include "tile_search.hpp"
 #include "launch.hpp"
 
 #include <algorithm>
@@ -662,6 +666,7 @@ __device__ __forceinline__ void load_sym6(const __attribute__((address_space(1))
 constexpr int kLinWaves = 4;      // waves per block (search and moment kernels)
 constexpr float kOptR2 = 0.25f;     // optimistic first-pass radius^2 (0.5 m)
 constexpr int kSearchQ = 16;        // queries per wavefront in the correspondence search
+constexpr int kSeedW = 4;           // Morton-window seed points per slice lane
 
 __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
@@ -678,6 +683,7 @@ __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__
     st->num_corr = 0;
     st->have_prev = 0;
     st->final_cost = 0.0;
+
   }
 }
 
@@ -790,12 +796,21 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
     const bool need_seed = active && !seeded;
     bool again = false;
     if (__any(need_seed)) {
+      // Morton window of kSeedW points per slice lane (64/Q * kSeedW per query)
       const int pos = group_lower_bound<Q>(tgt.keys, tgt.n, morton_key(qx, qy, qz, tgt.quant));
       const int s = lane / Q;
-      const int cand = min(max(pos - (64 / Q) / 2 + s, 0), tgt.n - 1);
-      const float4 p = ldg4(tgt.pts, cand);
-      const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
-      unsigned long long bk = need_seed ? dkey(d, cand) : dkey(vis.best, vis.bestj);
+      const int w0 = pos - (64 / Q) * kSeedW / 2 + s * kSeedW;
+      unsigned long long bk = dkey(vis.best, vis.bestj);
+      float4 p[kSeedW];
+#pragma unroll
+      for (int k = 0; k < kSeedW; ++k) p[k] = ldg4(tgt.pts, min(max(w0 + k, 0), tgt.n - 1));
+      if (need_seed) {
+#pragma unroll
+        for (int k = 0; k < kSeedW; ++k) {
+          const int cand = min(max(w0 + k, 0), tgt.n - 1);
+          bk = umin64(bk, dkey(dist2(qx, qy, qz, p[k].x, p[k].y, p[k].z), cand));
+        }
+      }
       vis.merge_slices(bk);
       if (need_seed) {
         const float bd = __uint_as_float((unsigned)(bk >> 32));
@@ -805,6 +820,29 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
         }
       }
       again = need_seed;
+    }
+    // Group sharing: every query also takes the exact distance to the other
+    // queries' candidate points (Morton-adjacent queries are spatially
+    // adjacent, so a neighbour's candidate is often far closer than the
+    // query's own).  Valid (distance, position) pairs only: exactness kept.
+    {
+      const unsigned long long donors = __ballot(lane < Q && active && vis.bestj >= 0);
+      if (donors && __any(active)) {
+        const float4 bp = ldg4(tgt.pts, max(vis.bestj, 0));
+        unsigned long long bk = dkey(vis.best, vis.bestj);
+        unsigned long long m = donors;
+        while (m) {
+          const int k = __builtin_ctzll(m);
+          m &= m - 1;
+          const float sx = readlane_f(bp.x, k), sy = readlane_f(bp.y, k), sz = readlane_f(bp.z, k);
+          const int sj = readlane_i(vis.bestj, k);
+          bk = umin64(bk, dkey(dist2(qx, qy, qz, sx, sy, sz), sj));
+        }
+        if (active) {
+          vis.best = __uint_as_float((unsigned)(bk >> 32));
+          vis.bestj = (int)(unsigned)bk;
+        }
+      }
     }
     const unsigned long long skey = gp(src.keys)[ic];
     unsigned cst[6] = {0, 0, 0, 0, 0, 0};
@@ -831,6 +869,224 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
       o[6] = (unsigned)__popcll(__ballot(again)) | (vis.st_splits << 16);
       o[7] = 1;
     }
+  }
+}
+
+// K3 (tile search): phase A.  One wavefront per 64 sorted source points.
+__global__ __launch_bounds__(256) void k_nn_tile_a(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  const CloudDev src = job->src;
+  const CloudDev tgt = job->tgt;
+  const auto corr = gpw(job->corr);
+  const auto sqd = gpw(job->sqd);
+  unsigned int* const stats = job->stats;
+  const float cap2 = job->cap2;
+  const double max_corr2 = job->max_corr2;
+  const int have_prev = st->have_prev;
+  const int own_axis = job->own_axis;
+  const float own_lo = job->own_lo, own_hi = job->own_hi;
+  float Rf[9], tf[3], Rp[9], tp[3];
+  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
+  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
+  for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
+  for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
+
+  const int lane = lane_id();
+  const int wib = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  TileLds* L = reinterpret_cast<TileLds*>(dsm) + wib;
+  f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kTileLdsBytes);
+  fill_upper(tgt, upper);
+  __syncthreads();
+  const int ngroups = (src.n + 63) >> 6;
+  for (int g = blockIdx.x * kLinWaves + wib; g < ngroups; g += gridDim.x * kLinWaves) {
+    const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    const int i = g * 64 + lane;
+    const bool inrange = i < src.n;
+    const int ic = inrange ? i : src.n - 1;
+    // independent loads issued together
+    const float4 a = ldg4(src.pts, ic);
+    const int jprev = have_prev ? corr[ic] : -1;
+    const float dprev = have_prev ? sqd[ic] : 0.f;
+    const unsigned long long key = gp(src.keys)[ic];
+    // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
+    const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
+    const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
+    const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
+    const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
+    const bool active = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi));
+    // upper bound of the 1-NN distance: NN(q) <= |q - p_prev| <= sqrt(sqd_prev) + |q - q_prev|
+    float b = cap2;
+    if (active && jprev >= 0) {
+      const float qpx = (Rp[0] * a.x + Rp[1] * a.y) + (Rp[2] * a.z + tp[0]);
+      const float qpy = (Rp[3] * a.x + Rp[4] * a.y) + (Rp[5] * a.z + tp[1]);
+      const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
+      const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
+      const double r = sqrt((double)dprev) + sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
+      const double b2 = r * r * (1.0 + 1e-5) + 1e-12;   // fp64 with an upward margin
+      if (b2 < (double)cap2) b = __uint_as_float(__float_as_uint((float)b2) + 1);
+    }
+    const unsigned long long tm1 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    TileSearch ts;
+    ts.c = tgt;
+    ts.L = L;
+    ts.U = upper;
+    ts.nup = upper_count(tgt);
+    ts.qx = qx;
+    ts.qy = qy;
+    ts.qz = qz;
+    ts.active = active;
+    ts.cap = job->tile_r0 * job->tile_r0;
+    ts.split_ext = job->split_extent;
+    ts.best = b;
+    ts.bestj = -1;
+    ts.bx = ts.by = ts.bz = 0.f;
+    if (__any(active)) ts.run(key);
+    const bool resolved = ts.best <= fminf(b, ts.cap);
+    // deferred lanes: tighten their bound with the resolved neighbours' points
+    ts.seed_from_lanes(active && !resolved, __ballot(active && resolved && ts.bestj >= 0));
+    if (inrange) {
+      if (!active) {
+        corr[i] = -1;
+        sqd[i] = INFINITY;
+      } else if (resolved) {
+        corr[i] = (ts.bestj >= 0 && (double)ts.best < max_corr2) ? ts.bestj : -1;
+        sqd[i] = ts.bestj >= 0 ? ts.best : INFINITY;
+      }
+    }
+    // queries not resolved within R0 -> phase B (mask per group, key per point)
+    const bool defer = active && !resolved;
+    const unsigned long long dm = __ballot(defer);
+    if (defer) job->defer_key[i] = dkey(ts.best, ts.bestj);
+    if (lane == 0) job->defer_mask[g] = dm;
+    if (stats && lane == 0) {
+      unsigned int* o = stats + (size_t)g * kStatFields;
+      o[0] = ts.st.blocks;
+      o[1] = ts.st.cand;
+      o[2] = ts.st.listed;
+      o[3] = ts.st.batches;
+      o[4] = (unsigned)(__builtin_amdgcn_s_memtime() - tm0);
+      o[5] = (unsigned)(tm1 - tm0) | ((unsigned)min(ts.st.cyc_scan >> 4, 0xffffull) << 16);  // prologue | scan/16
+      o[6] = (unsigned)__popcll(dm) | (ts.st.splits << 16);
+      o[7] = 1 | ((unsigned)min(ts.st.cyc_blocks >> 4, 0xffffull) << 16);             // blocks/16
+    }
+  }
+}
+
+// K3 (tile search): phase B — the queries phase A could not resolve, in
+// source (Morton) order: one wavefront gathers the deferred lanes of
+// kDeferGroups consecutive phase-A groups and searches them 64 at a time
+// with their full bound (the phase-A best, which is <= the a-priori bound).
+__global__ __launch_bounds__(256) void k_nn_tile_b(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  const CloudDev src = job->src;
+  const CloudDev tgt = job->tgt;
+  const int ngroups = (src.n + 63) >> 6;
+  // skip the whole workgroup when none of its groups deferred anything
+  const int gb0 = blockIdx.x * kLinWaves * kDeferGroups;
+  {
+    unsigned long long any = 0ull;
+    const int t = threadIdx.x;
+    if (t < kLinWaves * kDeferGroups && gb0 + t < ngroups) any = job->defer_mask[gb0 + t];
+    if (!__syncthreads_or(any != 0ull)) return;
+  }
+  const auto corr = gpw(job->corr);
+  const auto sqd = gpw(job->sqd);
+  const double max_corr2 = job->max_corr2;
+  float Rf[9], tf[3];
+  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
+  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
+  const int lane = lane_id();
+  const int wib = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  TileLds* L = reinterpret_cast<TileLds*>(dsm) + wib;
+  f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kTileLdsBytes);
+  fill_upper(tgt, upper);
+  __syncthreads();
+  const int g0 = gb0 + wib * kDeferGroups;
+  unsigned int* const stats = job->stats;
+  const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+  TileStats tst;
+  unsigned rounds = 0;
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < kDeferGroups; ++k) {
+    const int g = g0 + k;
+    const unsigned long long m = g < ngroups ? job->defer_mask[g] : 0ull;
+    if ((m >> lane) & 1ull)
+      L->defer[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+          g * 64 + lane;
+    n += __popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int e = b0 + lane;
+    const bool active = e < n;
+    const int i = L->defer[min(e, n - 1)];
+    const unsigned long long bk = job->defer_key[i];
+    const float4 a = ldg4(src.pts, i);
+    const unsigned long long key = gp(src.keys)[i];
+    TileSearch ts;
+    ts.c = tgt;
+    ts.L = L;
+    ts.U = upper;
+    ts.nup = upper_count(tgt);
+    ts.qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
+    ts.qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
+    ts.qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
+    ts.split_ext = job->split_extent;
+    ts.best = __uint_as_float((unsigned)(bk >> 32));
+    ts.bestj = (int)(unsigned)bk;
+    {  // coordinates of the phase-A best (seeding needs them)
+      const float4 p = ldg4(tgt.pts, max(ts.bestj, 0));
+      ts.bx = p.x;
+      ts.by = p.y;
+      ts.bz = p.z;
+    }
+    // radius doubling from 2 R0: scanning leaves within min(best, R^2)
+    // resolves a lane once best <= R^2; the last round is unbounded (the
+    // lane's own bound, <= max_corr^2)
+    // a bound without a point (bestj < 0, below the cap) is phase A's
+    // triangle bound from the previous correspondence: tight, so the lane
+    // searches with it at once; bounds from scanned points may be loose
+    // and go through the doubling rounds
+    const bool tight = ts.bestj < 0 && ts.best < job->cap2;
+    bool pending = active;
+    float R = 2.f * job->tile_r0;
+    for (;;) {
+      const bool last = (double)R * R >= job->max_corr2;
+      ts.cap = (last || tight) ? INFINITY : R * R;
+      ts.active = pending;
+      ts.run(key);
+      rounds += 1;
+      pending = pending && !(ts.best <= ts.cap);
+      if (last || !__any(pending)) break;
+      // lanes resolved this round seed the ones still pending
+      ts.seed_from_lanes(pending, __ballot(active && !pending && ts.bestj >= 0));
+      R *= 2.f;
+    }
+    if (active) {
+      corr[i] = (ts.bestj >= 0 && (double)ts.best < max_corr2) ? ts.bestj : -1;
+      sqd[i] = ts.bestj >= 0 ? ts.best : INFINITY;
+    }
+    tst.blocks += ts.st.blocks;
+    tst.cand += ts.st.cand;
+    tst.listed += ts.st.listed;
+    tst.batches += ts.st.batches;
+    tst.splits += ts.st.splits;
+  }
+  if (stats && lane == 0 && g0 < ngroups) {  // phase-B rows follow the phase-A rows
+    unsigned int* o = stats + (size_t)(ngroups + g0 / kDeferGroups) * kStatFields;
+    o[0] = tst.blocks;
+    o[1] = tst.cand;
+    o[2] = tst.listed;
+    o[3] = tst.batches;
+    o[4] = (unsigned)(__builtin_amdgcn_s_memtime() - tm0);
+    o[5] = rounds;
+    o[6] = (unsigned)n | (tst.splits << 16);
+    o[7] = 2;
   }
 }
 
@@ -1475,10 +1731,26 @@ size_t search_lds_bytes(int upper_count) {
 void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int job_upper_count) {
   const int search_groups = (nsrc + kSearchQ - 1) / kSearchQ;
   const int sb = std::max(1, std::min((search_groups + kLinWaves - 1) / kLinWaves, 8192));
-  k_nn_search<kSearchQ><<<sb, 64 * kLinWaves, search_lds_bytes(job_upper_count), s>>>(job);
+  if (use_tile_search()) {  // experimental 64-query tile search (tile_search.hpp)
+    const int groups = (nsrc + 63) / 64;
+    const int tb = std::max(1, (groups + kLinWaves - 1) / kLinWaves);
+    const size_t lds = (size_t)kLinWaves * kTileLdsBytes + 2 * sizeof(f4v) * (size_t)job_upper_count;
+    k_nn_tile_a<<<tb, 64 * kLinWaves, lds, s>>>(job);
+    const int tbb = std::max(1, (groups + kLinWaves * kDeferGroups - 1) / (kLinWaves * kDeferGroups));
+    k_nn_tile_b<<<tbb, 64 * kLinWaves, lds, s>>>(job);
+  } else {
+    k_nn_search<kSearchQ><<<sb, 64 * kLinWaves, search_lds_bytes(job_upper_count), s>>>(job);
+  }
   k_moments<<<nblocks, 64 * kMomWaves, 0, s>>>(job);
 }
-int search_queries_per_wave() { return kSearchQ; }
+bool use_tile_search() {
+  static const bool tile = [] {
+    const char* v = std::getenv("DDLO_SEARCH");
+    return v && std::strcmp(v, "tile") == 0;
+  }();
+  return tile;
+}
+int search_queries_per_wave() { return use_tile_search() ? 64 : kSearchQ; }
 int moment_blocks(int nsrc) {
   const int groups = (nsrc + 63) / 64;
   return std::max(1, std::min((groups + kMomWaves - 1) / kMomWaves, kMomBlocksMax));

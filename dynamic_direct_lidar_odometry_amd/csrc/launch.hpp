@@ -24,6 +24,7 @@ void launch_align_init(hipStream_t s, const AlignJob* job);
 // tgt_upper: number of upper-level (>= 1) boxes of the target (LDS cache size)
 void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int tgt_upper);
 int search_queries_per_wave();
+bool use_tile_search();  // DDLO_SEARCH=tile selects the experimental 64-query tile search
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
 void launch_lm_step(hipStream_t s, const AlignJob* job);
 void launch_mom_reduce(hipStream_t s, const AlignJob* job);  // sharded align: slab -> job->mom

@@ -562,8 +562,10 @@ namespace ddlo {
 // bound, and bounds only shrink while scanning.
 // ===========================================================================
 constexpr int kListMax = 256;       // leaf list capacity per wavefront
+constexpr int kListFlush = 16;      // scan once this many leaves are listed: early
+                                    // scans tighten the bounds that filter later blocks
 constexpr int kBlkMax = 32;         // candidate level-1 blocks per wavefront
-constexpr int kBatch = 4;           // leaves per LDS-DMA batch
+constexpr int kBatch = 8;           // leaves per LDS-DMA batch
 constexpr int kQMax = 16;           // queries per wavefront (collect path)
 
 struct CollectLds {
@@ -694,7 +696,7 @@ struct NNCollector {
         const unsigned long long m = __ballot(need);
         const int cm = __popcll(m);
         st_exact += cm;
-        if (L->nleaves + cm > kListMax) flush_leaves(c);  // tightens bounds; list empties
+        if (L->nleaves + cm > kListFlush) flush_leaves(c);  // tightens bounds; list empties
         const int n0 = L->nleaves;
         if (need) {
           const int slot =
