@@ -171,6 +171,11 @@ def sharded_leg(dist, rank, world, local_rank, args):
 
 
 def main():
+    # Native libraries (RCCL's version banner) print to fd 1; the contract is
+    # ONE JSON line on stdout, so route fd 1 to stderr and keep the real
+    # stdout for the result line only.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -298,7 +303,7 @@ def main():
     if not args.no_sharded:
         result["sharded_s2m"] = sharded_leg(dist, rank, world, local_rank, args)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

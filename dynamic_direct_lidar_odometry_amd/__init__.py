@@ -77,7 +77,8 @@ class GicpResult(C.Structure):
 
 
 def lib_path() -> str:
-    return os.path.join(_HERE, "_lib", "libddlo_gicp.so")
+    # DDLO_GICP_LIB: an alternative in-tree build of the same library (A/B runs)
+    return os.environ.get("DDLO_GICP_LIB") or os.path.join(_HERE, "_lib", "libddlo_gicp.so")
 
 
 def load():

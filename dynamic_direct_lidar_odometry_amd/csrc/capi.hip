@@ -169,6 +169,12 @@ const Rccl& rccl() {
 
 }  // namespace
 
+// one captured chunk: the graph and its executable instance
+struct hipExecGraphPair {
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+};
+
 struct gicp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -184,10 +190,12 @@ struct gicp_ctx {
   int* flag_host = nullptr;       // pinned
   bool have_align = false;        // a linearize ran against the current src/tgt
   int last_nsrc = 0;
-  // chunk graphs: [init + C iterations + flag copy] and [C iterations + flag copy]
-  hipGraphExec_t g_first = nullptr, g_rest = nullptr;
-  hipGraph_t gg_first = nullptr, gg_rest = nullptr;
+  // chunk graphs: [init + n iterations + flag copy] for the predicted
+  // iteration count n (one per n, index n - 1) and [1 iteration + flag copy]
+  std::vector<hipExecGraphPair> g_first;
+  hipExecGraphPair g_rest;
   std::tuple<int, int, const void*> graph_key{-1, -1, nullptr};
+  int predicted_iters = 4;   // iterations of the previous align on this ctx
   std::vector<hipEvent_t> chunk_ev;
   hipStream_t copy_stream = nullptr;
   bool profiling = false;
@@ -338,6 +346,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
     j.defer_key = reinterpret_cast<unsigned long long*>(u);
     j.defer_mask = reinterpret_cast<unsigned long long*>(u + sizeof(unsigned long long) * ns);
   }
+  j.xcd_remap = (int)env_float("DDLO_XCD_REMAP", 0.f);
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   return GICP_OK;
 }
@@ -369,7 +378,7 @@ gicp_status prepare_align(gicp_ctx* c) {
   return GICP_OK;
 }
 
-constexpr int kChunk = 4;  // outer iterations per graph launch
+constexpr int kMaxFirstChunk = 8;  // largest predicted first chunk (iterations)
 
 // One outer iteration: linearize (search + moments), then — on a sharded ctx —
 // this rank's reduced moments all-reduced across ranks (80 doubles over
@@ -385,10 +394,10 @@ gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks) {
   return GICP_OK;
 }
 
-gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int nblocks) {
+gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks) {
   const AlignJob* jd = c->job_dev.as<AlignJob>();
   if (with_init) launch_align_init(c->stream, jd);
-  for (int i = 0; i < kChunk; ++i) {
+  for (int i = 0; i < iters; ++i) {
     gicp_status s = enqueue_iteration(c, jd, nblocks);
     if (s) return s;
   }
@@ -398,39 +407,47 @@ gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int nblocks) {
   return GICP_OK;
 }
 
-gicp_status capture_chunk(gicp_ctx* c, bool with_init, int nblocks, hipGraph_t* g, hipGraphExec_t* ge) {
+gicp_status capture_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks, hipExecGraphPair* out) {
   HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-  const gicp_status s = enqueue_chunk(c, with_init, nblocks);
-  const hipError_t e = hipStreamEndCapture(c->stream, g);  // always leave capture mode
+  const gicp_status s = enqueue_chunk(c, with_init, iters, nblocks);
+  const hipError_t e = hipStreamEndCapture(c->stream, &out->g);  // always leave capture mode
   if (s) return s;
   HIP_TRY(e);
-  HIP_TRY(hipGraphInstantiate(ge, *g, nullptr, nullptr, 0));
+  HIP_TRY(hipGraphInstantiate(&out->ge, out->g, nullptr, nullptr, 0));
   return GICP_OK;
 }
 
+void drop_pair(hipExecGraphPair& p) {
+  if (p.ge) (void)hipGraphExecDestroy(p.ge);
+  if (p.g) (void)hipGraphDestroy(p.g);
+  p.ge = nullptr;
+  p.g = nullptr;
+}
+
 void drop_graphs(gicp_ctx* c) {
-  if (c->g_first) (void)hipGraphExecDestroy(c->g_first);
-  if (c->g_rest) (void)hipGraphExecDestroy(c->g_rest);
-  if (c->gg_first) (void)hipGraphDestroy(c->gg_first);
-  if (c->gg_rest) (void)hipGraphDestroy(c->gg_rest);
-  c->g_first = c->g_rest = nullptr;
-  c->gg_first = c->gg_rest = nullptr;
+  for (auto& p : c->g_first) drop_pair(p);
+  c->g_first.clear();
+  drop_pair(c->g_rest);
   c->graph_key = std::make_tuple(-1, -1, nullptr);
 }
 
-// Launch chunks of kChunk iterations, keeping one chunk queued ahead while the
-// host checks the previous chunk's done flag: at most one chunk of no-op
-// launches runs after convergence, and it overlaps the final state read-back.
-// Returns the index of the chunk after which the state is final.
+// Launch the align as a first chunk of n outer iterations (n = the previous
+// align's iteration count on this ctx: aligns of consecutive scans converge
+// in similar counts) followed by single-iteration chunks, keeping one
+// speculative single-iteration chunk queued ahead while the host checks the
+// previous chunk's done flag.  After convergence at most that one no-op
+// iteration (three early-exiting kernels) runs, overlapping the final state
+// read-back.  Returns the index of the chunk after which the state is final.
 gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chunk) {
   const void* jd = c->job_dev.p;
-  // key: chunk length, grid, job buffer and whether RCCL is in the chunk
-  auto key = std::make_tuple(kChunk * (c->comm ? -1 : 1), nblocks, jd);
+  // key: grid, job buffer and whether RCCL is in the chunk
+  auto key = std::make_tuple(c->comm ? -1 : 1, nblocks, jd);
   const bool use_graph = !c->comm || c->comm_graphs;
-  if (use_graph && (!c->g_first || c->graph_key != key)) {
+  const int first = std::max(1, std::min({c->predicted_iters, max_it, kMaxFirstChunk}));
+  if (use_graph && c->graph_key != key) {
     drop_graphs(c);
-    gicp_status s = capture_chunk(c, true, nblocks, &c->gg_first, &c->g_first);
-    if (!s) s = capture_chunk(c, false, nblocks, &c->gg_rest, &c->g_rest);
+    c->g_first.resize(kMaxFirstChunk);
+    gicp_status s = capture_chunk(c, false, 1, nblocks, &c->g_rest);
     if (s) {
       drop_graphs(c);
       (void)hipGetLastError();
@@ -440,14 +457,21 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     }
     c->graph_key = key;
   }
-  auto launch_chunk = [&](bool first) -> gicp_status {
+  if (use_graph && !c->g_first[first - 1].ge) {
+    gicp_status s = capture_chunk(c, true, first, nblocks, &c->g_first[first - 1]);
+    if (s) {
+      drop_graphs(c);
+      return s;
+    }
+  }
+  auto launch_chunk = [&](bool is_first) -> gicp_status {
     if (use_graph) {
-      HIP_TRY(hipGraphLaunch(first ? c->g_first : c->g_rest, c->stream));
+      HIP_TRY(hipGraphLaunch(is_first ? c->g_first[first - 1].ge : c->g_rest.ge, c->stream));
       return GICP_OK;
     }
-    return enqueue_chunk(c, first, nblocks);
+    return enqueue_chunk(c, is_first, is_first ? first : 1, nblocks);
   };
-  const int nchunks = (max_it + kChunk - 1) / kChunk;
+  const int nchunks = 1 + (max_it - first);
   while ((int)c->chunk_ev.size() < nchunks) {
     hipEvent_t e;
     HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -482,6 +506,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     ++k;
   }
   *final_chunk = k;
+  c->predicted_iters = std::max(1, c->flag_host[0]);
   return GICP_OK;
 }
 

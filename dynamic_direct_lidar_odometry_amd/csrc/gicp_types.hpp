@@ -107,6 +107,7 @@ struct AlignJob {
   float split_extent;      // sub-range split threshold of a wave's union box (m)
   unsigned long long* defer_mask;  // [ceil(n_src / 64)]
   unsigned long long* defer_key;   // [n_src]
+  int xcd_remap;           // search: contiguous group range per XCD block label
 };
 
 }  // namespace ddlo

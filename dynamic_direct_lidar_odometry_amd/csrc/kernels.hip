@@ -693,8 +693,8 @@ __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__
 // (exact completion): queries whose pass-1 radius was clipped to kOptR and
 // found nothing search again with the full max_corr bound.  Writes corr/sqd
 // (update_correspondences, nano_gicp_impl.hpp:249-258).
-template <int Q>
-__global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict__ job) {
+template <int Q, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
   const CloudDev src = job->src;
@@ -720,7 +720,13 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
   f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kCollectLdsBytes);
   fill_upper(tgt, upper);
   __syncthreads();
-  const int wave = blockIdx.x * kLinWaves + wib;
+  // XCD-aware remap (job->xcd_remap): blocks b and b + 8 share an XCD and its
+  // L2, so give each of the 8 block labels one contiguous (Morton-compact)
+  // eighth of the groups.  Speed only: the mapping stays a bijection.
+  const int nb = gridDim.x;
+  const int bl = (job->xcd_remap && nb % 8 == 0) ? (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8)
+                                                 : (int)blockIdx.x;
+  const int wave = bl * kLinWaves + wib;
   const int nwaves_total = gridDim.x * kLinWaves;
   const int ngroups = (src.n + Q - 1) / Q;
   // previous linearization pose (for the triangle-inequality bound)
@@ -732,7 +738,11 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
     const int i = g * Q + qi;
     const bool inrange = i < src.n;
     const int ic = inrange ? i : src.n - 1;
+    // every independent per-query load of the prologue in one round trip
     const float4 a = ldg4(src.pts, ic);
+    const int jprev = have_prev ? corr[ic] : -1;
+    const float sqprev = have_prev ? sqd[ic] : 0.f;
+    const unsigned long long skey = gp(src.keys)[ic];
     // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
@@ -761,8 +771,11 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
     vis.skip_lo = 1;
     vis.skip_hi = 0;
     bool seeded = false;
+    // coordinates of the point behind vis.bestj when it is already in registers
+    float bpx = 0.f, bpy = 0.f, bpz = 0.f;
+    bool have_bp = true;
     if (have_prev && active) {
-      const int j = corr[i];
+      const int j = jprev;
       if (j >= 0) {
         // NN(q) <= |q - p_prev| <= sqrt(sqd_prev) + |q - q_prev| (triangle
         // inequality; fp64 with an upward margin covers fp32 rounding), so
@@ -773,7 +786,7 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
         const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
         const double mv = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
         if (mv < 0.02) {
-          const double r = sqrt((double)sqd[i]) + mv;
+          const double r = sqrt((double)sqprev) + mv;
           const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
           if (b2 < (double)cap2) {
             vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
@@ -785,6 +798,9 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
           if (d < cap2) {
             vis.best = d;
             vis.bestj = j;
+            bpx = p.x;
+            bpy = p.y;
+            bpz = p.z;
             seeded = true;
           }
         }
@@ -817,6 +833,7 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
         if (bd < cap2) {
           vis.best = bd;
           vis.bestj = (int)(unsigned)bk;
+          have_bp = false;   // the winning window point may sit in another slice lane
         }
       }
       again = need_seed;
@@ -828,7 +845,10 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
     {
       const unsigned long long donors = __ballot(lane < Q && active && vis.bestj >= 0);
       if (donors && __any(active)) {
-        const float4 bp = ldg4(tgt.pts, max(vis.bestj, 0));
+        float4 bp = make_float4(bpx, bpy, bpz, 0.f);
+        if (__any(!have_bp && vis.bestj >= 0)) {
+          if (!have_bp) bp = ldg4(tgt.pts, max(vis.bestj, 0));
+        }
         unsigned long long bk = dkey(vis.best, vis.bestj);
         unsigned long long m = donors;
         while (m) {
@@ -844,11 +864,11 @@ __global__ __launch_bounds__(256, 4) void k_nn_search(const AlignJob* __restrict
         }
       }
     }
-    const unsigned long long skey = gp(src.keys)[ic];
     unsigned cst[6] = {0, 0, 0, 0, 0, 0};
+    const unsigned tm_pro = stats ? (unsigned)__builtin_amdgcn_s_memtime() : 0u;
     collect_scan_nn<Q>(tgt, CL, upper, qx, qy, qz, active, vis.best, vis.bestj, skey, cst);
     vis.st_blocks = cst[0];
-    vis.st_box = cst[1];
+    vis.st_box = min((tm_pro - (unsigned)tm0) >> 4, 65535u) | (min((cst[1] - (unsigned)tm0) >> 4, 65535u) << 16);
     vis.st_exact = cst[2];
     vis.st_scan = cst[3];
     vis.st_splits = cst[4];
@@ -1739,7 +1759,15 @@ void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks,
     const int tbb = std::max(1, (groups + kLinWaves * kDeferGroups - 1) / (kLinWaves * kDeferGroups));
     k_nn_tile_b<<<tbb, 64 * kLinWaves, lds, s>>>(job);
   } else {
-    k_nn_search<kSearchQ><<<sb, 64 * kLinWaves, search_lds_bytes(job_upper_count), s>>>(job);
+    static const int occ = [] {
+      const char* v = std::getenv("DDLO_SEARCH_OCC");
+      return v && *v ? std::atoi(v) : 4;
+    }();
+    const size_t lds = search_lds_bytes(job_upper_count);
+    if (occ == 3)
+      k_nn_search<kSearchQ, 3><<<sb, 64 * kLinWaves, lds, s>>>(job);
+    else
+      k_nn_search<kSearchQ, 4><<<sb, 64 * kLinWaves, lds, s>>>(job);
   }
   k_moments<<<nblocks, 64 * kMomWaves, 0, s>>>(job);
 }

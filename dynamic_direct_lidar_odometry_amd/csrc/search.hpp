@@ -561,7 +561,7 @@ namespace ddlo {
 // Exactness: a leaf is dropped only if its box is farther than the query's
 // bound, and bounds only shrink while scanning.
 // ===========================================================================
-constexpr int kListMax = 256;       // leaf list capacity per wavefront
+constexpr int kListMax = 288;       // leaf list capacity per wavefront (>= kListFlush + 4 blocks x 64 leaves)
 constexpr int kListFlush = 16;      // scan once this many leaves are listed: early
                                     // scans tighten the bounds that filter later blocks
 constexpr int kBlkMax = 32;         // candidate level-1 blocks per wavefront
@@ -574,6 +574,11 @@ struct CollectLds {
   int blocks[kBlkMax];
   int nleaves, nblocks, pad0, pad1;
   f4v pts[kBatch * kLeafSize];      // streamed leaves (AoS float4)
+  f4v sb_lo[kFanout], sb_hi[kFanout];  // boxes of a block's leaves that pass the union test
+  int sb_leaf[kFanout];
+  unsigned long long wmask[kMaxLevels];  // traversal stack: per level, nodes still to expand
+  int wbase[kMaxLevels];
+  int sr_lo[4], sr_hi[4], nsr, pad2;     // query sub-ranges of a split wave
 };
 constexpr int kCollectLdsBytes = (int)sizeof(CollectLds);
 
@@ -665,7 +670,14 @@ struct NNCollector {
     publish_bounds();
   }
 
-  // exact leaf filter of the listed blocks (4 blocks per round trip)
+  // Exact leaf filter of the listed blocks (4 blocks per round trip).
+  // (1) lane = leaf: one test of the leaf box against the union box of the
+  //     wave's current balls; (2) only the survivors are tested against the
+  //     individual queries, as (leaf, query) pairs spread over the lanes
+  //     (64/Q leaves per round) instead of every leaf against all Q queries.
+  // The leaf list is scanned (bounds tightened) between groups of 4 blocks;
+  // the scan sits outside the unrolled block loop so that its code exists
+  // once (the kernel must stay small for the instruction cache).
   __device__ __forceinline__ void flush_blocks(const CloudDev& c) {
     const int lane = lane_id();
     const int nb = L->nblocks;
@@ -681,45 +693,62 @@ struct NNCollector {
         lo[u] = ldg4(c.box_lo, li);
         hi[u] = ldg4(c.box_hi, li);
       }
+      // union of the current balls (bounds only shrink: a superset)
+      const WaveBox wb = make_wave_box(active, qx, qy, qz, bound());
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (cnt[u] == 0) continue;
         st_blocks += 1;
-        bool need = false;
-        if (lane < cnt[u]) {
-#pragma unroll 4
-          for (int q = 0; q < Q; ++q) {
-            const f4v qk = L->q[q];
-            need |= qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, lo[u], hi[u]) <= qk.w;
-          }
-        }
-        const unsigned long long m = __ballot(need);
+        const bool pass = lane < cnt[u] && box_overlap(wb, lo[u], hi[u]);
+        const unsigned long long m = __ballot(pass);
         const int cm = __popcll(m);
-        st_exact += cm;
-        if (L->nleaves + cm > kListFlush) flush_leaves(c);  // tightens bounds; list empties
-        const int n0 = L->nleaves;
-        if (need) {
-          const int slot =
-              n0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-          L->leaves[slot] = base[u] + lane;
+        if (cm == 0) continue;
+        if (pass) {
+          const int slot = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+          L->sb_lo[slot] = f4v{lo[u].x, lo[u].y, lo[u].z, 0.f};
+          L->sb_hi[slot] = f4v{hi[u].x, hi[u].y, hi[u].z, 0.f};
+          L->sb_leaf[slot] = base[u] + lane;
         }
         __builtin_amdgcn_wave_barrier();
-        if (lane == 0) L->nleaves = n0 + cm;
-        __builtin_amdgcn_wave_barrier();
+        pair_filter(cm);
       }
+      if (L->nleaves > kListFlush) flush_leaves(c);  // tightens bounds; list empties
     }
     if (lane == 0) L->nblocks = 0;
     __builtin_amdgcn_wave_barrier();
   }
 
-  __device__ __forceinline__ void push_block(const CloudDev& c, int node) {
-    if (L->nblocks >= kBlkMax) flush_blocks(c);
-    if (lane_id() == 0) {
-      const int n = L->nblocks;
-      L->blocks[n] = node;
-      L->nblocks = n + 1;
+  // (leaf, query) pair tests of the cm staged leaves; listed leaves appended
+  __device__ __forceinline__ void pair_filter(int cm) {
+    const int lane = lane_id();
+    constexpr int LPR = 64 / Q;
+    for (int r0 = 0; r0 < cm; r0 += LPR) {
+      const int li = r0 + lane / Q;
+      bool need = false;
+      if (li < cm) {
+        const f4v qk = L->q[lane % Q];
+        const f4v blo = L->sb_lo[li], bhi = L->sb_hi[li];
+        need = qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, make_float4(blo.x, blo.y, blo.z, 0.f),
+                                        make_float4(bhi.x, bhi.y, bhi.z, 0.f)) <= qk.w;
+      }
+      const unsigned long long bal = __ballot(need);
+      // the first lane of each Q-lane segment lists the segment's leaf
+      const unsigned long long segm = Q >= 64 ? ~0ull : ((1ull << Q) - 1ull);
+      const bool lead = (lane % Q) == 0 && li < cm && ((bal >> (lane & ~(Q - 1))) & segm) != 0ull;
+      const unsigned long long lm = __ballot(lead);
+      const int cl = __popcll(lm);
+      if (cl == 0) continue;
+      st_exact += cl;
+      const int n0 = L->nleaves;
+      if (lead) {
+        const int slot =
+            n0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(lm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)lm, 0u));
+        L->leaves[slot] = L->sb_leaf[li];
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) L->nleaves = n0 + cl;
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
   }
 
   __device__ __forceinline__ bool upper_ov(const CloudDev& c, int level, int idx) const {
@@ -727,51 +756,61 @@ struct NNCollector {
     return box_overlap_v(box, U[k], U[nup + k]);
   }
 
-  template <int LV>
-  __device__ __forceinline__ void walk(const CloudDev& c, int base, unsigned long long mask) {
-    // mask selects nodes of level LV (>= 2) overlapping the box
-    while (mask) {
-      const int ci = __builtin_ctzll(mask);
-      mask &= mask - 1;
-      const int node = base + ci;
-      const int cb = node * kFanout;
-      const int cnt = min(kFanout, lvl_cnt(c, LV - 1) - cb);
-      const int lane = lane_id();
-      const bool ov = lane < cnt && upper_ov(c, LV - 1, cb + lane);
-      unsigned long long m = __ballot(ov);
-      if constexpr (LV == 2) {
-        while (m) {
-          const int b = __builtin_ctzll(m);
-          m &= m - 1;
-          push_block(c, cb + b);
-        }
-      } else {
-        walk<LV - 1>(c, cb, m);
-      }
-    }
-  }
-
+  // Depth-first walk of the upper levels with the wave box: an explicit
+  // per-level stack of 64-bit child masks in LDS, so the block push (and the
+  // block flush it may trigger) has a single call site whatever the depth.
   __device__ __forceinline__ void collect_blocks(const CloudDev& c) {
     const int T = c.nlevels - 1;
-    if (T == 0) {
-      push_block(c, 0);
-      return;
-    }
     const int lane = lane_id();
-    const bool ov = lane < lvl_cnt(c, T) && upper_ov(c, T, lane);
-    unsigned long long m = __ballot(ov);
-    if (T == 1) {
-      while (m) {
-        const int b = __builtin_ctzll(m);
-        m &= m - 1;
-        push_block(c, b);
+    if (T == 0) {  // a single leaf block
+      if (lane == 0) {
+        L->blocks[L->nblocks] = 0;
+        L->nblocks = L->nblocks + 1;
       }
+      __builtin_amdgcn_wave_barrier();
       return;
     }
-    switch (T) {
-      case 2: walk<2>(c, 0, m); break;
-      case 3: walk<3>(c, 0, m); break;
-      default: walk<4>(c, 0, m); break;
+    {
+      const bool ov = lane < lvl_cnt(c, T) && upper_ov(c, T, lane);
+      const unsigned long long m = __ballot(ov);
+      if (lane == 0) {
+        L->wmask[T] = m;
+        L->wbase[T] = 0;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    int lv = T;
+    while (true) {
+      const unsigned long long m = L->wmask[lv];
+      if (m == 0ull) {
+        if (lv == T) break;
+        ++lv;
+        continue;
+      }
+      const int ci = __builtin_ctzll(m);
+      const int node = L->wbase[lv] + ci;
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) L->wmask[lv] = m & (m - 1);
+      __builtin_amdgcn_wave_barrier();
+      if (lv == 1) {  // a level-1 node is a block of 64 leaves
+        if (L->nblocks >= kBlkMax) flush_blocks(c);
+        if (lane == 0) {
+          L->blocks[L->nblocks] = node;
+          L->nblocks = L->nblocks + 1;
+        }
+        __builtin_amdgcn_wave_barrier();
+        continue;
+      }
+      const int cb = node * kFanout;
+      const int cnt = min(kFanout, lvl_cnt(c, lv - 1) - cb);
+      const bool ov = lane < cnt && upper_ov(c, lv - 1, cb + lane);
+      const unsigned long long cm = __ballot(ov);
+      --lv;
+      if (lane == 0) {
+        L->wmask[lv] = cm;
+        L->wbase[lv] = cb;
+      }
+      __builtin_amdgcn_wave_barrier();
     }
   }
 };
@@ -799,14 +838,20 @@ __device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L
   col.qz = qz;
   col.active = active;
   col.bk = dkey(best, bestj);
+  // Query sub-ranges: the whole group, or — when the union box of its balls
+  // is wider than kSplitExtent — up to 4 Morton-jump sub-ranges, each walked
+  // with its own (smaller) box.  A runtime worklist keeps one walk site.
   const WaveBox whole = make_wave_box(active, qx, qy, qz, best);
-  if (!(box_extent(whole) > kSplitExtent)) {
-    col.box = whole;
-    col.collect_blocks(c);
-  } else {
+  if (lane == 0) {
+    L->sr_lo[0] = 0;
+    L->sr_hi[0] = Q;
+    L->nsr = 1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (box_extent(whole) > kSplitExtent) {
     col.st_splits += 1;
     const int sp = morton_jump_split<Q>(key, 0, Q);
-#pragma unroll
+    int nsr = 0;
     for (int h = 0; h < 2; ++h) {
       const int lo = h == 0 ? 0 : sp, hi = h == 0 ? sp : Q;
       if (lo >= hi) continue;
@@ -815,27 +860,37 @@ __device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L
       if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
         col.st_splits += 1;
         const int s2 = morton_jump_split<Q>(key, lo, hi);
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const int l2 = h2 == 0 ? lo : s2, r2 = h2 == 0 ? s2 : hi;
-          const bool a2 = active && qi >= l2 && qi < r2;
-          if (!__any(a2)) continue;
-          col.box = make_wave_box(a2, qx, qy, qz, col.bound());
-          col.collect_blocks(c);
+        if (lane == 0) {
+          L->sr_lo[nsr] = lo; L->sr_hi[nsr] = s2;
+          L->sr_lo[nsr + 1] = s2; L->sr_hi[nsr + 1] = hi;
         }
-      } else if (__any(act)) {
-        col.box = hb;
-        col.collect_blocks(c);
+        nsr += 2;
+      } else {
+        if (lane == 0) {
+          L->sr_lo[nsr] = lo; L->sr_hi[nsr] = hi;
+        }
+        nsr += 1;
       }
     }
+    if (lane == 0) L->nsr = nsr;
+    __builtin_amdgcn_wave_barrier();
+  }
+  for (int r = 0; r < L->nsr; ++r) {
+    const int lo = L->sr_lo[r], hi = L->sr_hi[r];
+    if (lo >= hi) continue;
+    const bool act = active && qi >= lo && qi < hi;
+    if (!__any(act)) continue;
+    col.box = make_wave_box(act, qx, qy, qz, col.bound());
+    col.collect_blocks(c);
   }
   // a block listed by two sub-ranges is filtered twice: harmless (a leaf
   // scanned twice leaves the minimum unchanged)
+  const unsigned tm_trav = (unsigned)__builtin_amdgcn_s_memtime();
   col.flush_blocks(c);
   st[5] = (unsigned)__builtin_amdgcn_s_memtime();
   col.flush_leaves(c);
   st[0] = col.st_blocks;
-  st[1] = 0;
+  st[1] = tm_trav;
   st[2] = col.st_exact;
   st[3] = col.st_scan;
   st[4] = col.st_splits;
