@@ -170,6 +170,41 @@ def sharded_leg(dist, rank, world, local_rank, args):
     return out_leg
 
 
+def batched_leg(dist, rank, world, local_rank, args):
+    """BASELINE.json configs[4] / SURVEY.md §8(e) cfg 5: frame-parallel S2S
+    over a 64x2048 scan sequence (moving pedestrians), the frames split into
+    one contiguous range per rank (no collective; every pair needs only its
+    two scans) and, inside a rank, into `--batch-streams` chained chunks on
+    their own HIP streams (gicp_s2s_batch).  Each pair pays the real per-scan
+    cost: H2D upload, index build, k=10 covariances and the align."""
+    import dynamic_direct_lidar_odometry_amd as P
+    from dynamic_direct_lidar_odometry_amd import scene
+    t0 = time.time()
+    frames, _ = scene.sequence(64, 2048, args.batch_frames, args.batch_unique)
+    npairs = len(frames) - 1
+    a = npairs * rank // world
+    b = npairs * (rank + 1) // world
+    mine = frames[a:b + 1]
+    params = P.default_params(k_correspondences=10, max_correspondence_distance=1.0, max_iterations=32,
+                              transformation_epsilon=0.01)   # ddlo.yaml:187-192 (S2S)
+    log(f"[rank {rank}] batch setup {time.time() - t0:.1f}s: pairs {a}..{b}")
+    P.s2s_batch(mine[:min(len(mine), 2 * args.batch_streams + 1)], params, device=local_rank,
+                nstreams=args.batch_streams)   # warmup (allocations, graphs)
+    if dist is not None:
+        dist.barrier()
+    c0 = time.perf_counter()
+    poses, res = P.s2s_batch(mine, params, device=local_rank, nstreams=args.batch_streams)
+    elapsed = time.perf_counter() - c0
+    iters = sum(r.iterations_run for r in res[1:])
+    elapsed, iters_total = reduce_over_ranks(dist, elapsed, iters, f"cuda:{local_rank}")
+    return {"workload": f"cfg5 frame-parallel S2S: {npairs} pairs of 64x2048 scans "
+                        f"({args.batch_unique} ray-cast frames replayed forward/backward), k=10, maxCorr 1.0 m",
+            "n_gpus": world, "streams_per_gpu": args.batch_streams, "pairs": npairs,
+            "pairs_per_s": round(npairs / elapsed, 2), "ms_per_pair": round(1e3 * elapsed / npairs, 4),
+            "iters_per_s": round(iters_total / elapsed, 2),
+            "per_pair_work": "H2D + index build + covariances + align", "collective": "none (frames split by rank)"}
+
+
 def main():
     # Native libraries (RCCL's version banner) print to fd 1; the contract is
     # ONE JSON line on stdout, so route fd 1 to stderr and keep the real
@@ -184,6 +219,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-sharded", action="store_true", help="skip the spatially sharded cfg4 leg")
     ap.add_argument("--sharded-steps", type=int, default=10)
+    ap.add_argument("--no-batch", action="store_true", help="skip the frame-parallel S2S cfg5 leg")
+    ap.add_argument("--batch-frames", type=int, default=201)
+    ap.add_argument("--batch-unique", type=int, default=20)
+    ap.add_argument("--batch-streams", type=int, default=4)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -302,6 +341,8 @@ def main():
     ctx.close()
     if not args.no_sharded:
         result["sharded_s2m"] = sharded_leg(dist, rank, world, local_rank, args)
+    if not args.no_batch:
+        result["batched_s2s"] = batched_leg(dist, rank, world, local_rank, args)
     if rank == 0:
         print(json.dumps(result), file=json_out, flush=True)
     if dist:

@@ -16,7 +16,7 @@ import os
 
 import numpy as np
 
-__all__ = ["GicpParams", "GicpResult", "Context", "NanoGICP", "GicpError", "lib_path", "load",
+__all__ = ["GicpParams", "GicpResult", "Context", "NanoGICP", "GicpError", "lib_path", "load", "s2s_batch",
            "REG_NONE", "REG_MIN_EIG", "REG_NORMALIZED_MIN_EIG", "REG_PLANE", "REG_FROBENIUS",
            "GAUSS_NEWTON", "LEVENBERG_MARQUARDT", "SOURCE", "TARGET"]
 
@@ -125,6 +125,7 @@ def load():
         "gicp_comm_unique_id": (I, [P, S]),
         "gicp_set_comm": (I, [P, P, S, I, I]),
         "gicp_get_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+        "gicp_s2s_batch": (I, [I, C.POINTER(GicpParams), P, P, S, I, I, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -162,6 +163,27 @@ def comm_unique_id() -> bytes:
     if rc != 0:
         raise GicpError(rc, L.gicp_last_error().decode())
     return bytes(buf)
+
+
+def s2s_batch(frames, params: GicpParams | None = None, device: int = 0, nstreams: int = 4):
+    """Frame-parallel S2S over a scan sequence (gicp_s2s_batch; odom.cc:754-768).
+
+    frames: list of (N_t, 3) float32 clouds in sensor frames.  Returns
+    (poses (T, 4, 4) float32, results list): poses[t] aligns scan t onto scan
+    t-1 (poses[0] = identity)."""
+    L = load()
+    p = params if params is not None else default_params()
+    arrs = [np.ascontiguousarray(np.asarray(f, np.float32).reshape(-1, 3)) for f in frames]
+    n = len(arrs)
+    ptrs = (C.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    sizes = (C.c_size_t * n)(*[len(a) for a in arrs])
+    out = np.zeros((n, 4, 4), np.float32)
+    res = (GicpResult * n)()
+    rc = L.gicp_s2s_batch(device, C.byref(p), C.cast(ptrs, C.c_void_p), C.cast(sizes, C.c_void_p), 12, n,
+                          nstreams, _ptr(out), C.cast(res, C.c_void_p))
+    if rc != 0:
+        raise GicpError(rc, L.gicp_last_error().decode())
+    return out, list(res)
 
 
 class Context:

@@ -22,6 +22,7 @@
 #include <memory>
 #include <string>
 #include <tuple>
+#include <thread>
 #include <vector>
 
 #include "../../include/ddlo_gicp.h"
@@ -1040,3 +1041,47 @@ gicp_status gicp_get_stream(const gicp_ctx* c, void** stream) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Frame-parallel S2S batch (ddlo_gicp.h): nstreams chained chunks, one ctx,
+// HIP stream and host thread each.
+gicp_status gicp_s2s_batch(int device, const gicp_params* p, const float* const* clouds, const size_t* sizes,
+                           size_t stride_bytes, int nframes, int nstreams, float* out16, gicp_result* res) {
+  if (!p || !clouds || !sizes || !out16 || nframes < 1 || nstreams < 1)
+    return fail(GICP_EINVAL, "invalid batch arguments");
+  for (int t = 0; t < nframes; ++t)
+    if (!clouds[t] || sizes[t] == 0) return fail(GICP_EINVAL, "null or empty frame");
+  for (int e = 0; e < 16; ++e) out16[e] = (e % 5 == 0) ? 1.f : 0.f;
+  if (res) std::memset(&res[0], 0, sizeof(gicp_result));
+  const int npairs = nframes - 1;
+  if (npairs == 0) return GICP_OK;
+  const int nthreads = std::min(nstreams, npairs);
+  std::vector<gicp_status> status(nthreads, GICP_OK);
+  std::vector<std::string> errors(nthreads);
+  auto worker = [&](int w) {
+    // pairs (t-1, t) for t in [t0, t1)
+    const int t0 = 1 + (int)((long)npairs * w / nthreads);
+    const int t1 = 1 + (int)((long)npairs * (w + 1) / nthreads);
+    gicp_ctx* c = nullptr;
+    gicp_status s = gicp_ctx_create(device, &c);
+    if (!s) s = gicp_set_params(c, p);
+    if (!s) s = gicp_set_target(c, clouds[t0 - 1], sizes[t0 - 1], stride_bytes);
+    for (int t = t0; t < t1 && !s; ++t) {
+      s = gicp_set_source(c, clouds[t], sizes[t], stride_bytes, 1);
+      if (!s) s = gicp_align(c, nullptr, out16 + 16 * (size_t)t, res ? &res[t] : nullptr);
+      if (!s) s = gicp_swap_source_target(c);  // scan t becomes the next target (odom.cc:768)
+    }
+    if (s) {
+      status[w] = s;
+      errors[w] = g_last_error;
+    }
+    if (c) (void)gicp_ctx_destroy(c);
+  };
+  std::vector<std::thread> pool;
+  for (int w = 1; w < nthreads; ++w) pool.emplace_back(worker, w);
+  worker(0);
+  for (auto& th : pool) th.join();
+  for (int w = 0; w < nthreads; ++w)
+    if (status[w]) return fail(status[w], "s2s batch chunk " + std::to_string(w) + ": " + errors[w]);
+  return GICP_OK;
+}

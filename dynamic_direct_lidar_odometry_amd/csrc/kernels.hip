@@ -1761,7 +1761,7 @@ void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks,
   } else {
     static const int occ = [] {
       const char* v = std::getenv("DDLO_SEARCH_OCC");
-      return v && *v ? std::atoi(v) : 4;
+      return v && *v ? std::atoi(v) : 3;  // 3 waves/SIMD: no scratch spills (same speed as 4, no spill traffic)
     }();
     const size_t lds = search_lds_bytes(job_upper_count);
     if (occ == 3)

@@ -576,8 +576,6 @@ struct CollectLds {
   f4v pts[kBatch * kLeafSize];      // streamed leaves (AoS float4)
   f4v sb_lo[kFanout], sb_hi[kFanout];  // boxes of a block's leaves that pass the union test
   int sb_leaf[kFanout];
-  unsigned long long wmask[kMaxLevels];  // traversal stack: per level, nodes still to expand
-  int wbase[kMaxLevels];
   int sr_lo[4], sr_hi[4], nsr, pad2;     // query sub-ranges of a split wave
 };
 constexpr int kCollectLdsBytes = (int)sizeof(CollectLds);
@@ -757,8 +755,9 @@ struct NNCollector {
   }
 
   // Depth-first walk of the upper levels with the wave box: an explicit
-  // per-level stack of 64-bit child masks in LDS, so the block push (and the
-  // block flush it may trigger) has a single call site whatever the depth.
+  // per-level stack of 64-bit child masks (uniform values: scalar registers),
+  // so the block push (and the block flush it may trigger) has a single call
+  // site whatever the depth.
   __device__ __forceinline__ void collect_blocks(const CloudDev& c) {
     const int T = c.nlevels - 1;
     const int lane = lane_id();
@@ -770,28 +769,25 @@ struct NNCollector {
       __builtin_amdgcn_wave_barrier();
       return;
     }
+    unsigned long long m1 = 0, m2 = 0, m3 = 0, m4 = 0;
+    int b1 = 0, b2 = 0, b3 = 0;
     {
       const bool ov = lane < lvl_cnt(c, T) && upper_ov(c, T, lane);
       const unsigned long long m = __ballot(ov);
-      if (lane == 0) {
-        L->wmask[T] = m;
-        L->wbase[T] = 0;
-      }
-      __builtin_amdgcn_wave_barrier();
+      if (T == 1) m1 = m; else if (T == 2) m2 = m; else if (T == 3) m3 = m; else m4 = m;
     }
     int lv = T;
     while (true) {
-      const unsigned long long m = L->wmask[lv];
+      unsigned long long m = lv == 1 ? m1 : lv == 2 ? m2 : lv == 3 ? m3 : m4;
       if (m == 0ull) {
         if (lv == T) break;
         ++lv;
         continue;
       }
-      const int ci = __builtin_ctzll(m);
-      const int node = L->wbase[lv] + ci;
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) L->wmask[lv] = m & (m - 1);
-      __builtin_amdgcn_wave_barrier();
+      const int base = lv == 1 ? b1 : lv == 2 ? b2 : lv == 3 ? b3 : 0;
+      const int node = base + __builtin_ctzll(m);
+      m &= m - 1;
+      if (lv == 1) m1 = m; else if (lv == 2) m2 = m; else if (lv == 3) m3 = m; else m4 = m;
       if (lv == 1) {  // a level-1 node is a block of 64 leaves
         if (L->nblocks >= kBlkMax) flush_blocks(c);
         if (lane == 0) {
@@ -806,11 +802,7 @@ struct NNCollector {
       const bool ov = lane < cnt && upper_ov(c, lv - 1, cb + lane);
       const unsigned long long cm = __ballot(ov);
       --lv;
-      if (lane == 0) {
-        L->wmask[lv] = cm;
-        L->wbase[lv] = cb;
-      }
-      __builtin_amdgcn_wave_barrier();
+      if (lv == 1) { m1 = cm; b1 = cb; } else if (lv == 2) { m2 = cm; b2 = cb; } else { m3 = cm; b3 = cb; }
     }
   }
 };

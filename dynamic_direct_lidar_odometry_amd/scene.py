@@ -267,3 +267,26 @@ def s2m_problem(rows: int, cols: int, n_keyframes: int, submap_size: int, cfg_id
         subset = np.arange(total)
     guess = cur @ PERTURB
     return {"source": src, "keyframes": kfs, "subset": subset, "T_true": cur, "guess": guess}
+
+
+def sequence(rows: int, cols: int, n_frames: int, n_unique: int, cfg_id: int = 5):
+    """Scan sequence for the batched-odometry case (SURVEY.md §8(d) cfg 5):
+    ``n_unique`` consecutive ray-cast frames of the plaza with MOVING
+    pedestrians (1.0 m/s at 10 Hz), replayed forward and backward
+    (0..u-1, u-1..0, 0..) up to ``n_frames`` so that every consecutive pair
+    stays a real adjacent-pose pair while only ``n_unique`` frames are cast.
+    Returns (frames list of sensor-frame clouds, per-frame world poses)."""
+    seed = 1000 + cfg_id
+    scene = make_scene(seed, moving=True)
+    poses = trajectory(n_unique, seed)
+    uniq = [raycast(scene, poses[k], rows, cols, seed=seed + k, t=0.1 * k) for k in range(n_unique)]
+    order = []
+    k, step = 0, 1
+    while len(order) < n_frames:
+        order.append(k)
+        if not 0 <= k + step < n_unique:
+            step = -step
+            order.append(k)  # the turn-around frame repeats (a zero-motion pair)
+        k += step
+    order = order[:n_frames]
+    return [uniq[i] for i in order], [poses[i] for i in order]

@@ -221,6 +221,19 @@ gicp_status gicp_set_comm(struct gicp_ctx* ctx, const uint8_t* id, size_t nbytes
  * in the align graphs (1) or launched eagerly (0). */
 gicp_status gicp_get_comm_info(const struct gicp_ctx* ctx, int* nranks, int* rank, int* graphs);
 
+/* ---- frame-parallel scan-to-scan batch (SURVEY.md §8(e) cfg 5) ----------
+ * The S2S half of OdomNode::scanMatching over a recorded sequence
+ * (odom.cc:754-768: align(guess = I), getFinalTransformation, then
+ * swapSourceAndTarget so scan t becomes the target of scan t+1 with its
+ * index and covariances).  S2S pairs are independent (each uses only scans
+ * t-1 and t), so the sequence is cut into nstreams contiguous chunks, each
+ * chained on its own ctx / HIP stream / host thread; a chunk's first pair
+ * builds scan t-1 once more.  out16[t] (row-major 4x4) = the transform
+ * aligning scan t onto scan t-1 (out16[0] = identity); res[t] (optional)
+ * its result.  clouds[t] points to sizes[t] points with the given stride. */
+gicp_status gicp_s2s_batch(int device, const gicp_params* p, const float* const* clouds, const size_t* sizes,
+                           size_t stride_bytes, int nframes, int nstreams, float* out16, gicp_result* res);
+
 #ifdef __cplusplus
 }
 #endif
