@@ -20,6 +20,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <thread>
@@ -48,22 +49,83 @@ gicp_status fail(gicp_status s, const std::string& msg) {
                   std::string(#expr) + ": " + hipGetErrorString(_e));                       \
   } while (0)
 
+// Caching device allocator.  hipFree synchronizes the whole device, which
+// would serialize every ctx of a multi-stream batch (a new cloud index and
+// covariance set per scan); released blocks go to a per-(device, size class)
+// free list instead and are handed out again.  Safe because every entry
+// point that enqueues work on a buffer waits for it before returning, so a
+// buffer is idle whenever its owner releases it (the speculative no-op
+// iteration of an align touches only ctx-owned state, freed at ctx
+// destruction after a stream synchronize).
+struct DevicePool {
+  std::mutex m;
+  std::multimap<std::pair<int, size_t>, void*> free_blocks;
+  static size_t size_class(size_t b) {  // <= 12.5 % rounding, so same-shape clouds share a class
+    b = std::max<size_t>(b, 256);
+    size_t top = 1;
+    while ((top << 1) <= b) top <<= 1;
+    const size_t g = std::max<size_t>(top / 8, 256);
+    return (b + g - 1) / g * g;
+  }
+  hipError_t alloc(size_t cls, void** p) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+      std::lock_guard<std::mutex> lk(m);
+      auto it = free_blocks.find({dev, cls});
+      if (it != free_blocks.end()) {
+        *p = it->second;
+        free_blocks.erase(it);
+        return hipSuccess;
+      }
+    }
+    e = hipMalloc(p, cls);
+    if (e == hipErrorOutOfMemory) {  // give the cached blocks back and retry once
+      trim();
+      e = hipMalloc(p, cls);
+    }
+    return e;
+  }
+  void release(int dev, size_t cls, void* p) {
+    std::lock_guard<std::mutex> lk(m);
+    free_blocks.insert({{dev, cls}, p});
+  }
+  void trim() {
+    std::lock_guard<std::mutex> lk(m);
+    for (auto& kv : free_blocks) (void)hipFree(kv.second);
+    free_blocks.clear();
+  }
+};
+DevicePool& device_pool() {
+  static DevicePool* pool = new DevicePool();  // never destroyed: blocks live until exit
+  return *pool;
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  int dev = 0;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+  ~DevBuf() { reset(); }
+  void reset() {
+    if (p) device_pool().release(dev, bytes, p);
+    p = nullptr;
+    bytes = 0;
   }
   hipError_t ensure(size_t b) {
     if (b <= bytes && p) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-    hipError_t e = hipMalloc(&p, std::max<size_t>(b, 256));
-    if (e == hipSuccess) bytes = std::max<size_t>(b, 256);
+    reset();
+    const size_t cls = DevicePool::size_class(b);
+    hipError_t e = device_pool().alloc(cls, &p);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    (void)hipGetDevice(&dev);
+    bytes = cls;
     return e;
   }
   template <class T>
