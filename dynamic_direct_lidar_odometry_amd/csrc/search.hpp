@@ -292,48 +292,55 @@ __device__ __forceinline__ bool scan_leaves_lds(const CloudDev& c, int base, uns
   return improved;
 }
 
-template <int LV, class V>
-__device__ __forceinline__ void trav_level(const CloudDev& c, int base, unsigned long long mask, V& vis, WaveLds* L) {
-  // mask selects nodes of level LV (>= 1); their children are at LV-1
-  while (mask) {
-    const int ci = __builtin_ctzll(mask);
-    mask &= mask - 1;
-    const int node = base + ci;
-    const int cb = node * kFanout;
-    const int cnt = min(kFanout, lvl_cnt(c, LV - 1) - cb);
-    if constexpr (LV == 1) {
-      leaf_block(c, cb, cnt, vis, L);
-    } else {
-      const int lane = lane_id();
-      bool ov = false;
-      if (lane < cnt) {
-        const int o = lvl_off(c, LV - 1) + cb + lane;
-        ov = box_overlap(vis.box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
-      }
-      trav_level<LV - 1>(c, cb, __ballot(ov), vis, L);
-    }
-  }
-}
-
+// Depth-first walk with an explicit per-level stack of child masks (uniform
+// values: scalar registers), so leaf_block — and the visitor's scan it
+// inlines — has ONE call site whatever the depth (the kernels must stay
+// small enough for the instruction cache).  A single-level cloud is walked
+// as the children of a virtual level-1 node 0.
 template <class V>
 __device__ __forceinline__ void traverse(const CloudDev& c, V& vis, WaveLds* L) {
   const int T = c.nlevels - 1;
-  if (T == 0) {  // the leaves are the top level
-    leaf_block(c, 0, c.cnt0, vis, L);
-    return;
-  }
+  const int Tt = T < 1 ? 1 : T;
   const int lane = lane_id();
-  bool ov = false;
-  if (lane < lvl_cnt(c, T)) {
-    const int o = lvl_off(c, T) + lane;
-    ov = box_overlap(vis.box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
+  unsigned long long m1 = 0, m2 = 0, m3 = 0, m4 = 0;
+  int b1 = 0, b2 = 0, b3 = 0;
+  if (T == 0) {
+    m1 = 1ull;
+  } else {
+    bool ov = false;
+    if (lane < lvl_cnt(c, T)) {
+      const int o = lvl_off(c, T) + lane;
+      ov = box_overlap(vis.box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
+    }
+    const unsigned long long m = __ballot(ov);
+    if (T == 1) m1 = m; else if (T == 2) m2 = m; else if (T == 3) m3 = m; else m4 = m;
   }
-  const unsigned long long m = __ballot(ov);
-  switch (T) {
-    case 1: trav_level<1>(c, 0, m, vis, L); break;
-    case 2: trav_level<2>(c, 0, m, vis, L); break;
-    case 3: trav_level<3>(c, 0, m, vis, L); break;
-    default: trav_level<4>(c, 0, m, vis, L); break;
+  int lv = Tt;
+  while (true) {
+    unsigned long long m = lv == 1 ? m1 : lv == 2 ? m2 : lv == 3 ? m3 : m4;
+    if (m == 0ull) {
+      if (lv == Tt) break;
+      ++lv;
+      continue;
+    }
+    const int base = lv == 1 ? b1 : lv == 2 ? b2 : lv == 3 ? b3 : 0;
+    const int node = base + __builtin_ctzll(m);
+    m &= m - 1;
+    if (lv == 1) m1 = m; else if (lv == 2) m2 = m; else if (lv == 3) m3 = m; else m4 = m;
+    const int cb = node * kFanout;
+    const int cnt = min(kFanout, lvl_cnt(c, lv - 1) - cb);
+    if (lv == 1) {
+      leaf_block(c, cb, cnt, vis, L);
+      continue;
+    }
+    bool ov = false;
+    if (lane < cnt) {
+      const int o = lvl_off(c, lv - 1) + cb + lane;
+      ov = box_overlap(vis.box, ldg4(c.box_lo, o), ldg4(c.box_hi, o));
+    }
+    const unsigned long long cm = __ballot(ov);
+    --lv;
+    if (lv == 1) { m1 = cm; b1 = cb; } else if (lv == 2) { m2 = cm; b2 = cb; } else { m3 = cm; b3 = cb; }
   }
 }
 
@@ -382,31 +389,40 @@ __device__ __forceinline__ float box_extent(const WaveBox& b) {
 template <class V, int Q = 64>
 __device__ __forceinline__ void split_search(const CloudDev& c, V& vis, unsigned long long key, WaveLds* L) {
   const bool base_active = vis.active;
+  const int qi = lane_id() % Q;
+  // sub-ranges as a list of cut points (8 bits each): [cut_r, cut_{r+1})
+  unsigned long long cuts = (unsigned long long)Q << 8;   // {0, Q}: the whole group
+  int ncut = 2;
   const WaveBox whole = make_wave_box(base_active, vis.qx, vis.qy, vis.qz, vis.bound());
-  if (!(box_extent(whole) > kSplitExtent)) {
-    vis.box = whole;
-    traverse(c, vis, L);
-    return;
-  }
-  vis.st_splits += 1;
-  const int s = morton_jump_split<Q>(key, 0, Q);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int lo = h == 0 ? 0 : s, hi = h == 0 ? s : Q;
-    if (lo >= hi) continue;
-    const int qi = lane_id() % Q;
-    const bool act = base_active && qi >= lo && qi < hi;
-    const WaveBox hb = make_wave_box(act, vis.qx, vis.qy, vis.qz, vis.bound());
-    if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
-      vis.st_splits += 1;
-      const int s2 = morton_jump_split<Q>(key, lo, hi);
-      search_range<Q>(c, vis, base_active, lo, s2, L);
-      search_range<Q>(c, vis, base_active, s2, hi, L);
-    } else if (__any(act)) {
-      vis.active = act;
-      vis.box = hb;
-      traverse(c, vis, L);
+  if (box_extent(whole) > kSplitExtent) {
+    vis.st_splits += 1;
+    const int sp = morton_jump_split<Q>(key, 0, Q);
+    cuts = 0;
+    ncut = 1;
+    for (int h = 0; h < 2; ++h) {
+      const int lo = h == 0 ? 0 : sp, hi = h == 0 ? sp : Q;
+      if (lo < hi) {
+        const bool act = base_active && qi >= lo && qi < hi;
+        const WaveBox hb = make_wave_box(act, vis.qx, vis.qy, vis.qz, vis.bound());
+        if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
+          vis.st_splits += 1;
+          cuts |= (unsigned long long)morton_jump_split<Q>(key, lo, hi) << (8 * ncut);
+          ++ncut;
+        }
+      }
+      cuts |= (unsigned long long)hi << (8 * ncut);
+      ++ncut;
     }
+  }
+  // one traversal site for every sub-range
+  for (int r = 0; r + 1 < ncut; ++r) {
+    const int lo = (int)((cuts >> (8 * r)) & 0xff), hi = (int)((cuts >> (8 * (r + 1))) & 0xff);
+    if (lo >= hi) continue;
+    const bool act = base_active && qi >= lo && qi < hi;
+    if (!__any(act)) continue;
+    vis.active = act;
+    vis.box = make_wave_box(act, vis.qx, vis.qy, vis.qz, vis.bound());
+    traverse(c, vis, L);
   }
   vis.active = base_active;
 }
