@@ -222,7 +222,7 @@ def main():
     ap.add_argument("--no-batch", action="store_true", help="skip the frame-parallel S2S cfg5 leg")
     ap.add_argument("--batch-frames", type=int, default=201)
     ap.add_argument("--batch-unique", type=int, default=20)
-    ap.add_argument("--batch-streams", type=int, default=4)
+    ap.add_argument("--batch-streams", type=int, default=2)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -358,7 +358,7 @@ void invalidate_align(gicp_ctx* c) { c->have_align = false; }
 
 // Tuning knobs of the tile search (development; defaults are the tuned values)
 constexpr float kTileR0Default = 0.25f;
-constexpr float kSplitExtentDefault = 3.0f;
+constexpr float kSplitExtentDefault = 5.0f;
 float env_float(const char* name, float dflt) {
   const char* v = std::getenv(name);
   if (!v || !*v) return dflt;
@@ -410,6 +410,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
     j.defer_mask = reinterpret_cast<unsigned long long*>(u + sizeof(unsigned long long) * ns);
   }
   j.xcd_remap = (int)env_float("DDLO_XCD_REMAP", 0.f);
+  j.list_flush = (int)env_float("DDLO_LIST_FLUSH", 16.f);
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   return GICP_OK;
 }
@@ -637,7 +638,10 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   HIP_TRY(c->state_dev.ensure(sizeof(AlignState)));
   std::memset(c->state_host, 0, sizeof(AlignState));
   for (int i = 0; i < 6; ++i) c->state_host->final_hessian[7 * i] = 1.0;  // final_hessian_.setIdentity()
-  HIP_TRY(hipMemcpy(c->state_dev.p, c->state_host, sizeof(AlignState), hipMemcpyHostToDevice));
+  // stream-ordered (never the legacy stream: another ctx's thread may be
+  // capturing its align graph at this moment)
+  HIP_TRY(hipMemcpyAsync(c->state_dev.p, c->state_host, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   *out = c.release();
@@ -1018,7 +1022,8 @@ gicp_status gicp_debug_stats(gicp_ctx* c, int enable, unsigned int* out, size_t 
     const int q = search_queries_per_wave();
     const size_t groups = (c->src.cloud->n + q - 1) / q;
     const size_t words = std::min(max_words, (size_t)kStatFields * (groups + (groups + 3) / 4));  // phase A + B rows
-    HIP_TRY(hipMemcpy(out, c->stats.p, sizeof(unsigned int) * words, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(out, c->stats.p, sizeof(unsigned int) * words, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     if (nwords) *nwords = words;
   }
   return GICP_OK;
@@ -1120,14 +1125,25 @@ gicp_status gicp_s2s_batch(int device, const gicp_params* p, const float* const*
   const int nthreads = std::min(nstreams, npairs);
   std::vector<gicp_status> status(nthreads, GICP_OK);
   std::vector<std::string> errors(nthreads);
+  // contexts are made (and destroyed) on this thread, outside any worker's
+  // graph capture
+  std::vector<gicp_ctx*> ctxs(nthreads, nullptr);
+  for (int w = 0; w < nthreads; ++w) {
+    gicp_status s = gicp_ctx_create(device, &ctxs[w]);
+    if (!s) s = gicp_set_params(ctxs[w], p);
+    if (s) {
+      const std::string why = g_last_error;
+      for (auto* c : ctxs)
+        if (c) (void)gicp_ctx_destroy(c);
+      return fail(s, why);
+    }
+  }
   auto worker = [&](int w) {
     // pairs (t-1, t) for t in [t0, t1)
     const int t0 = 1 + (int)((long)npairs * w / nthreads);
     const int t1 = 1 + (int)((long)npairs * (w + 1) / nthreads);
-    gicp_ctx* c = nullptr;
-    gicp_status s = gicp_ctx_create(device, &c);
-    if (!s) s = gicp_set_params(c, p);
-    if (!s) s = gicp_set_target(c, clouds[t0 - 1], sizes[t0 - 1], stride_bytes);
+    gicp_ctx* c = ctxs[w];
+    gicp_status s = gicp_set_target(c, clouds[t0 - 1], sizes[t0 - 1], stride_bytes);
     for (int t = t0; t < t1 && !s; ++t) {
       s = gicp_set_source(c, clouds[t], sizes[t], stride_bytes, 1);
       if (!s) s = gicp_align(c, nullptr, out16 + 16 * (size_t)t, res ? &res[t] : nullptr);
@@ -1137,12 +1153,12 @@ gicp_status gicp_s2s_batch(int device, const gicp_params* p, const float* const*
       status[w] = s;
       errors[w] = g_last_error;
     }
-    if (c) (void)gicp_ctx_destroy(c);
   };
   std::vector<std::thread> pool;
   for (int w = 1; w < nthreads; ++w) pool.emplace_back(worker, w);
   worker(0);
   for (auto& th : pool) th.join();
+  for (auto* c : ctxs) (void)gicp_ctx_destroy(c);
   for (int w = 0; w < nthreads; ++w)
     if (status[w]) return fail(status[w], "s2s batch chunk " + std::to_string(w) + ": " + errors[w]);
   return GICP_OK;

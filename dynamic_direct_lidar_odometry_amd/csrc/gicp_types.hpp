@@ -108,6 +108,7 @@ struct AlignJob {
   unsigned long long* defer_mask;  // [ceil(n_src / 64)]
   unsigned long long* defer_key;   // [n_src]
   int xcd_remap;           // search: contiguous group range per XCD block label
+  int list_flush;          // search: leaf-list length that triggers an early scan
 };
 
 }  // namespace ddlo

@@ -866,7 +866,8 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
     }
     unsigned cst[6] = {0, 0, 0, 0, 0, 0};
     const unsigned tm_pro = stats ? (unsigned)__builtin_amdgcn_s_memtime() : 0u;
-    collect_scan_nn<Q>(tgt, CL, upper, qx, qy, qz, active, vis.best, vis.bestj, skey, cst);
+    collect_scan_nn<Q>(tgt, CL, upper, qx, qy, qz, active, vis.best, vis.bestj, skey, cst, job->split_extent,
+                       job->list_flush);
     vis.st_blocks = cst[0];
     vis.st_box = min((tm_pro - (unsigned)tm0) >> 4, 65535u) | (min((cst[1] - (unsigned)tm0) >> 4, 65535u) << 16);
     vis.st_exact = cst[2];
@@ -1764,10 +1765,21 @@ void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks,
       return v && *v ? std::atoi(v) : 3;  // 3 waves/SIMD: no scratch spills (same speed as 4, no spill traffic)
     }();
     const size_t lds = search_lds_bytes(job_upper_count);
-    if (occ == 3)
-      k_nn_search<kSearchQ, 3><<<sb, 64 * kLinWaves, lds, s>>>(job);
-    else
+    static const int q = [] {
+      const char* v = std::getenv("DDLO_SEARCH_Q");
+      return v && *v ? std::atoi(v) : kSearchQ;
+    }();
+    if (q == 8) {
+      const int g8 = (nsrc + 7) / 8;
+      k_nn_search<8, 3><<<std::max(1, (g8 + kLinWaves - 1) / kLinWaves), 64 * kLinWaves, lds, s>>>(job);
+    } else if (q == 32) {
+      const int g32 = (nsrc + 31) / 32;
+      k_nn_search<32, 3><<<std::max(1, (g32 + kLinWaves - 1) / kLinWaves), 64 * kLinWaves, lds, s>>>(job);
+    } else if (occ == 4) {
       k_nn_search<kSearchQ, 4><<<sb, 64 * kLinWaves, lds, s>>>(job);
+    } else {
+      k_nn_search<kSearchQ, 3><<<sb, 64 * kLinWaves, lds, s>>>(job);
+    }
   }
   k_moments<<<nblocks, 64 * kMomWaves, 0, s>>>(job);
 }

@@ -357,7 +357,7 @@ struct VisitStats {
 // Morton jump (at most twice => <= 4 sub-groups), searching each sub-range
 // with the other lanes inactive.  `key` is the lane's Morton key in the
 // query cloud's own quantisation (rigid transforms keep the geometry).
-constexpr float kSplitExtent = 3.0f;
+constexpr float kSplitExtent = 5.0f;   // tuned on cfg3 (3 m: 0.59, 5 m: 0.50, 10 m: 0.52 ms/scan)
 
 template <int Q = 64>
 __device__ __forceinline__ int morton_jump_split(unsigned long long key, int lo, int hi) {
@@ -582,7 +582,7 @@ constexpr int kListFlush = 16;      // scan once this many leaves are listed: ea
                                     // scans tighten the bounds that filter later blocks
 constexpr int kBlkMax = 32;         // candidate level-1 blocks per wavefront
 constexpr int kBatch = 8;           // leaves per LDS-DMA batch
-constexpr int kQMax = 16;           // queries per wavefront (collect path)
+constexpr int kQMax = 32;           // queries per wavefront (collect path)
 
 struct CollectLds {
   f4v q[kQMax];                     // per query: x, y, z, bound (bound < 0: inactive)
@@ -629,6 +629,7 @@ struct NNCollector {
   bool active;
   unsigned long long bk;
   unsigned st_blocks = 0, st_exact = 0, st_scan = 0, st_splits = 0;
+  int list_flush = kListFlush;   // leaf-list length that triggers an early scan
 
   __device__ __forceinline__ float bound() const { return __uint_as_float((unsigned)(bk >> 32)); }
 
@@ -676,6 +677,7 @@ struct NNCollector {
       st_scan += nb;
       __builtin_amdgcn_wave_barrier();
     }
+    for (int m = Q; m < 16; m <<= 1) k = umin64(k, __shfl_xor(k, m));
     if constexpr (Q <= 16) k = xor_min64<16>(k);
     if constexpr (Q <= 32) k = xor_min64<32>(k);
     if (active) bk = k;
@@ -726,7 +728,7 @@ struct NNCollector {
         __builtin_amdgcn_wave_barrier();
         pair_filter(cm);
       }
-      if (L->nleaves > kListFlush) flush_leaves(c);  // tightens bounds; list empties
+      if (L->nleaves > list_flush) flush_leaves(c);  // tightens bounds; list empties
     }
     if (lane == 0) L->nblocks = 0;
     __builtin_amdgcn_wave_barrier();
@@ -828,7 +830,8 @@ struct NNCollector {
 template <int Q>
 __device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L, const f4v* U, float qx, float qy,
                                                 float qz, bool active, float& best, int& bestj,
-                                                unsigned long long key, unsigned (&st)[6]) {
+                                                unsigned long long key, unsigned (&st)[6],
+                                                float split_extent = kSplitExtent, int list_flush = kListFlush) {
   const int lane = lane_id();
   const int qi = lane % Q;
   if (lane < Q) L->q[lane] = f4v{qx, qy, qz, active ? best : -1.f};
@@ -846,6 +849,7 @@ __device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L
   col.qz = qz;
   col.active = active;
   col.bk = dkey(best, bestj);
+  col.list_flush = list_flush;
   // Query sub-ranges: the whole group, or — when the union box of its balls
   // is wider than kSplitExtent — up to 4 Morton-jump sub-ranges, each walked
   // with its own (smaller) box.  A runtime worklist keeps one walk site.
@@ -856,7 +860,7 @@ __device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L
     L->nsr = 1;
   }
   __builtin_amdgcn_wave_barrier();
-  if (box_extent(whole) > kSplitExtent) {
+  if (box_extent(whole) > split_extent) {
     col.st_splits += 1;
     const int sp = morton_jump_split<Q>(key, 0, Q);
     int nsr = 0;
@@ -865,7 +869,7 @@ __device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L
       if (lo >= hi) continue;
       const bool act = active && qi >= lo && qi < hi;
       const WaveBox hb = make_wave_box(act, qx, qy, qz, col.bound());
-      if (box_extent(hb) > kSplitExtent && hi - lo > 4) {
+      if (box_extent(hb) > split_extent && hi - lo > 4) {
         col.st_splits += 1;
         const int s2 = morton_jump_split<Q>(key, lo, hi);
         if (lane == 0) {
