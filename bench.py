@@ -40,6 +40,20 @@ sys.path.insert(0, HERE)
 
 METRIC = "GICP iters/sec + ms/scan, 131k-pt source → 500k-pt submap; pose Δ vs CPU ref"
 HBM_PEAK_GBS = 8000.0
+# rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same workload
+# (tools/pmc_traffic.sh -> tools/pmc_traffic.py), committed per round
+TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r01_traffic.json"))
+
+
+def pmc_traffic():
+    """Measured HBM-side bytes per linearize launch (FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md corrections), or None when no PMC pass is on file."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            d = json.load(f)
+        return int(d["bytes_per_linearize"]), os.path.relpath(TRAFFIC_JSON, HERE)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def log(*a):
@@ -291,6 +305,7 @@ def main():
     ctx.synchronize()
     avg_launch_s = (lin_ms / max(lin_launches, 1)) * 1e-3
     bytes_per_launch = 76.0 * len(src)   # SURVEY.md §8(d) B_lin = 76 * N_s
+    traffic, traffic_src = pmc_traffic()
     achieved_gbs = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
 
     result = {
@@ -312,7 +327,9 @@ def main():
                    "iterations_per_scan": round(iters_total / steps_total, 3),
                    "parallelism": f"replicas x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": None,
+                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
+                     "traffic_unit": "bytes per linearize launch (L2->fabric, Infinity-Cache hits included)",
+                     "traffic_source": traffic_src,
                      "kernel": "linearize = k_nn_search + k_moments (per outer iteration)",
                      "avg_launch_us": round(avg_launch_s * 1e6, 2),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch)},
