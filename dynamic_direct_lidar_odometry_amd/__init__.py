@@ -12,6 +12,7 @@ visible, every entry point raises.
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 
 import numpy as np
@@ -126,6 +127,7 @@ def load():
         "gicp_set_comm": (I, [P, P, S, I, I]),
         "gicp_get_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
         "gicp_s2s_batch": (I, [I, C.POINTER(GicpParams), P, P, S, I, I, P, P]),
+        "gicp_residual_image": (I, [P, D, D, I, I, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -287,6 +289,15 @@ class Context:
         out = np.zeros(n, np.float64)
         self._check(self.L.gicp_get_residuals(self.h, _ptr(out), n))
         return out
+
+    def residual_image(self, theta_min=-math.pi / 3, theta_max=math.pi / 3, width=512, height=512, with_xyz=False):
+        """Residual image of the last linearization (odom.cc:804-827): (H, W)
+        float32 residuals and, optionally, the (H, W, 3) winning points."""
+        img = np.zeros((height, width), np.float32)
+        xyz = np.zeros((height, width, 3), np.float32) if with_xyz else None
+        self._check(self.L.gicp_residual_image(self.h, theta_min, theta_max, width, height, _ptr(img),
+                                               None if xyz is None else _ptr(xyz)))
+        return (img, xyz) if with_xyz else img
 
     def correspondences(self):
         n = self.size(SOURCE)

@@ -892,6 +892,36 @@ gicp_status gicp_get_residuals(gicp_ctx* c, double* out, size_t n) {
   return GICP_OK;
 }
 
+gicp_status gicp_residual_image(gicp_ctx* c, double theta_min, double theta_max, int width, int height, float* img,
+                                float* xyz) {
+  if (!c || !img) return fail(GICP_EINVAL, "null argument");
+  if (width <= 0 || height <= 0 || (long)width * height > (1L << 28) || !(theta_max > theta_min))
+    return fail(GICP_EINVAL, "invalid image geometry");
+  if (!c->have_align || !c->src.cloud || !c->tgt.cloud) return fail(GICP_ESTATE, "no linearization to report residuals of");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  const int n = c->src.cloud->n;
+  const size_t npix = (size_t)width * height;
+  HIP_TRY(c->tmp_out.ensure(sizeof(double) * n));
+  launch_residuals(c->stream, c->job_dev.as<AlignJob>(), n, c->tmp_out.as<double>());
+  if (c->comm)  // sharded: global residual = min over ranks (see gicp_get_residuals)
+    NCCL_TRY(rccl().all_reduce(c->tmp_out.p, c->tmp_out.p, n, ncclFloat64, ncclMin, c->comm, c->stream));
+  DevBuf winner, dimg, dxyz;
+  HIP_TRY(winner.ensure(sizeof(int) * npix));
+  HIP_TRY(dimg.ensure(sizeof(float) * npix));
+  if (xyz) HIP_TRY(dxyz.ensure(sizeof(float) * 3 * npix));
+  HIP_TRY(hipMemsetAsync(winner.p, 0xff, sizeof(int) * npix, c->stream));  // -1: no point
+  const CloudData& cd = *c->src.cloud;
+  launch_residual_image(c->stream, cd.pts.as<float4>(), cd.perm.as<int>(), cd.inv_perm.as<int>(), n,
+                        c->tmp_out.as<double>(), theta_min, theta_max, width, height, winner.as<int>(),
+                        dimg.as<float>(), xyz ? dxyz.as<float>() : nullptr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(img, dimg.p, sizeof(float) * npix, hipMemcpyDeviceToHost, c->stream));
+  if (xyz) HIP_TRY(hipMemcpyAsync(xyz, dxyz.p, sizeof(float) * 3 * npix, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GICP_OK;
+}
+
 gicp_status gicp_get_correspondences(gicp_ctx* c, int32_t* corr, float* sq_dist, size_t n) {
   if (!c || (!corr && !sq_dist)) return fail(GICP_EINVAL, "null argument");
   if (!c->have_align || !c->src.cloud) return fail(GICP_ESTATE, "no linearization");

@@ -1661,6 +1661,54 @@ __global__ __launch_bounds__(256) void k_residuals(const AlignJob* __restrict__ 
   }
 }
 
+// Residual image (odom.cc:804-827 -> detection.cpp
+// projectResiduals :203-252).  Pixel of source point i (sensor frame, the
+// scan the residuals belong to): theta = atan2(x, z), phi = atan2(y,
+// sqrt(x^2 + z^2)) in double, u = int((theta - tmin) / (tmax - tmin) * W),
+// v likewise with phi; points outside [0, W) x [0, H) are skipped.
+// (Which atan2/sqrt overload the reference's unqualified calls on float
+// members resolve to depends on the headers reaching odom.cc; this takes
+// the C double functions.  Only pixel-boundary cases can differ.)  The
+// reference fills the image in point order, so the HIGHEST original index
+// that lands on a pixel wins: atomicMax of the index, then a gather pass.
+__global__ __launch_bounds__(256) void k_resimg_claim(const float4* __restrict__ pts, const int* __restrict__ perm,
+                                                      int n, double tmin, double tmax, int W, int H,
+                                                      int* __restrict__ winner) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = pts[i];
+  // x*x + z*z is float arithmetic in the reference (PointXYZI members);
+  // atan2 / sqrt then run on the promoted values
+  const float xz2 = p.x * p.x + p.z * p.z;
+  const double theta = atan2((double)p.x, (double)p.z);
+  const double phi = atan2((double)p.y, sqrt((double)xz2));
+  const int u = (int)((theta - tmin) / (tmax - tmin) * W);
+  const int v = (int)((phi - tmin) / (tmax - tmin) * H);
+  if (u < 0 || u >= W || v < 0 || v >= H) return;
+  atomicMax(&winner[(size_t)v * W + u], perm[i]);
+}
+
+__global__ __launch_bounds__(256) void k_resimg_fill(const int* __restrict__ winner, int npix,
+                                                     const double* __restrict__ residual,
+                                                     const float4* __restrict__ pts, const int* __restrict__ inv_perm,
+                                                     float* __restrict__ img, float* __restrict__ xyz) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const int o = winner[p];
+  float r = 0.f, x = 0.f, y = 0.f, z = 0.f;   // empty pixel: PCL's default point, intensity 0
+  if (o >= 0) {
+    r = (float)residual[o];
+    const float4 q = pts[inv_perm[o]];
+    x = q.x; y = q.y; z = q.z;
+  }
+  img[p] = r;
+  if (xyz) {
+    xyz[3 * (size_t)p + 0] = x;
+    xyz[3 * (size_t)p + 1] = y;
+    xyz[3 * (size_t)p + 2] = z;
+  }
+}
+
 // pcl::transformPointCloud with final_transformation_ (float 4x4)
 __global__ __launch_bounds__(256) void k_transform(const float4* __restrict__ pts, int n, const int* __restrict__ perm,
                                                    const float* __restrict__ T16, float* __restrict__ out,
@@ -1797,6 +1845,12 @@ int moment_blocks(int nsrc) {
 }
 void launch_lm_step(hipStream_t s, const AlignJob* job) { k_lm_step<<<1, kLmThreads, 0, s>>>(job); }
 void launch_mom_reduce(hipStream_t s, const AlignJob* job) { k_mom_reduce<<<1, kLmThreads, 0, s>>>(job); }
+void launch_residual_image(hipStream_t s, const float4* pts, const int* perm, const int* inv_perm, int n,
+                           const double* residual, double tmin, double tmax, int W, int H, int* winner, float* img,
+                           float* xyz) {
+  k_resimg_claim<<<cdiv(n, 256), 256, 0, s>>>(pts, perm, n, tmin, tmax, W, H, winner);
+  k_resimg_fill<<<cdiv((long)W * H, 256), 256, 0, s>>>(winner, W * H, residual, pts, inv_perm, img, xyz);
+}
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out) {
   k_residuals<<<group_blocks(nsrc), 256, 0, s>>>(job, out);
 }

@@ -29,6 +29,9 @@ int moment_blocks(int nsrc);  // slab rows written by the moment kernel
 void launch_lm_step(hipStream_t s, const AlignJob* job);
 void launch_mom_reduce(hipStream_t s, const AlignJob* job);  // sharded align: slab -> job->mom
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out);
+void launch_residual_image(hipStream_t s, const float4* pts, const int* perm, const int* inv_perm, int n,
+                           const double* residual, double tmin, double tmax, int W, int H, int* winner, float* img,
+                           float* xyz);
 void launch_transform(hipStream_t s, const float4* pts, int n, const int* perm, const float* T16, float* out,
                       size_t stride_floats);
 void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr, float* sqd);

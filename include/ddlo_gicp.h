@@ -165,6 +165,17 @@ gicp_status gicp_align(struct gicp_ctx* ctx, const float* guess16, float* out16,
  * 1-NN distance of every source point (original order) from the LAST
  * update_correspondences; the trans argument is ignored there too. */
 gicp_status gicp_get_residuals(struct gicp_ctx* ctx, double* out, size_t n);
+/* Residual image for the dynamic-object detection:
+ * the projection OdomNode does after getResiduals (odom.cc:804-827; the
+ * reference uses theta in [-60, 60] deg and 512 x 512) feeding
+ * DetectionModule::projectResiduals (detection.cpp:203-252).  Source point i
+ * (sensor frame) goes to u = int((atan2(x, z) - tmin) / (tmax - tmin) * W),
+ * v = int((atan2(y, hypot(x, z)) - tmin) / (tmax - tmin) * H); the highest
+ * original index landing on a pixel wins (the reference's write order).
+ * img: H*W floats, the residual (0 where no point); xyz (optional): H*W*3,
+ * the winning point (0 where none). */
+gicp_status gicp_residual_image(struct gicp_ctx* ctx, double theta_min, double theta_max, int width, int height,
+                                float* img, float* xyz);
 /* correspondences_ / sq_distances_ of the last linearization, original
  * indices (-1 = no correspondence within max_correspondence_distance).
  * sq_dist is the unbounded 1-NN squared distance of every point, as

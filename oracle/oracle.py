@@ -246,3 +246,23 @@ def regularize(C9, reg):
     C9 = np.ascontiguousarray(C9, np.float64); out = np.zeros(9)
     lib().oref_regularize(_fp(C9), REG[reg] if isinstance(reg, str) else reg, _fp(out))
     return out.reshape(3, 3)
+
+
+def residual_image(points, residuals, theta_min=-np.pi / 3, theta_max=np.pi / 3, width=512, height=512):
+    """Residual image restated from odom.cc:804-827 (projection, point order:
+    the last point written to a pixel wins) and detection.cpp:203-252
+    (projectResiduals: intensity -> CV_32F, empty pixels 0).  x*x + z*z in
+    float32 as on PointXYZI members; atan2 / sqrt in double."""
+    p = np.asarray(points, np.float32).reshape(-1, 3)
+    xz2 = (p[:, 0] * p[:, 0] + p[:, 2] * p[:, 2]).astype(np.float64)
+    theta = np.arctan2(p[:, 0].astype(np.float64), p[:, 2].astype(np.float64))
+    phi = np.arctan2(p[:, 1].astype(np.float64), np.sqrt(xz2))
+    u = ((theta - theta_min) / (theta_max - theta_min) * width).astype(np.int64)   # static_cast<int>: toward 0
+    v = ((phi - theta_min) / (theta_max - theta_min) * height).astype(np.int64)
+    keep = (u >= 0) & (u < width) & (v >= 0) & (v < height)
+    winner = np.full(width * height, -1, np.int64)
+    np.maximum.at(winner, (v * width + u)[keep], np.flatnonzero(keep))
+    img = np.zeros(width * height, np.float32)
+    hit = winner >= 0
+    img[hit] = np.asarray(residuals, np.float64)[winner[hit]].astype(np.float32)
+    return img.reshape(height, width), winner.reshape(height, width)
