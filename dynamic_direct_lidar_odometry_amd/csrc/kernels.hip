@@ -309,48 +309,41 @@ struct KnnVisitor : VisitStats {
   float qx, qy, qz;
   bool active;
   int k;
-  float D[KCAP];
-  int J[KCAP];
-  float wd;   // worst kept (bound)
-  int wj;
+  // kept neighbours as order-preserving (squared distance, sorted position)
+  // keys, ascending: the exact rule (d < D) || (d == D && j < J) of
+  // KNNResultSet + the position tie-break is one u64 compare per slot
+  unsigned long long K[KCAP];
+  unsigned long long wk;   // worst kept key (bound)
+  float wd;                // its distance
   int skip_lo, skip_hi;
 
+  __device__ __forceinline__ float dist(int s) const { return __uint_as_float((unsigned)(K[s] >> 32)); }
+  __device__ __forceinline__ int idx(int s) const { return (int)(unsigned)K[s]; }
   __device__ __forceinline__ void init(int kk) {
     k = kk;
 #pragma unroll
-    for (int s = 0; s < KCAP; ++s) {
-      D[s] = INFINITY;
-      J[s] = -1;
-    }
+    for (int s = 0; s < KCAP; ++s) K[s] = dkey(INFINITY, -1);
+    wk = K[0];
     wd = INFINITY;
-    wj = -1;
     skip_lo = 1;
     skip_hi = 0;
   }
   __device__ __forceinline__ void update_worst() {
     if constexpr (EXACT) {
-      wd = D[KCAP - 1];
-      wj = J[KCAP - 1];
+      wk = K[KCAP - 1];
     } else {
 #pragma unroll
-      for (int s = 0; s < KCAP; ++s) {
-        if (s == k - 1) {
-          wd = D[s];
-          wj = J[s];
-        }
-      }
+      for (int s = 0; s < KCAP; ++s)
+        if (s == k - 1) wk = K[s];
     }
+    wd = __uint_as_float((unsigned)(wk >> 32));
   }
-  __device__ __forceinline__ void insert(float d, int j) {
+  __device__ __forceinline__ void insert(unsigned long long key) {
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
-      const bool lt = d < D[s] || (d == D[s] && (unsigned)j < (unsigned)J[s]);
-      const float td = lt ? D[s] : d;
-      const int tj = lt ? J[s] : j;
-      D[s] = lt ? d : D[s];
-      J[s] = lt ? j : J[s];
-      d = td;
-      j = tj;
+      const unsigned long long lo = umin64(key, K[s]);
+      key = key < K[s] ? K[s] : key;
+      K[s] = lo;
     }
     update_worst();
   }
@@ -359,9 +352,8 @@ struct KnnVisitor : VisitStats {
   __device__ __forceinline__ void process(const WaveLds* L, int start) {
     for (int j = 0; j < kLeafSize; ++j) {
       const float d = dist2(qx, qy, qz, L->px[j], L->py[j], L->pz[j]);
-      const int pj = start + j;
-      const bool cand = active && (d < wd || (d == wd && (unsigned)pj < (unsigned)wj));
-      if (cand) insert(d, pj);
+      const unsigned long long key = dkey(d, start + j);
+      if (active && key < wk) insert(key);
     }
   }
   __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
@@ -425,7 +417,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
       if (s < k) {
-        const float4 p = ldg4(c.pts, vis.J[s]);
+        const float4 p = ldg4(c.pts, vis.idx(s));
         mx += (double)p.x;
         my += (double)p.y;
         mz += (double)p.z;
@@ -438,7 +430,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
       if (s < k) {
-        const float4 p = ldg4(c.pts, vis.J[s]);
+        const float4 p = ldg4(c.pts, vis.idx(s));
         const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
         C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
         C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
@@ -480,9 +472,9 @@ __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __r
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
       if (s < k) {
-        const int j = vis.J[s];
+        const int j = vis.idx(s);
         out_idx[(size_t)i * k + s] = j >= 0 ? c.perm[j] : -1;
-        out_d[(size_t)i * k + s] = vis.D[s];
+        out_d[(size_t)i * k + s] = vis.dist(s);
       }
     }
   }
