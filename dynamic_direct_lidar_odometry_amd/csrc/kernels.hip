@@ -1328,43 +1328,57 @@ __device__ __forceinline__ double Sgen(int c, int r, int s) {
 
 // H = sum J^T M J, b = sum J^T M e with J = [skew(q) | -I] (nano_gicp_impl.hpp:317-324),
 // one entry per thread: e in [0,36) -> H(e/6, e%6), e in [36,42) -> b(e-36).
+// Column i of the generators S_c has exactly two non-zeros S_c[r][i] = +-1:
+// (c, r, sign) = kSk[i][0..1], ordered by c, so the 4-term sums below add
+// the same products in the same order as the full sum over (c, d, r, q).
+__device__ __forceinline__ void skew_nz(int i, int p, int& c, int& r, double& sg) {
+  // i=0: S_1[2][0]=-1, S_2[1][0]=+1; i=1: S_0[2][1]=+1, S_2[0][1]=-1; i=2: S_0[1][2]=-1, S_1[0][2]=+1
+  const int cc[3][2] = {{1, 2}, {0, 2}, {0, 1}};
+  const int rr[3][2] = {{2, 1}, {2, 0}, {1, 0}};
+  const double ss[3][2] = {{-1.0, 1.0}, {1.0, -1.0}, {-1.0, 1.0}};
+  c = i == 0 ? cc[0][p] : i == 1 ? cc[1][p] : cc[2][p];
+  r = i == 0 ? rr[0][p] : i == 1 ? rr[1][p] : rr[2][p];
+  sg = i == 0 ? ss[0][p] : i == 1 ? ss[1][p] : ss[2][p];
+}
 __device__ double normal_eq_entry(const Moments& mo, int e) {
   if (e >= 36) {
     const int i = e - 36;
     if (i >= 3) return -mo.G(i - 3, 3);  // b_t = -G(:,3)
     double s = 0.0;                      // b_r(i) = sum_c sum_r S_c[r][i] G(r,c)
-    for (int c = 0; c < 3; ++c)
-      for (int r = 0; r < 3; ++r) {
-        const double sr = Sgen(c, r, i);
-        if (sr != 0.0) s += sr * mo.G(r, c);
-      }
+    for (int p = 0; p < 2; ++p) {
+      int c, r;
+      double sg;
+      skew_nz(i, p, c, r, sg);
+      s += sg * mo.G(r, c);
+    }
     return s;
   }
   const int i = e / 6, j = e % 6;
   if (i < 3 && j < 3) {  // H_rr(i,j) = sum_{c,d} sum_{r,q} S_c[r][i] W(c,d)[r][q] S_d[q][j]
     double s = 0.0;
-    for (int c = 0; c < 3; ++c)
-      for (int d = 0; d < 3; ++d)
-        for (int r = 0; r < 3; ++r) {
-          const double sr = Sgen(c, r, i);
-          if (sr == 0.0) continue;
-          for (int q = 0; q < 3; ++q) {
-            const double sq = Sgen(d, q, j);
-            if (sq == 0.0) continue;
-            s += sr * mo.W(c, d, r, q) * sq;
-          }
-        }
+    for (int p = 0; p < 2; ++p) {
+      int c, r;
+      double sr;
+      skew_nz(i, p, c, r, sr);
+      for (int u = 0; u < 2; ++u) {
+        int d, q;
+        double sq;
+        skew_nz(j, u, d, q, sq);
+        s += sr * mo.W(c, d, r, q) * sq;
+      }
+    }
     return s;
   }
   if (i >= 3 && j >= 3) return mo.W(3, 3, i - 3, j - 3);  // H_tt = sum M
   // H_rt(a, t) = -sum_c sum_r S_c[r][a] W(c,3)[r][t]
   const int a = i < 3 ? i : j, t = i < 3 ? j - 3 : i - 3;
   double s = 0.0;
-  for (int c = 0; c < 3; ++c)
-    for (int r = 0; r < 3; ++r) {
-      const double sr = Sgen(c, r, a);
-      if (sr != 0.0) s += sr * mo.W(c, 3, r, t);
-    }
+  for (int p = 0; p < 2; ++p) {
+    int c, r;
+    double sr;
+    skew_nz(a, p, c, r, sr);
+    s += sr * mo.W(c, 3, r, t);
+  }
   return -s;
 }
 
@@ -1470,6 +1484,9 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
   __shared__ int tr_conv[kMaxTrials];
   __shared__ double lambda0_s;
   const int tid = threadIdx.x;
+  // state words thread 0 needs at the end, loaded now (overlaps the slab loads)
+  const int it_pre = st->iter;
+  const int trials_pre = st->lm_trials;
   if (job->premom) {  // moments already reduced (and summed across shards)
     if (tid < kSlabStride) mom[tid] = gp((const double*)job->mom)[tid];
     __syncthreads();
@@ -1533,16 +1550,17 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
     for (int e = 0; e < 3; ++e) tr_t[tid][e] = td[e];
   }
   __syncthreads();
+  // the per-linearize record, stored by many threads at once
+  if (tid < kSlabStride) st->last_mom[tid] = mom[tid];
+  else if (tid < kSlabStride + 9) st->last_lin_R[tid - kSlabStride] = R[tid - kSlabStride];
+  else if (tid < kSlabStride + 12) st->last_lin_t[tid - kSlabStride - 9] = t[tid - kSlabStride - 9];
+  else if (tid < kSlabStride + 18) st->last_b[tid - kSlabStride - 12] = bs[tid - kSlabStride - 12];
   if (tid != 0) return;
 
-  const int it = st->iter;
+  const int it = it_pre;
   st->nr_iterations = it;
   st->final_cost = mo.y0();
   st->num_corr = (int)mo.count();
-  for (int e = 0; e < 9; ++e) st->last_lin_R[e] = R[e];
-  for (int e = 0; e < 3; ++e) st->last_lin_t[e] = t[e];
-  for (int e = 0; e < 6; ++e) st->last_b[e] = bs[e];
-  for (int e = 0; e < kSlabStride; ++e) st->last_mom[e] = mom[e];
 
   bool ok = false;
   int chosen = -1;
@@ -1567,7 +1585,7 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
       chosen = i;
       break;
     }
-    st->lm_trials += ok ? chosen + 1 : ntr;
+    st->lm_trials = trials_pre + (ok ? chosen + 1 : ntr);
     if (accept) {
       const double c = 2 * tr_rho[chosen] - 1;
       st->lambda = tr_lambda[chosen] * fmax(1.0 / 3.0, 1 - c * c * c);
