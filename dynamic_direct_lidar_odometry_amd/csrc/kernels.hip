@@ -658,7 +658,7 @@ __device__ __forceinline__ void load_sym6(const __attribute__((address_space(1))
 constexpr int kLinWaves = 4;      // waves per block (search and moment kernels)
 constexpr float kOptR2 = 0.25f;     // optimistic first-pass radius^2 (0.5 m)
 constexpr int kSearchQ = 16;        // queries per wavefront in the correspondence search
-constexpr int kSeedW = 4;           // Morton-window seed points per slice lane
+constexpr int kSeedW = 8;           // Morton-window seed points per slice lane
 
 __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
