@@ -465,9 +465,11 @@ gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks) {
     gicp_status s = enqueue_iteration(c, jd, nblocks);
     if (s) return s;
   }
-  // publish {iter, done} to pinned host memory at the end of the chunk
-  HIP_TRY(hipMemcpyAsync(c->flag_host, &c->state_dev.as<AlignState>()->iter, 2 * sizeof(int), hipMemcpyDeviceToHost,
-                         c->stream));
+  // publish the whole state to pinned host memory at the end of the chunk:
+  // the host polls {iter, done} from it, and once done it already holds the
+  // final pose, so no separate read-back round trip follows convergence (a
+  // speculative no-op chunk behind it rewrites the same bytes)
+  HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
   return GICP_OK;
 }
 
@@ -538,11 +540,9 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   const int nchunks = 1 + (max_it - first);
   while ((int)c->chunk_ev.size() < nchunks) {
     hipEvent_t e;
-    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipEventCreate(&e));  // timed: the last one ends the align's device time
     c->chunk_ev.push_back(e);
   }
-  c->flag_host[0] = 0;
-  c->flag_host[1] = 0;
   gicp_status s = launch_chunk(true);
   if (s) return s;
   HIP_TRY(hipEventRecord(c->chunk_ev[0], c->stream));
@@ -559,8 +559,8 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   int k = 0;
   for (;;) {
     HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
-    const volatile int* fl = c->flag_host;
-    if (fl[1] || k == nchunks - 1) break;
+    const volatile AlignState* st = c->state_host;
+    if (st->done || k == nchunks - 1) break;
     if (launched < nchunks) {
       s = launch_chunk(false);
       if (s) return s;
@@ -570,7 +570,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     ++k;
   }
   *final_chunk = k;
-  c->predicted_iters = std::max(1, c->flag_host[0]);
+  c->predicted_iters = std::max(1, (int)((const volatile AlignState*)c->state_host)->iter);
   return GICP_OK;
 }
 
@@ -814,6 +814,7 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
   s = fill_job(c, guess16, nblocks);
   if (s) return s;
   const int max_it = c->job_host->max_iterations;
+  hipEvent_t end_ev = c->ev1;
   HIP_TRY(hipEventRecord(c->ev0, c->stream));
   if (c->profiling || max_it <= 0) {
     s = max_it > 0 ? run_align_eager_profiled(c, max_it, nblocks) : GICP_OK;
@@ -826,12 +827,10 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
     int fc = 0;
     s = run_align_graph(c, max_it, nblocks, &fc);
     if (s) return s;
-    // the state is final after chunk fc; read it on the copy stream so the
-    // (at most one) speculative no-op chunk still queued does not delay us
-    HIP_TRY(hipStreamWaitEvent(c->copy_stream, c->chunk_ev[fc], 0));
-    HIP_TRY(hipEventRecord(c->ev1, c->copy_stream));
-    HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->copy_stream));
-    HIP_TRY(hipStreamSynchronize(c->copy_stream));
+    // chunk fc's end-of-chunk copy already put the final state in
+    // state_host; the (at most one) speculative no-op chunk still queued
+    // does not delay the return
+    end_ev = c->chunk_ev[fc];
   }
   const AlignState& st = *c->state_host;
   c->have_align = st.iter > 0;
@@ -856,7 +855,7 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
     std::memcpy(res->final_hessian, st.final_hessian, sizeof(res->final_hessian));
     res->lm_lambda = st.lambda;
     float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, end_ev));
     res->device_ms = ms;
     if (c->profiling) {
       double tot = 0.0;
