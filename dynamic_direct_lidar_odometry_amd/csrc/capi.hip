@@ -271,6 +271,7 @@ struct gicp_ctx {
   int nranks = 1, rank = 0;
   DevBuf mom;          // [kSlabStride] reduced moments, all-reduced in place
   DevBuf unres;        // phase-B search state: [defer_key u64 x n][defer_mask u64 x groups]
+  bool speculate = true;    // queue a follow-on chunk before the first one's flag is seen
   bool comm_graphs = true;  // RCCL captured into the chunk graphs (else eager chunks)
 };
 
@@ -501,9 +502,10 @@ void drop_graphs(gicp_ctx* c) {
 // align's iteration count on this ctx: aligns of consecutive scans converge
 // in similar counts) followed by single-iteration chunks, keeping one
 // speculative single-iteration chunk queued ahead while the host checks the
-// previous chunk's done flag.  After convergence at most that one no-op
-// iteration (three early-exiting kernels) runs, overlapping the final state
-// read-back.  Returns the index of the chunk after which the state is final.
+// previous chunk's done flag (from the first chunk on only when the previous
+// align needed more than its first chunk).  After convergence at most that
+// one no-op iteration (three early-exiting kernels) runs.  Returns the index
+// of the chunk after which the state is final.
 gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chunk) {
   const void* jd = c->job_dev.p;
   // key: grid, job buffer and whether RCCL is in the chunk
@@ -547,7 +549,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   if (s) return s;
   HIP_TRY(hipEventRecord(c->chunk_ev[0], c->stream));
   int launched = 1;
-  if (nchunks > 1) {
+  if (nchunks > 1 && c->speculate) {
     s = launch_chunk(false);
     if (s) return s;
     HIP_TRY(hipEventRecord(c->chunk_ev[1], c->stream));
@@ -561,7 +563,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
     const volatile AlignState* st = c->state_host;
     if (st->done || k == nchunks - 1) break;
-    if (launched < nchunks) {
+    while (launched < nchunks && launched <= k + 2) {  // keep one chunk queued ahead of k+1
       s = launch_chunk(false);
       if (s) return s;
       HIP_TRY(hipEventRecord(c->chunk_ev[launched], c->stream));
@@ -570,6 +572,10 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     ++k;
   }
   *final_chunk = k;
+  // Speculate next time only if this align outran its predicted first chunk:
+  // when the prediction held, the queued no-op chunk only delays the next
+  // align (A/B at cfg 3: 0.466 -> 0.459 ms/scan without it).
+  c->speculate = k > 0;
   c->predicted_iters = std::max(1, (int)((const volatile AlignState*)c->state_host)->iter);
   return GICP_OK;
 }
