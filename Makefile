@@ -14,7 +14,7 @@ all: lib oracle facade
 
 lib: $(LIBDIR)/libddlo_gicp.so
 
-$(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/search.hpp $(CSRC)/tile_search.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
+$(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/search.hpp $(CSRC)/nn_tasks.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -137,7 +137,7 @@ struct DevBuf {
 // Immutable device cloud + search hierarchy (shared between ctxs/sides).
 struct CloudData {
   int n = 0;
-  DevBuf pts, keys, perm, inv_perm, box_lo, box_hi, quant;
+  DevBuf pts, keys, perm, inv_perm, box_lo, box_hi, quant, soa;
   int nlevels = 0;
   int lvl_off[kMaxLevels] = {0};
   int lvl_cnt[kMaxLevels] = {0};
@@ -153,6 +153,7 @@ struct CloudData {
     c.box_lo = box_lo.as<float4>();
     c.box_hi = box_hi.as<float4>();
     c.quant = quant.as<float>();
+    c.soa = soa.as<float>();
     c.n = n;
     c.nlevels = nlevels;
     c.off0 = lvl_off[0]; c.off1 = lvl_off[1]; c.off2 = lvl_off[2]; c.off3 = lvl_off[3]; c.off4 = lvl_off[4];
@@ -238,6 +239,8 @@ struct hipExecGraphPair {
   hipGraphExec_t ge = nullptr;
 };
 
+constexpr int kDefaultPredictedIters = 4;
+
 struct gicp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -249,16 +252,23 @@ struct gicp_ctx {
   DevBuf corr, sqd, slab, job_dev, state_dev, tmp_out, stats;
   bool stats_on = false;
   AlignJob* job_host = nullptr;   // pinned
-  AlignState* state_host = nullptr;  // pinned
+  // pinned, two slots: chunk k publishes its end state to slot k % 2, so the
+  // (at most one) chunk queued behind the one the host is reading never
+  // writes the bytes being read (no torn pose / done / iter)
+  AlignState* state_host = nullptr;
+  int state_slot = 0;              // slot holding the state of the last align / linearize
+  hipEvent_t tail_ev = nullptr;    // last chunk launched by the last align (may still be queued)
+  bool tail_pending = false;
   int* flag_host = nullptr;       // pinned
   bool have_align = false;        // a linearize ran against the current src/tgt
   int last_nsrc = 0;
-  // chunk graphs: [init + n iterations + flag copy] for the predicted
-  // iteration count n (one per n, index n - 1) and [1 iteration + flag copy]
+  // chunk graphs: [init + n iterations + state copy to slot 0] for the
+  // predicted iteration count n (one per n, index n - 1) and [1 iteration +
+  // state copy to slot s] for s = 0, 1
   std::vector<hipExecGraphPair> g_first;
-  hipExecGraphPair g_rest;
+  hipExecGraphPair g_rest[2];
   std::tuple<int, int, const void*> graph_key{-1, -1, nullptr};
-  int predicted_iters = 4;   // iterations of the previous align on this ctx
+  int predicted_iters = kDefaultPredictedIters;   // iterations of the previous align on this ctx
   std::vector<hipEvent_t> chunk_ev;
   hipStream_t copy_stream = nullptr;
   bool profiling = false;
@@ -270,12 +280,24 @@ struct gicp_ctx {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   DevBuf mom;          // [kSlabStride] reduced moments, all-reduced in place
-  DevBuf unres;        // phase-B search state: [defer_key u64 x n][defer_mask u64 x groups]
+  DevBuf search;       // correspondence search: [qstate f4 x n][key u64 x n][counters][tasks]
   bool speculate = true;    // queue a follow-on chunk before the first one's flag is seen
   bool comm_graphs = true;  // RCCL captured into the chunk graphs (else eager chunks)
 };
 
 namespace {
+
+const AlignState& final_state(const gicp_ctx* c) { return c->state_host[c->state_slot]; }
+
+// Wait for the align's trailing no-op chunk (if one is still queued) before
+// a ctx-owned buffer it touches may be released to the device pool.
+gicp_status drain_tail(gicp_ctx* c) {
+  if (c->tail_pending) {
+    HIP_TRY(hipEventSynchronize(c->tail_ev));
+    c->tail_pending = false;
+  }
+  return GICP_OK;
+}
 
 gicp_status set_device(const gicp_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
@@ -325,6 +347,8 @@ gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, 
   HIP_TRY(cd->pts.ensure(sizeof(float4) * npad));
   HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
   launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
+  HIP_TRY(cd->soa.ensure(sizeof(float) * 3 * (size_t)npad));
+  launch_leaf_soa(s, cd->pts.as<float4>(), npad, cd->soa.as<float>());
   HIP_TRY(cd->box_lo.ensure(sizeof(float4) * total_boxes));
   HIP_TRY(cd->box_hi.ensure(sizeof(float4) * total_boxes));
   launch_leaf_boxes(s, cd->pts.as<float4>(), N, cd->lvl_cnt[0], cd->box_lo.as<float4>(), cd->box_hi.as<float4>());
@@ -357,8 +381,7 @@ gicp_status compute_cov(gicp_ctx* c, Side& side) {
 
 void invalidate_align(gicp_ctx* c) { c->have_align = false; }
 
-// Tuning knobs of the tile search (development; defaults are the tuned values)
-constexpr float kTileR0Default = 0.25f;
+// Tuning knob of the search (development; the default is the tuned value)
 constexpr float kSplitExtentDefault = 5.0f;
 float env_float(const char* name, float dflt) {
   const char* v = std::getenv(name);
@@ -367,6 +390,28 @@ float env_float(const char* name, float dflt) {
   const float f = std::strtof(v, &end);
   return (end && end != v && f > 0.f) ? f : dflt;
 }
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// byte layout of ctx->search for ns source points
+struct SearchLayout {
+  size_t qstate, key, ctr, hard_list, hard_flag, tasks, total;
+  int cap_r;
+  explicit SearchLayout(int ns) {
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    cap_r = task_cap_per_region(ns);
+    qstate = 0;
+    key = al(sizeof(float4) * (size_t)ns);
+    ctr = key + al(sizeof(unsigned long long) * (size_t)ns);
+    hard_list = ctr + al(sizeof(unsigned) * kTaskCounters * kCtrStride);
+    hard_flag = hard_list + al(sizeof(int) * kHardMax);
+    tasks = hard_flag + al((size_t)ns / 16 + 16);
+    total = tasks + sizeof(unsigned long long) * (size_t)kTaskRegions * cap_r;
+  }
+};
 
 gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   AlignJob& j = *c->job_host;
@@ -400,18 +445,24 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.own_axis = c->own_axis;
   j.own_lo = c->own_lo;
   j.own_hi = c->own_hi;
-  j.tile_r0 = env_float("DDLO_TILE_R0", kTileR0Default);
   j.split_extent = env_float("DDLO_SPLIT_EXTENT", kSplitExtentDefault);
   j.premom = c->comm ? 1 : 0;
   j.mom = c->mom.as<double>();
   {
-    const size_t ns = (size_t)c->src.cloud->n;
-    char* u = c->unres.as<char>();
-    j.defer_key = reinterpret_cast<unsigned long long*>(u);
-    j.defer_mask = reinterpret_cast<unsigned long long*>(u + sizeof(unsigned long long) * ns);
+    const SearchLayout sl(c->src.cloud->n);
+    char* u = c->search.as<char>();
+    j.qstate = reinterpret_cast<float4*>(u + sl.qstate);
+    j.key = reinterpret_cast<unsigned long long*>(u + sl.key);
+    j.task_ctr = reinterpret_cast<unsigned*>(u + sl.ctr);
+    j.tasks = reinterpret_cast<unsigned long long*>(u + sl.tasks);
+    j.task_cap_r = sl.cap_r;
+    j.hard_list = reinterpret_cast<int*>(u + sl.hard_list);
+    j.hard_flag = reinterpret_cast<unsigned char*>(u + sl.hard_flag);
   }
-  j.xcd_remap = (int)env_float("DDLO_XCD_REMAP", 0.f);
   j.list_flush = (int)env_float("DDLO_LIST_FLUSH", 16.f);
+  j.xcd_scan = env_int("DDLO_XCD_SCAN", 1);
+  j.hard_extent = env_float("DDLO_HARD_EXTENT", 4.0f);
+  j.prev_window = env_int("DDLO_PREV_WINDOW", 1);
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   return GICP_OK;
 }
@@ -431,11 +482,21 @@ gicp_status prepare_align(gicp_ctx* c) {
     if (s) return s;
   }
   const int ns = c->src.cloud->n;
+  // a growing buffer goes back to the pool: the queued no-op chunk of the
+  // previous align must not still reference it
+  const size_t need_corr = sizeof(int) * ns, need_sqd = sizeof(float) * ns,
+               need_slab = sizeof(double) * kSlabStride * linearize_blocks(ns),
+               need_search = SearchLayout(ns).total;
+  if (need_corr > c->corr.bytes || need_sqd > c->sqd.bytes || need_slab > c->slab.bytes ||
+      need_search > c->search.bytes || (c->stats_on && sizeof(unsigned int) * kStatFields * (ns + 15) > c->stats.bytes)) {
+    gicp_status s = drain_tail(c);
+    if (s) return s;
+  }
   HIP_TRY(c->corr.ensure(sizeof(int) * ns));
   HIP_TRY(c->sqd.ensure(sizeof(float) * ns));
   HIP_TRY(c->slab.ensure(sizeof(double) * kSlabStride * linearize_blocks(ns)));
   HIP_TRY(c->mom.ensure(sizeof(double) * kSlabStride));
-  HIP_TRY(c->unres.ensure(sizeof(unsigned long long) * ((size_t)ns + (size_t)ns / 64 + 2)));
+  HIP_TRY(c->search.ensure(need_search));
   if (c->stats_on) {
     HIP_TRY(c->stats.ensure(sizeof(unsigned int) * kStatFields * (ns + 15)));
     HIP_TRY(hipMemsetAsync(c->stats.p, 0, c->stats.bytes, c->stream));
@@ -459,7 +520,7 @@ gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks) {
   return GICP_OK;
 }
 
-gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks) {
+gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks, int slot) {
   const AlignJob* jd = c->job_dev.as<AlignJob>();
   if (with_init) launch_align_init(c->stream, jd);
   for (int i = 0; i < iters; ++i) {
@@ -470,13 +531,13 @@ gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks) {
   // the host polls {iter, done} from it, and once done it already holds the
   // final pose, so no separate read-back round trip follows convergence (a
   // speculative no-op chunk behind it rewrites the same bytes)
-  HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->state_host + slot, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
   return GICP_OK;
 }
 
-gicp_status capture_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks, hipExecGraphPair* out) {
+gicp_status capture_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks, int slot, hipExecGraphPair* out) {
   HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-  const gicp_status s = enqueue_chunk(c, with_init, iters, nblocks);
+  const gicp_status s = enqueue_chunk(c, with_init, iters, nblocks, slot);
   const hipError_t e = hipStreamEndCapture(c->stream, &out->g);  // always leave capture mode
   if (s) return s;
   HIP_TRY(e);
@@ -494,7 +555,8 @@ void drop_pair(hipExecGraphPair& p) {
 void drop_graphs(gicp_ctx* c) {
   for (auto& p : c->g_first) drop_pair(p);
   c->g_first.clear();
-  drop_pair(c->g_rest);
+  drop_pair(c->g_rest[0]);
+  drop_pair(c->g_rest[1]);
   c->graph_key = std::make_tuple(-1, -1, nullptr);
 }
 
@@ -515,7 +577,8 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   if (use_graph && c->graph_key != key) {
     drop_graphs(c);
     c->g_first.resize(kMaxFirstChunk);
-    gicp_status s = capture_chunk(c, false, 1, nblocks, &c->g_rest);
+    gicp_status s = capture_chunk(c, false, 1, nblocks, 0, &c->g_rest[0]);
+    if (!s) s = capture_chunk(c, false, 1, nblocks, 1, &c->g_rest[1]);
     if (s) {
       drop_graphs(c);
       (void)hipGetLastError();
@@ -526,18 +589,20 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     c->graph_key = key;
   }
   if (use_graph && !c->g_first[first - 1].ge) {
-    gicp_status s = capture_chunk(c, true, first, nblocks, &c->g_first[first - 1]);
+    gicp_status s = capture_chunk(c, true, first, nblocks, 0, &c->g_first[first - 1]);
     if (s) {
       drop_graphs(c);
       return s;
     }
   }
-  auto launch_chunk = [&](bool is_first) -> gicp_status {
+  // chunk k publishes to slot k % 2 (chunk 0: the first-chunk graph, slot 0)
+  auto launch_chunk = [&](int k) -> gicp_status {
+    const bool is_first = k == 0;
     if (use_graph) {
-      HIP_TRY(hipGraphLaunch(is_first ? c->g_first[first - 1].ge : c->g_rest.ge, c->stream));
+      HIP_TRY(hipGraphLaunch(is_first ? c->g_first[first - 1].ge : c->g_rest[k & 1].ge, c->stream));
       return GICP_OK;
     }
-    return enqueue_chunk(c, is_first, is_first ? first : 1, nblocks);
+    return enqueue_chunk(c, is_first, is_first ? first : 1, nblocks, k & 1);
   };
   const int nchunks = 1 + (max_it - first);
   while ((int)c->chunk_ev.size() < nchunks) {
@@ -545,26 +610,28 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     HIP_TRY(hipEventCreate(&e));  // timed: the last one ends the align's device time
     c->chunk_ev.push_back(e);
   }
-  gicp_status s = launch_chunk(true);
+  gicp_status s = launch_chunk(0);
   if (s) return s;
   HIP_TRY(hipEventRecord(c->chunk_ev[0], c->stream));
   int launched = 1;
   if (nchunks > 1 && c->speculate) {
-    s = launch_chunk(false);
+    s = launch_chunk(1);
     if (s) return s;
     HIP_TRY(hipEventRecord(c->chunk_ev[1], c->stream));
     launched = 2;
   }
   // The number of chunks launched depends only on the done flags, which the
   // replicated LM step makes identical on every rank of a sharded align, so
-  // every rank issues the same sequence of collectives.
+  // every rank issues the same sequence of collectives.  When chunk k is
+  // read, at most chunk k + 1 (the other slot) is queued behind it; chunk
+  // k + 2 (same slot as k) is launched only after the read.
   int k = 0;
   for (;;) {
     HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
-    const volatile AlignState* st = c->state_host;
+    const volatile AlignState* st = c->state_host + (k & 1);
     if (st->done || k == nchunks - 1) break;
     while (launched < nchunks && launched <= k + 2) {  // keep one chunk queued ahead of k+1
-      s = launch_chunk(false);
+      s = launch_chunk(launched);
       if (s) return s;
       HIP_TRY(hipEventRecord(c->chunk_ev[launched], c->stream));
       ++launched;
@@ -572,11 +639,14 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     ++k;
   }
   *final_chunk = k;
+  c->state_slot = k & 1;
+  c->tail_ev = c->chunk_ev[launched - 1];
+  c->tail_pending = launched - 1 > k;
   // Speculate next time only if this align outran its predicted first chunk:
   // when the prediction held, the queued no-op chunk only delays the next
   // align (A/B at cfg 3: 0.466 -> 0.459 ms/scan without it).
   c->speculate = k > 0;
-  c->predicted_iters = std::max(1, (int)((const volatile AlignState*)c->state_host)->iter);
+  c->predicted_iters = std::max(1, (int)((const volatile AlignState*)(c->state_host + (k & 1)))->iter);
   return GICP_OK;
 }
 
@@ -638,11 +708,11 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
   HIP_TRY(hipHostMalloc((void**)&c->job_host, sizeof(AlignJob), hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&c->state_host, sizeof(AlignState), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&c->state_host, 2 * sizeof(AlignState), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&c->flag_host, sizeof(int) * 4, hipHostMallocDefault));
   HIP_TRY(c->job_dev.ensure(sizeof(AlignJob)));
   HIP_TRY(c->state_dev.ensure(sizeof(AlignState)));
-  std::memset(c->state_host, 0, sizeof(AlignState));
+  std::memset(c->state_host, 0, 2 * sizeof(AlignState));
   for (int i = 0; i < 6; ++i) c->state_host->final_hessian[7 * i] = 1.0;  // final_hessian_.setIdentity()
   // stream-ordered (never the legacy stream: another ctx's thread may be
   // capturing its align graph at this moment)
@@ -685,6 +755,10 @@ gicp_status gicp_set_params(gicp_ctx* c, const gicp_params* p) {
   if (!(p->max_correspondence_distance > 0) || !(p->transformation_epsilon > 0) || !(p->rotation_epsilon > 0))
     return fail(GICP_EINVAL, "distances/epsilons must be positive");
   c->params = *p;
+  // per-ctx launch history restarts with the parameters: every rank of a
+  // sharded align then derives the same chunk sequence (same collectives)
+  c->speculate = true;
+  c->predicted_iters = kDefaultPredictedIters;
   return GICP_OK;
 }
 
@@ -829,16 +903,18 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->state_slot = 0;
+    c->tail_pending = false;
   } else {
     int fc = 0;
     s = run_align_graph(c, max_it, nblocks, &fc);
     if (s) return s;
-    // chunk fc's end-of-chunk copy already put the final state in
-    // state_host; the (at most one) speculative no-op chunk still queued
-    // does not delay the return
+    // chunk fc's end-of-chunk copy already put the final state in its
+    // slot; the (at most one) speculative no-op chunk still queued writes
+    // the other slot and does not delay the return
     end_ev = c->chunk_ev[fc];
   }
-  const AlignState& st = *c->state_host;
+  const AlignState& st = final_state(c);
   c->have_align = st.iter > 0;
   c->last_nsrc = ns;
   if (out16) {
@@ -956,7 +1032,7 @@ gicp_status gicp_transform_source(gicp_ctx* c, float* out_xyz, size_t n, size_t 
   if (s) return s;
   // final_transformation_ = x0.cast<float>() of the last align
   float T[16];
-  const AlignState& st = *c->state_host;
+  const AlignState& st = final_state(c);
   for (int r = 0; r < 3; ++r) {
     for (int cc = 0; cc < 3; ++cc) T[4 * r + cc] = (float)st.R[3 * r + cc];
     T[4 * r + 3] = (float)st.t[r];
@@ -1005,7 +1081,9 @@ gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, doubl
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  const AlignState& st = *c->state_host;
+  c->state_slot = 0;
+  c->tail_pending = false;
+  const AlignState& st = final_state(c);
   if (H36) std::memcpy(H36, st.final_hessian, sizeof(double) * 36);
   if (cost) *cost = st.final_cost;
   if (ncorr) *ncorr = st.num_corr;
@@ -1045,7 +1123,7 @@ gicp_status gicp_knn_target(gicp_ctx* c, const float* q, size_t nq, size_t strid
 
 gicp_status gicp_get_moments(const gicp_ctx* c, double* out80) {
   if (!c || !out80) return fail(GICP_EINVAL, "null argument");
-  std::memcpy(out80, c->state_host->last_mom, sizeof(double) * kSlabStride);
+  std::memcpy(out80, final_state(c).last_mom, sizeof(double) * kSlabStride);
   return GICP_OK;
 }
 
@@ -1113,6 +1191,9 @@ gicp_status gicp_set_comm(gicp_ctx* c, const uint8_t* id, size_t nbytes, int nra
   c->nranks = 1;
   c->rank = 0;
   c->comm_graphs = true;
+  c->tail_pending = false;  // the stream was synchronized above
+  c->speculate = true;      // identical launch history on every rank
+  c->predicted_iters = kDefaultPredictedIters;
   if (nranks == 0) return GICP_OK;  // detach
   if (!id || nbytes < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks)
     return fail(GICP_EINVAL, "invalid communicator arguments");

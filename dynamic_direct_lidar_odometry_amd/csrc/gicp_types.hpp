@@ -23,6 +23,15 @@ constexpr int kMomentSlots = 96;
 constexpr int kSlabStride = 80;   // doubles per block partial in the slab
 constexpr int kStatFields = 8;    // per-wave diagnostic counters (DDLO_STATS)
 
+// Task list of the correspondence search (nn_tasks.hpp): kTaskRegions
+// append counters, kCtrStride words apart (one 128-B line each), and
+// kTasksPerGroup task slots per 16-query sub-group on average.
+constexpr int kTaskRegions = 64;
+constexpr int kTaskCounters = kTaskRegions + 1;   // + the hard sub-group list's length
+constexpr int kCtrStride = 32;
+constexpr int kHardMax = 1024;    // hard sub-groups walked first (longest walks first)
+constexpr int kTasksPerGroup = 48;
+
 struct CloudDev {
   const float4* pts;              // n sorted points; w = original index (int bits)
   const unsigned long long* keys; // n sorted Morton keys
@@ -31,6 +40,7 @@ struct CloudDev {
   const float4* box_lo;           // all levels, level 0 = leaves
   const float4* box_hi;
   const float* quant;             // device [lo.x, lo.y, lo.z, scale]
+  const float* soa;               // per leaf: x[32], y[32], z[32] (sorted, sentinel-padded)
   int n;
   int nlevels;
   // per-level node offset/count, kept as scalars (no array => no scratch
@@ -101,14 +111,19 @@ struct AlignJob {
   // mom instead of reducing the slab itself.
   int premom;
   double* mom;             // [kSlabStride]
-  // phase B of the correspondence search: per 64-query group, the mask of
-  // lanes phase A could not resolve; per source point, their (best, bestj)
-  float tile_r0;           // phase-A radius of the tile search (m)
   float split_extent;      // sub-range split threshold of a wave's union box (m)
-  unsigned long long* defer_mask;  // [ceil(n_src / 64)]
-  unsigned long long* defer_key;   // [n_src]
-  int xcd_remap;           // search: contiguous group range per XCD block label
-  int list_flush;          // search: leaf-list length that triggers an early scan
+  int list_flush;          // search (collect-scan variant): leaf-list length that triggers an early scan
+  // task-based correspondence search (nn_tasks.hpp)
+  float4* qstate;                // [n_src] transformed query (x, y, z) + seed bound (< 0: inactive)
+  unsigned long long* key;       // [n_src] (squared distance, sorted target position) of the best match
+  unsigned long long* tasks;     // [kTaskRegions][task_cap_r]
+  unsigned* task_ctr;            // [kTaskRegions * kCtrStride]
+  int task_cap_r;
+  int* hard_list;                // [kHardMax] sub-groups with a wide union box
+  unsigned char* hard_flag;      // [n_src / 16] 1 = listed (walked by the first waves)
+  float hard_extent;             // union-box extent (m) above which a sub-group is hard
+  int xcd_scan;                  // scan: one spatial eighth of the tasks per XCD (speed only)
+  int prev_window;         // search: seed a large pose step from the window around the previous match
 };
 
 }  // namespace ddlo

@@ -22,7 +22,7 @@
 
 #include "gicp_types.hpp"
 #include "search.hpp"
-#include "tile_search.hpp"
+#include "nn_tasks.hpp"
 #include "launch.hpp"
 
 #include <algorithm>
@@ -136,6 +136,20 @@ __global__ __launch_bounds__(256) void k_gather(const float4* __restrict__ raw, 
 }
 
 // one 32-lane half-wave per leaf
+// Per-leaf SoA copy of the sorted points: leaf l = x[32], y[32], z[32], so
+// that a lane's 8 consecutive coordinates are two 16-B loads per axis and
+// pairs of them feed the packed-math distance directly (k_nn_scan).
+__global__ __launch_bounds__(256) void k_leaf_soa(const float4* __restrict__ pts, int npad, float* __restrict__ soa) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npad) return;
+  const float4 p = pts[i];
+  const int l = i / kLeafSize, t = i % kLeafSize;
+  float* o = soa + (size_t)l * 3 * kLeafSize;
+  o[t] = p.x;
+  o[kLeafSize + t] = p.y;
+  o[2 * kLeafSize + t] = p.z;
+}
+
 __global__ __launch_bounds__(256) void k_leaf_boxes(const float4* __restrict__ pts, int n, int nleaves,
                                                     float4* __restrict__ lo, float4* __restrict__ hi) {
   const int leaf = blockIdx.x * 8 + (threadIdx.x >> 5);
@@ -656,12 +670,12 @@ __device__ __forceinline__ void load_sym6(const __attribute__((address_space(1))
 }
 
 constexpr int kLinWaves = 4;      // waves per block (search and moment kernels)
-constexpr float kOptR2 = 0.25f;     // optimistic first-pass radius^2 (0.5 m)
 constexpr int kSearchQ = 16;        // queries per wavefront in the correspondence search
 constexpr int kSeedW = 8;           // Morton-window seed points per slice lane
 
 __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
+  if (threadIdx.x < kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;
   if (threadIdx.x == 0) {
     for (int i = 0; i < 9; ++i) st->R[i] = job->guess_R[i];
     for (int i = 0; i < 3; ++i) st->t[i] = job->guess_t[i];
@@ -685,6 +699,405 @@ __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__
 // (exact completion): queries whose pass-1 radius was clipped to kOptR and
 // found nothing search again with the full max_corr bound.  Writes corr/sqd
 // (update_correspondences, nano_gicp_impl.hpp:249-258).
+// K3a: seeds of the exact bounded 1-NN correspondence search (nn_tasks.hpp),
+// Q = 16 queries (a sub-group) per wavefront: the fp32 query transform,
+// then an exact upper bound — the triangle bound from the previous
+// correspondence for a small pose step (no load), the Morton window around
+// the previous match after a large step, else the Morton window around the
+// query's own key — then group sharing.  Writes the per-query search state
+// (qstate) and the seed key, and lists the sub-groups whose union box is
+// wider than hard_extent, so that k_nn_collect starts them first.
+template <int MINW>
+__global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restrict__ job) {
+  constexpr int Q = kTaskQ;
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  const CloudDev src = job->src;
+  const CloudDev tgt = job->tgt;
+  const auto corr = gpw(job->corr);
+  const auto sqd = gpw(job->sqd);
+  unsigned int* const stats = job->stats;
+  const float cap2 = job->cap2;
+  const int have_prev = st->have_prev;
+  const int prev_window = job->prev_window;
+  const int own_axis = job->own_axis;
+  const float own_lo = job->own_lo, own_hi = job->own_hi;
+  float Rf[9], tf[3];
+  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
+  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
+
+  const int lane = lane_id();
+  const int qi = lane % Q;
+  const int wib = threadIdx.x >> 6;
+  float4* const qstate = job->qstate;
+  unsigned long long* const keyout = job->key;
+  const int wave = (int)blockIdx.x * kLinWaves + wib;
+  const int nwaves_total = gridDim.x * kLinWaves;
+  const int ngroups = (src.n + Q - 1) / Q;
+  // previous linearization pose (for the triangle-inequality bound)
+  float Rp[9], tp[3];
+  for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
+  for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
+  for (int g = wave; g < ngroups; g += nwaves_total) {
+    const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    const int i = g * Q + qi;
+    const bool inrange = i < src.n;
+    const int ic = inrange ? i : src.n - 1;
+    // every independent per-query load of the prologue in one round trip
+    const float4 a = ldg4(src.pts, ic);
+    const int jprev = have_prev ? corr[ic] : -1;
+    const float sqprev = have_prev ? sqd[ic] : 0.f;
+    const unsigned long long skey = gp(src.keys)[ic];
+    // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
+    const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
+    const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
+    const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
+    // spatial sharding: search only the queries this rank owns
+    const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
+    const bool active = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi));
+    if (!__any(active)) {
+      if (inrange && lane < Q) {
+        keyout[i] = dkey(INFINITY, -1);
+        qstate[i] = make_float4(qx, qy, qz, -1.f);
+      }
+      if (lane == 0) job->hard_flag[g] = 0;
+      if (stats && lane == 0) {
+        unsigned int* o = stats + (size_t)g * kStatFields;
+        for (int f = 0; f < kStatFields; ++f) o[f] = 0;
+      }
+      continue;
+    }
+    NNVisitor<Q> vis;
+    vis.qx = qx;
+    vis.qy = qy;
+    vis.qz = qz;
+    vis.active = active;
+    vis.best = active ? cap2 : -1.f;
+    vis.bestj = -1;
+    vis.skip_lo = 1;
+    vis.skip_hi = 0;
+    bool seeded = false;
+    bool large_step = false;   // previous match exists but the pose moved >= 2 cm since
+    // coordinates of the point behind vis.bestj when it is already in registers
+    float bpx = 0.f, bpy = 0.f, bpz = 0.f;
+    bool have_bp = true;
+    if (have_prev && active) {
+      const int j = jprev;
+      if (j >= 0) {
+        // NN(q) <= |q - p_prev| <= sqrt(sqd_prev) + |q - q_prev| (triangle
+        // inequality; fp64 with an upward margin covers fp32 rounding), so
+        // the bound needs no load of the previous match.
+        const float qpx = (Rp[0] * a.x + Rp[1] * a.y) + (Rp[2] * a.z + tp[0]);
+        const float qpy = (Rp[3] * a.x + Rp[4] * a.y) + (Rp[5] * a.z + tp[1]);
+        const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
+        const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
+        const double mv = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
+        if (mv < 0.02) {
+          const double r = sqrt((double)sqprev) + mv;
+          const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
+          if (b2 < (double)cap2) {
+            vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
+            seeded = true;
+          }
+        } else if (prev_window) {
+          large_step = true;   // exact distances to the Morton window around p_prev (below)
+        } else {  // large pose step: the exact distance to the previous match
+          const float4 p = ldg4(tgt.pts, j);
+          const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
+          if (d < cap2) {
+            vis.best = d;
+            vis.bestj = j;
+            bpx = p.x;
+            bpy = p.y;
+            bpz = p.z;
+            seeded = true;
+          }
+        }
+      }
+    }
+    // Exact seeding for queries without a usable previous correspondence:
+    // the real target points around the query's Morton position give an
+    // upper bound, so the single search below stays exact.  After a large
+    // pose step the window is centred on the previous match instead (its
+    // sorted position IS a Morton position next to the new nearest point,
+    // and no key search is needed); the window contains the previous match.
+    const bool need_seed = active && !seeded && !large_step;
+    const bool use_window = need_seed || large_step;
+    bool again = false;
+    if (__any(use_window)) {
+      // Morton window of kSeedW points per slice lane (64/Q * kSeedW per query)
+      int pos = large_step ? jprev : 0;
+      if (__any(need_seed)) {
+        const int lb = group_lower_bound<Q>(tgt.keys, tgt.n, morton_key(qx, qy, qz, tgt.quant));
+        if (need_seed) pos = lb;
+      }
+      const int s = lane / Q;
+      const int w0 = pos - (64 / Q) * kSeedW / 2 + s * kSeedW;
+      unsigned long long bk = dkey(vis.best, vis.bestj);
+      float4 p[kSeedW];
+#pragma unroll
+      for (int k = 0; k < kSeedW; ++k) p[k] = ldg4(tgt.pts, min(max(w0 + k, 0), tgt.n - 1));
+      if (use_window) {
+#pragma unroll
+        for (int k = 0; k < kSeedW; ++k) {
+          const int cand = min(max(w0 + k, 0), tgt.n - 1);
+          bk = umin64(bk, dkey(dist2(qx, qy, qz, p[k].x, p[k].y, p[k].z), cand));
+        }
+      }
+      vis.merge_slices(bk);
+      if (use_window) {
+        const float bd = __uint_as_float((unsigned)(bk >> 32));
+        if (bd < cap2) {
+          vis.best = bd;
+          vis.bestj = (int)(unsigned)bk;
+          have_bp = false;   // the winning window point may sit in another slice lane
+        }
+      }
+      again = need_seed;
+    }
+    // Group sharing: every query also takes the exact distance to the other
+    // queries' candidate points (Morton-adjacent queries are spatially
+    // adjacent, so a neighbour's candidate is often far closer than the
+    // query's own).  Valid (distance, position) pairs only: exactness kept.
+    {
+      const unsigned long long donors = __ballot(lane < Q && active && vis.bestj >= 0);
+      if (donors && __any(active)) {
+        float4 bp = make_float4(bpx, bpy, bpz, 0.f);
+        if (__any(!have_bp && vis.bestj >= 0)) {
+          if (!have_bp) bp = ldg4(tgt.pts, max(vis.bestj, 0));
+        }
+        unsigned long long bk = dkey(vis.best, vis.bestj);
+        unsigned long long m = donors;
+        while (m) {
+          const int k = __builtin_ctzll(m);
+          m &= m - 1;
+          const float sx = readlane_f(bp.x, k), sy = readlane_f(bp.y, k), sz = readlane_f(bp.z, k);
+          const int sj = readlane_i(vis.bestj, k);
+          bk = umin64(bk, dkey(dist2(qx, qy, qz, sx, sy, sz), sj));
+        }
+        if (active) {
+          vis.best = __uint_as_float((unsigned)(bk >> 32));
+          vis.bestj = (int)(unsigned)bk;
+        }
+      }
+    }
+    if (inrange && lane < Q) {
+      qstate[i] = make_float4(qx, qy, qz, active ? vis.best : -1.f);
+      keyout[i] = active ? dkey(vis.best, vis.bestj) : dkey(INFINITY, -1);
+    }
+    // hard sub-group: a wide union box (a query far from every target point
+    // drags many blocks into the walk) -> listed, walked first
+    const WaveBox whole = make_wave_box(active, qx, qy, qz, active ? vis.best : -1.f);
+    const bool hard = box_extent(whole) > job->hard_extent;
+    if (lane == 0) {
+      int slot = -1;
+      if (hard) {
+        slot = (int)atomicAdd(job->task_ctr + kTaskRegions * kCtrStride, 1u);
+        if (slot < kHardMax) job->hard_list[slot] = g;
+      }
+      job->hard_flag[g] = (unsigned char)(hard && slot < kHardMax);
+    }
+    if (stats && lane == 0) {
+      unsigned int* o = stats + (size_t)g * kStatFields;
+      o[1] = min(((unsigned)__builtin_amdgcn_s_memtime() - (unsigned)tm0) >> 4, 65535u);
+      o[6] = (unsigned)hard;
+    }
+  }
+}
+
+// K3b: task collect, one wavefront per sub-group (nn_tasks.hpp): the
+// query states and seed keys of k_nn_seed, the LDS-cached walk of the upper
+// levels with the union box of the 16 balls, the exact (leaf, query) box
+// tests, tasks appended to the list.  Waves 0 .. kHardMax-1 take the hard
+// sub-groups listed by the seed kernel (dispatched first, so the longest
+// walks start first); the other waves take the remaining sub-groups in
+// order.
+template <int MINW>
+__global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __restrict__ job) {
+  constexpr int Q = kTaskQ;
+  const AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  const CloudDev src = job->src;
+  const CloudDev tgt = job->tgt;
+  unsigned int* const stats = job->stats;
+  const int lane = lane_id();
+  const int qi = lane % Q;
+  const int wib = threadIdx.x >> 6;
+  // dynamic LDS: [kLinWaves x TaskLds][upper-level box cache]
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  TaskLds* TL = reinterpret_cast<TaskLds*>(dsm) + wib;
+  f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kTaskLdsBytes);
+  TaskList tl;
+  tl.tasks = job->tasks;
+  tl.ctr = job->task_ctr;
+  tl.cap_r = job->task_cap_r;
+  unsigned long long* const keyout = job->key;
+  const int ngroups = (src.n + Q - 1) / Q;
+  const int wave = (int)blockIdx.x * kLinWaves + wib;
+  int g;
+  if (wave < kHardMax) {
+    const int nhard = min((int)__builtin_amdgcn_readfirstlane(job->task_ctr[kTaskRegions * kCtrStride]), kHardMax);
+    if (__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kLinWaves)) >= nhard) return;   // whole block idle
+    g = wave < nhard ? job->hard_list[wave] : -1;
+  } else {
+    g = wave - kHardMax;
+    if (g >= ngroups || job->hard_flag[g]) g = -1;
+  }
+  g = __builtin_amdgcn_readfirstlane(g);
+  fill_upper(tgt, upper);
+  __syncthreads();
+  if (g < 0) return;
+  const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+  const int i = g * Q + qi;
+  const bool inrange = i < src.n;
+  const int ic = inrange ? i : src.n - 1;
+  const float4 q = ldg4(job->qstate, ic);
+  const unsigned long long k0 = gp(keyout)[ic];
+  const unsigned long long skey = gp(src.keys)[ic];
+  TaskCollector col;
+  col.L = TL;
+  col.U = upper;
+  col.nup = upper_count(tgt);
+  col.qx = q.x;
+  col.qy = q.y;
+  col.qz = q.z;
+  col.active = inrange && q.w >= 0.f;
+  col.bk = k0;
+  col.sg = g;
+  col.run(tgt, tl, skey, job->split_extent);
+  if (inrange && lane < Q && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
+  if (stats && lane == 0) {
+    const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
+    unsigned int* o = stats + (size_t)g * kStatFields;
+    o[0] = col.st_blocks;
+    o[2] = col.st_tasks | (min(col.st_iters, 65535u) << 16);
+    o[3] = col.st_inline;
+    o[4] = (unsigned)(tm1 - tm0);
+    o[5] = min((col.tm_walk - (unsigned)tm0) >> 4, 65535u);
+    o[7] = 1;
+  }
+}
+
+// K3b: leaf scans of the task list.  The waves of region r split its tasks
+// into contiguous chunks (XCD-aware, see below).  A wave stages a batch of
+// kScanBatch tasks in LDS with LDS-DMA — per task the leaf's 32 SoA points
+// (384 B) and the sub-group's 16 query states (256 B) — waits once, and
+// scans them from LDS (lane = query qi x quarter s of the leaf).  A
+// sub-group's tasks sit next to each other in the list (one collect flush),
+// so the per-query minimum is kept in registers across a run of the same
+// sub-group and merged into the result with one 64-bit atomicMin per query.
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+constexpr int kScanBatch = 16;                        // tasks per LDS batch
+constexpr int kScanTaskBytes = 3 * kLeafSize * 4 + kTaskQ * 16;   // 384 B points + 256 B queries
+constexpr int kScanWaves = 4;                         // waves per block
+
+template <int MINW>
+__global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJob* __restrict__ job) {
+  const AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  const CloudDev tgt = job->tgt;
+  const float4* const qstate = job->qstate;
+  unsigned long long* const key = job->key;
+  const int cap_r = job->task_cap_r;
+  const int lane = lane_id();
+  const int qi = lane & 15, s = lane >> 4;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_all[kScanWaves][kScanBatch * kScanTaskBytes];
+  unsigned char* const L = lds_all[threadIdx.x >> 6];
+  const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
+  const int wpr = nwaves / kTaskRegions;   // the grid is a multiple of 8 * kTaskRegions waves
+  // (region, chunk) of this wave.  A region's tasks were appended roughly in
+  // sub-group (= Morton) order, so chunk c of every region covers about the
+  // same c-th slice of the scene; blocks b and b + 8 share an XCD and its
+  // L2, so XCD x = b % 8 gets chunks [x wpr / 8, (x + 1) wpr / 8) of all
+  // regions: one spatial eighth of the target per L2.  Speed only: any
+  // bijection of waves onto (region, chunk) is exact.
+  int r, c;
+  if (job->xcd_scan && wpr % 8 == 0) {
+    const int x = blockIdx.x % 8, u = (int)(blockIdx.x / 8) * kScanWaves + (int)(threadIdx.x >> 6);
+    r = u % kTaskRegions;
+    c = x * (wpr / 8) + u / kTaskRegions;
+  } else {
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    r = wave % kTaskRegions;
+    c = wave / kTaskRegions;
+  }
+  const int n = min((int)__builtin_amdgcn_readfirstlane(job->task_ctr[r * kCtrStride]), cap_r);
+  const int chunk = (n + wpr - 1) / wpr;
+  const int lo = c * chunk, hi = min(n, lo + chunk);
+  const unsigned long long* rt = job->tasks + (size_t)r * cap_r;
+  int run_sg = -1;
+  unsigned long long acc = ~0ull;   // lane's query minimum over the current run
+  float run_bound = -1.f;
+  for (int base = lo; base < hi; base += kScanBatch) {
+    const int cnt = min(kScanBatch, hi - base);
+    const unsigned long long tl = lane < cnt ? rt[base + lane] : 0ull;
+    // LDS-DMA the batch: 16 B per lane per instruction, 1 KB per wave-instruction
+#pragma unroll
+    for (int i = 0; i < kScanBatch * kScanTaskBytes / 1024; ++i) {
+      const int o = i * 1024 + lane * 16;
+      const int k = o / kScanTaskBytes, w = o % kScanTaskBytes;
+      const int kk = min(k, cnt - 1);   // past the batch: reload the last task (never read)
+      const unsigned long long tk = __shfl(tl, kk);
+      const char* src = w < 3 * kLeafSize * 4
+                            ? (const char*)(tgt.soa + (size_t)(tk >> 40) * (3 * kLeafSize)) + w
+                            : (const char*)(qstate + (size_t)((tk >> 16) & 0xffffffull) * kTaskQ) + (w - 3 * kLeafSize * 4);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(L + i * 1024), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the batch has landed in LDS
+    __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < cnt; ++k) {
+      const unsigned long long t = readlane_u64(tl, k);
+      const int sg = (int)((t >> 16) & 0xffffffull);
+      if (sg != run_sg) {   // uniform: a new sub-group's run starts
+        if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound))
+          atomicMin(key + (size_t)run_sg * kTaskQ + qi, acc);
+        run_sg = sg;
+        acc = ~0ull;
+        run_bound = -1.f;
+      }
+      const unsigned char* T = L + k * kScanTaskBytes;
+      const f4v x0 = *(const f4v*)(T + s * 32), x1 = *(const f4v*)(T + s * 32 + 16);
+      const f4v y0 = *(const f4v*)(T + 128 + s * 32), y1 = *(const f4v*)(T + 128 + s * 32 + 16);
+      const f4v z0 = *(const f4v*)(T + 256 + s * 32), z1 = *(const f4v*)(T + 256 + s * 32 + 16);
+      const f4v q = *(const f4v*)(T + 384 + qi * 16);
+      const float X[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      const float Y[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+      const float Z[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+      // same IEEE ops as dist2(), two points per packed instruction; the
+      // lane's points come in increasing position, so strict < keeps the
+      // lowest position among equal distances
+      const f2v qx2 = {q.x, q.x}, qy2 = {q.y, q.y}, qz2 = {q.z, q.z};
+      float bd = INFINITY;
+      int bh = 0;
+#pragma unroll
+      for (int h = 0; h < 8; h += 2) {
+        const f2v dx = qx2 - f2v{X[h], X[h + 1]};
+        const f2v dy = qy2 - f2v{Y[h], Y[h + 1]};
+        const f2v dz = qz2 - f2v{Z[h], Z[h + 1]};
+        const f2v d = (dx * dx + dy * dy) + dz * dz;
+        if (d.x < bd) { bd = d.x; bh = h; }
+        if (d.y < bd) { bd = d.y; bh = h + 1; }
+      }
+      unsigned long long bk = dkey(bd, (int)(t >> 40) * kLeafSize + s * 8 + bh);
+      bk = xor_min64<16>(bk);
+      bk = xor_min64<32>(bk);
+      if (((t >> qi) & 1ull) != 0ull) {
+        acc = umin64(acc, bk);
+        run_bound = q.w;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();   // LDS reads done before the next batch overwrites it
+  }
+  if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound))
+    atomicMin(key + (size_t)run_sg * kTaskQ + qi, acc);
+}
+
 template <int Q, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
@@ -697,6 +1110,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
   const float cap2 = job->cap2;
   const double max_corr2 = job->max_corr2;
   const int have_prev = st->have_prev;
+  const int prev_window = job->prev_window;
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
   float Rf[9], tf[3];
@@ -712,13 +1126,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
   f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kCollectLdsBytes);
   fill_upper(tgt, upper);
   __syncthreads();
-  // XCD-aware remap (job->xcd_remap): blocks b and b + 8 share an XCD and its
-  // L2, so give each of the 8 block labels one contiguous (Morton-compact)
-  // eighth of the groups.  Speed only: the mapping stays a bijection.
-  const int nb = gridDim.x;
-  const int bl = (job->xcd_remap && nb % 8 == 0) ? (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8)
-                                                 : (int)blockIdx.x;
-  const int wave = bl * kLinWaves + wib;
+  const int wave = (int)blockIdx.x * kLinWaves + wib;
   const int nwaves_total = gridDim.x * kLinWaves;
   const int ngroups = (src.n + Q - 1) / Q;
   // previous linearization pose (for the triangle-inequality bound)
@@ -746,6 +1154,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
       if (inrange && lane < Q) {
         corr[i] = -1;
         sqd[i] = INFINITY;
+        job->key[i] = dkey(INFINITY, -1);
       }
       if (stats && lane == 0) {
         unsigned int* o = stats + (size_t)g * kStatFields;
@@ -763,6 +1172,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
     vis.skip_lo = 1;
     vis.skip_hi = 0;
     bool seeded = false;
+    bool large_step = false;   // previous match exists but the pose moved >= 2 cm since
     // coordinates of the point behind vis.bestj when it is already in registers
     float bpx = 0.f, bpy = 0.f, bpz = 0.f;
     bool have_bp = true;
@@ -784,6 +1194,8 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
             vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
             seeded = true;
           }
+        } else if (prev_window) {
+          large_step = true;   // exact distances to the Morton window around p_prev (below)
         } else {  // large pose step: the exact distance to the previous match
           const float4 p = ldg4(tgt.pts, j);
           const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
@@ -800,19 +1212,27 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
     }
     // Exact seeding for queries without a usable previous correspondence:
     // the real target points around the query's Morton position give an
-    // upper bound, so the single search below stays exact.
-    const bool need_seed = active && !seeded;
+    // upper bound, so the single search below stays exact.  After a large
+    // pose step the window is centred on the previous match instead (its
+    // sorted position IS a Morton position next to the new nearest point,
+    // and no key search is needed); the window contains the previous match.
+    const bool need_seed = active && !seeded && !large_step;
+    const bool use_window = need_seed || large_step;
     bool again = false;
-    if (__any(need_seed)) {
+    if (__any(use_window)) {
       // Morton window of kSeedW points per slice lane (64/Q * kSeedW per query)
-      const int pos = group_lower_bound<Q>(tgt.keys, tgt.n, morton_key(qx, qy, qz, tgt.quant));
+      int pos = large_step ? jprev : 0;
+      if (__any(need_seed)) {
+        const int lb = group_lower_bound<Q>(tgt.keys, tgt.n, morton_key(qx, qy, qz, tgt.quant));
+        if (need_seed) pos = lb;
+      }
       const int s = lane / Q;
       const int w0 = pos - (64 / Q) * kSeedW / 2 + s * kSeedW;
       unsigned long long bk = dkey(vis.best, vis.bestj);
       float4 p[kSeedW];
 #pragma unroll
       for (int k = 0; k < kSeedW; ++k) p[k] = ldg4(tgt.pts, min(max(w0 + k, 0), tgt.n - 1));
-      if (need_seed) {
+      if (use_window) {
 #pragma unroll
         for (int k = 0; k < kSeedW; ++k) {
           const int cand = min(max(w0 + k, 0), tgt.n - 1);
@@ -820,7 +1240,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
         }
       }
       vis.merge_slices(bk);
-      if (need_seed) {
+      if (use_window) {
         const float bd = __uint_as_float((unsigned)(bk >> 32));
         if (bd < cap2) {
           vis.best = bd;
@@ -869,6 +1289,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
     if (inrange && lane < Q) {
       corr[i] = valid ? vis.bestj : -1;
       sqd[i] = active && vis.bestj >= 0 ? vis.best : INFINITY;
+      job->key[i] = active && vis.bestj >= 0 ? dkey(vis.best, vis.bestj) : dkey(INFINITY, -1);
     }
     if (stats && lane == 0) {
       const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
@@ -885,224 +1306,6 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
   }
 }
 
-// K3 (tile search): phase A.  One wavefront per 64 sorted source points.
-__global__ __launch_bounds__(256) void k_nn_tile_a(const AlignJob* __restrict__ job) {
-  AlignState* st = job->state;
-  if (__builtin_amdgcn_readfirstlane(st->done)) return;
-  const CloudDev src = job->src;
-  const CloudDev tgt = job->tgt;
-  const auto corr = gpw(job->corr);
-  const auto sqd = gpw(job->sqd);
-  unsigned int* const stats = job->stats;
-  const float cap2 = job->cap2;
-  const double max_corr2 = job->max_corr2;
-  const int have_prev = st->have_prev;
-  const int own_axis = job->own_axis;
-  const float own_lo = job->own_lo, own_hi = job->own_hi;
-  float Rf[9], tf[3], Rp[9], tp[3];
-  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
-  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
-  for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
-  for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
-
-  const int lane = lane_id();
-  const int wib = threadIdx.x >> 6;
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  TileLds* L = reinterpret_cast<TileLds*>(dsm) + wib;
-  f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kTileLdsBytes);
-  fill_upper(tgt, upper);
-  __syncthreads();
-  const int ngroups = (src.n + 63) >> 6;
-  for (int g = blockIdx.x * kLinWaves + wib; g < ngroups; g += gridDim.x * kLinWaves) {
-    const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
-    const int i = g * 64 + lane;
-    const bool inrange = i < src.n;
-    const int ic = inrange ? i : src.n - 1;
-    // independent loads issued together
-    const float4 a = ldg4(src.pts, ic);
-    const int jprev = have_prev ? corr[ic] : -1;
-    const float dprev = have_prev ? sqd[ic] : 0.f;
-    const unsigned long long key = gp(src.keys)[ic];
-    // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
-    const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
-    const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
-    const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
-    const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
-    const bool active = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi));
-    // upper bound of the 1-NN distance: NN(q) <= |q - p_prev| <= sqrt(sqd_prev) + |q - q_prev|
-    float b = cap2;
-    if (active && jprev >= 0) {
-      const float qpx = (Rp[0] * a.x + Rp[1] * a.y) + (Rp[2] * a.z + tp[0]);
-      const float qpy = (Rp[3] * a.x + Rp[4] * a.y) + (Rp[5] * a.z + tp[1]);
-      const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
-      const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
-      const double r = sqrt((double)dprev) + sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
-      const double b2 = r * r * (1.0 + 1e-5) + 1e-12;   // fp64 with an upward margin
-      if (b2 < (double)cap2) b = __uint_as_float(__float_as_uint((float)b2) + 1);
-    }
-    const unsigned long long tm1 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
-    TileSearch ts;
-    ts.c = tgt;
-    ts.L = L;
-    ts.U = upper;
-    ts.nup = upper_count(tgt);
-    ts.qx = qx;
-    ts.qy = qy;
-    ts.qz = qz;
-    ts.active = active;
-    ts.cap = job->tile_r0 * job->tile_r0;
-    ts.split_ext = job->split_extent;
-    ts.best = b;
-    ts.bestj = -1;
-    ts.bx = ts.by = ts.bz = 0.f;
-    if (__any(active)) ts.run(key);
-    const bool resolved = ts.best <= fminf(b, ts.cap);
-    // deferred lanes: tighten their bound with the resolved neighbours' points
-    ts.seed_from_lanes(active && !resolved, __ballot(active && resolved && ts.bestj >= 0));
-    if (inrange) {
-      if (!active) {
-        corr[i] = -1;
-        sqd[i] = INFINITY;
-      } else if (resolved) {
-        corr[i] = (ts.bestj >= 0 && (double)ts.best < max_corr2) ? ts.bestj : -1;
-        sqd[i] = ts.bestj >= 0 ? ts.best : INFINITY;
-      }
-    }
-    // queries not resolved within R0 -> phase B (mask per group, key per point)
-    const bool defer = active && !resolved;
-    const unsigned long long dm = __ballot(defer);
-    if (defer) job->defer_key[i] = dkey(ts.best, ts.bestj);
-    if (lane == 0) job->defer_mask[g] = dm;
-    if (stats && lane == 0) {
-      unsigned int* o = stats + (size_t)g * kStatFields;
-      o[0] = ts.st.blocks;
-      o[1] = ts.st.cand;
-      o[2] = ts.st.listed;
-      o[3] = ts.st.batches;
-      o[4] = (unsigned)(__builtin_amdgcn_s_memtime() - tm0);
-      o[5] = (unsigned)(tm1 - tm0) | ((unsigned)min(ts.st.cyc_scan >> 4, 0xffffull) << 16);  // prologue | scan/16
-      o[6] = (unsigned)__popcll(dm) | (ts.st.splits << 16);
-      o[7] = 1 | ((unsigned)min(ts.st.cyc_blocks >> 4, 0xffffull) << 16);             // blocks/16
-    }
-  }
-}
-
-// K3 (tile search): phase B — the queries phase A could not resolve, in
-// source (Morton) order: one wavefront gathers the deferred lanes of
-// kDeferGroups consecutive phase-A groups and searches them 64 at a time
-// with their full bound (the phase-A best, which is <= the a-priori bound).
-__global__ __launch_bounds__(256) void k_nn_tile_b(const AlignJob* __restrict__ job) {
-  AlignState* st = job->state;
-  if (__builtin_amdgcn_readfirstlane(st->done)) return;
-  const CloudDev src = job->src;
-  const CloudDev tgt = job->tgt;
-  const int ngroups = (src.n + 63) >> 6;
-  // skip the whole workgroup when none of its groups deferred anything
-  const int gb0 = blockIdx.x * kLinWaves * kDeferGroups;
-  {
-    unsigned long long any = 0ull;
-    const int t = threadIdx.x;
-    if (t < kLinWaves * kDeferGroups && gb0 + t < ngroups) any = job->defer_mask[gb0 + t];
-    if (!__syncthreads_or(any != 0ull)) return;
-  }
-  const auto corr = gpw(job->corr);
-  const auto sqd = gpw(job->sqd);
-  const double max_corr2 = job->max_corr2;
-  float Rf[9], tf[3];
-  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
-  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
-  const int lane = lane_id();
-  const int wib = threadIdx.x >> 6;
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  TileLds* L = reinterpret_cast<TileLds*>(dsm) + wib;
-  f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kTileLdsBytes);
-  fill_upper(tgt, upper);
-  __syncthreads();
-  const int g0 = gb0 + wib * kDeferGroups;
-  unsigned int* const stats = job->stats;
-  const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
-  TileStats tst;
-  unsigned rounds = 0;
-  int n = 0;
-#pragma unroll
-  for (int k = 0; k < kDeferGroups; ++k) {
-    const int g = g0 + k;
-    const unsigned long long m = g < ngroups ? job->defer_mask[g] : 0ull;
-    if ((m >> lane) & 1ull)
-      L->defer[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
-          g * 64 + lane;
-    n += __popcll(m);
-  }
-  __builtin_amdgcn_wave_barrier();
-  for (int b0 = 0; b0 < n; b0 += 64) {
-    const int e = b0 + lane;
-    const bool active = e < n;
-    const int i = L->defer[min(e, n - 1)];
-    const unsigned long long bk = job->defer_key[i];
-    const float4 a = ldg4(src.pts, i);
-    const unsigned long long key = gp(src.keys)[i];
-    TileSearch ts;
-    ts.c = tgt;
-    ts.L = L;
-    ts.U = upper;
-    ts.nup = upper_count(tgt);
-    ts.qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
-    ts.qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
-    ts.qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
-    ts.split_ext = job->split_extent;
-    ts.best = __uint_as_float((unsigned)(bk >> 32));
-    ts.bestj = (int)(unsigned)bk;
-    {  // coordinates of the phase-A best (seeding needs them)
-      const float4 p = ldg4(tgt.pts, max(ts.bestj, 0));
-      ts.bx = p.x;
-      ts.by = p.y;
-      ts.bz = p.z;
-    }
-    // radius doubling from 2 R0: scanning leaves within min(best, R^2)
-    // resolves a lane once best <= R^2; the last round is unbounded (the
-    // lane's own bound, <= max_corr^2)
-    // a bound without a point (bestj < 0, below the cap) is phase A's
-    // triangle bound from the previous correspondence: tight, so the lane
-    // searches with it at once; bounds from scanned points may be loose
-    // and go through the doubling rounds
-    const bool tight = ts.bestj < 0 && ts.best < job->cap2;
-    bool pending = active;
-    float R = 2.f * job->tile_r0;
-    for (;;) {
-      const bool last = (double)R * R >= job->max_corr2;
-      ts.cap = (last || tight) ? INFINITY : R * R;
-      ts.active = pending;
-      ts.run(key);
-      rounds += 1;
-      pending = pending && !(ts.best <= ts.cap);
-      if (last || !__any(pending)) break;
-      // lanes resolved this round seed the ones still pending
-      ts.seed_from_lanes(pending, __ballot(active && !pending && ts.bestj >= 0));
-      R *= 2.f;
-    }
-    if (active) {
-      corr[i] = (ts.bestj >= 0 && (double)ts.best < max_corr2) ? ts.bestj : -1;
-      sqd[i] = ts.bestj >= 0 ? ts.best : INFINITY;
-    }
-    tst.blocks += ts.st.blocks;
-    tst.cand += ts.st.cand;
-    tst.listed += ts.st.listed;
-    tst.batches += ts.st.batches;
-    tst.splits += ts.st.splits;
-  }
-  if (stats && lane == 0 && g0 < ngroups) {  // phase-B rows follow the phase-A rows
-    unsigned int* o = stats + (size_t)(ngroups + g0 / kDeferGroups) * kStatFields;
-    o[0] = tst.blocks;
-    o[1] = tst.cand;
-    o[2] = tst.listed;
-    o[3] = tst.batches;
-    o[4] = (unsigned)(__builtin_amdgcn_s_memtime() - tm0);
-    o[5] = rounds;
-    o[6] = (unsigned)n | (tst.splits << 16);
-    o[7] = 2;
-  }
-}
-
 // K3b: Mahalanobis + normal-equation moments of the matched pairs
 // (update_correspondences :265-273 + linearize :292-328), 64 points per
 // wavefront, in-register transpose reduction, one slab row per block.
@@ -1115,8 +1318,11 @@ __global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ j
   const CloudDev tgt = job->tgt;
   const auto src_cov = gp(job->src_cov);
   const auto tgt_cov = gp(job->tgt_cov);
-  const auto corr = gp((const int*)job->corr);
+  const auto key = gp((const unsigned long long*)job->key);
+  const auto corr = gpw(job->corr);
+  const auto sqd = gpw(job->sqd);
   const auto slab = gpw(job->slab);
+  const double max_corr2 = job->max_corr2;
   double R[9], t[3];
   for (int e = 0; e < 9; ++e) R[e] = st->R[e];
   for (int e = 0; e < 3; ++e) t[e] = st->t[e];
@@ -1125,11 +1331,24 @@ __global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ j
   const int wave = blockIdx.x * kMomWaves + wib;
   const int nwaves_total = gridDim.x * kMomWaves;
   const int ngroups = (src.n + 63) >> 6;
+  // the search's task counters are free again: zero them for the next one
+  if (blockIdx.x == 0 && threadIdx.x < kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const int i = g * 64 + lane;
     const bool active = i < src.n;
-    const int j = active ? corr[i] : -1;
+    // the search result key -> correspondences_ / sq_distances_
+    // (nano_gicp_impl.hpp:257-258): a match iff a point was found and its
+    // squared distance, promoted to double, is below max_corr^2
+    int j = -1;
+    if (active) {
+      const unsigned long long k = key[i];
+      const unsigned kj = (unsigned)k;
+      const float kd = __uint_as_float((unsigned)(k >> 32));
+      j = (kj != 0xffffffffu && (double)kd < max_corr2) ? (int)kj : -1;
+      corr[i] = j;
+      sqd[i] = kj != 0xffffffffu ? kd : INFINITY;
+    }
     Contrib C;
     if (j >= 0) {
       const float4 a = ldg4(src.pts, i);
@@ -1769,6 +1988,9 @@ void launch_morton(hipStream_t s, const float4* pts, int n, const float* quant, 
 void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, int npad, float4* sorted, int* inv_perm) {
   k_gather<<<cdiv(npad, 256), 256, 0, s>>>(raw, perm, n, npad, sorted, inv_perm);
 }
+void launch_leaf_soa(hipStream_t s, const float4* pts, int npad, float* soa) {
+  k_leaf_soa<<<cdiv(npad, 256), 256, 0, s>>>(pts, npad, soa);
+}
 void launch_leaf_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float4* lo, float4* hi) {
   k_leaf_boxes<<<cdiv(nleaves, 8), 256, 0, s>>>(pts, n, nleaves, lo, hi);
 }
@@ -1803,52 +2025,55 @@ void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out) {
   k_cov_export<<<cdiv(n, 256), 256, 0, s>>>(cov6, layout, n, perm, out);
 }
-void launch_align_init(hipStream_t s, const AlignJob* job) { k_align_init<<<1, 64, 0, s>>>(job); }
+void launch_align_init(hipStream_t s, const AlignJob* job) { k_align_init<<<1, 128, 0, s>>>(job); }
 size_t search_lds_bytes(int upper_count) {
   return (size_t)kLinWaves * kCollectLdsBytes + 2 * sizeof(f4v) * (size_t)upper_count;
 }
+static int env_knob(const char* name, int dflt) {   // development knobs (A/B of launch shapes)
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+size_t collect_lds_bytes(int upper_count) {
+  return (size_t)kLinWaves * kTaskLdsBytes + 2 * sizeof(f4v) * (size_t)upper_count;
+}
+// kTaskRegions-multiple grid of the scan kernel (4 waves per block)
+static int scan_blocks(int nsrc) {
+  const int groups = (nsrc + kTaskQ - 1) / kTaskQ;
+  static const int cap = [] {   // development knob
+    const char* v = std::getenv("DDLO_SCAN_WAVES");
+    return v && *v ? std::max(kTaskRegions, std::atoi(v)) : 8192;
+  }();
+  int waves = std::min(std::max(groups, kTaskRegions), cap);
+  waves = (waves + 8 * kTaskRegions - 1) / (8 * kTaskRegions) * (8 * kTaskRegions);
+  return waves / kScanWaves;
+}
 void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int job_upper_count) {
   const int search_groups = (nsrc + kSearchQ - 1) / kSearchQ;
-  const int sb = std::max(1, std::min((search_groups + kLinWaves - 1) / kLinWaves, 8192));
-  if (use_tile_search()) {  // experimental 64-query tile search (tile_search.hpp)
-    const int groups = (nsrc + 63) / 64;
-    const int tb = std::max(1, (groups + kLinWaves - 1) / kLinWaves);
-    const size_t lds = (size_t)kLinWaves * kTileLdsBytes + 2 * sizeof(f4v) * (size_t)job_upper_count;
-    k_nn_tile_a<<<tb, 64 * kLinWaves, lds, s>>>(job);
-    const int tbb = std::max(1, (groups + kLinWaves * kDeferGroups - 1) / (kLinWaves * kDeferGroups));
-    k_nn_tile_b<<<tbb, 64 * kLinWaves, lds, s>>>(job);
+  const int sb = std::max(1, (search_groups + kLinWaves - 1) / kLinWaves);
+  static const bool old_search = [] {   // DDLO_SEARCH=collect: the single-kernel collect-then-scan search (A/B)
+    const char* v = std::getenv("DDLO_SEARCH");
+    return v && std::strcmp(v, "collect") == 0;
+  }();
+  if (old_search) {
+    k_nn_search<kSearchQ, 3><<<sb, 64 * kLinWaves, search_lds_bytes(job_upper_count), s>>>(job);
   } else {
-    static const int occ = [] {
-      const char* v = std::getenv("DDLO_SEARCH_OCC");
-      return v && *v ? std::atoi(v) : 3;  // 3 waves/SIMD: no scratch spills (same speed as 4, no spill traffic)
-    }();
-    const size_t lds = search_lds_bytes(job_upper_count);
-    static const int q = [] {
-      const char* v = std::getenv("DDLO_SEARCH_Q");
-      return v && *v ? std::atoi(v) : kSearchQ;
-    }();
-    if (q == 8) {
-      const int g8 = (nsrc + 7) / 8;
-      k_nn_search<8, 3><<<std::max(1, (g8 + kLinWaves - 1) / kLinWaves), 64 * kLinWaves, lds, s>>>(job);
-    } else if (q == 32) {
-      const int g32 = (nsrc + 31) / 32;
-      k_nn_search<32, 3><<<std::max(1, (g32 + kLinWaves - 1) / kLinWaves), 64 * kLinWaves, lds, s>>>(job);
-    } else if (occ == 4) {
-      k_nn_search<kSearchQ, 4><<<sb, 64 * kLinWaves, lds, s>>>(job);
-    } else {
-      k_nn_search<kSearchQ, 3><<<sb, 64 * kLinWaves, lds, s>>>(job);
-    }
+    static const int occ_seed = env_knob("DDLO_OCC_SEED", 4), occ_col = env_knob("DDLO_OCC_COLLECT", 3),
+                     occ_scan = env_knob("DDLO_OCC_SCAN", 4);
+    if (occ_seed == 6) k_nn_seed<6><<<sb, 64 * kLinWaves, 0, s>>>(job);
+    else k_nn_seed<4><<<sb, 64 * kLinWaves, 0, s>>>(job);
+    const int cb = (search_groups + kHardMax + kLinWaves - 1) / kLinWaves;
+    if (occ_col == 4) k_nn_collect<4><<<cb, 64 * kLinWaves, collect_lds_bytes(job_upper_count), s>>>(job);
+    else k_nn_collect<3><<<cb, 64 * kLinWaves, collect_lds_bytes(job_upper_count), s>>>(job);
+    if (occ_scan == 6) k_nn_scan<6><<<scan_blocks(nsrc), 64 * kScanWaves, 0, s>>>(job);
+    else k_nn_scan<4><<<scan_blocks(nsrc), 64 * kScanWaves, 0, s>>>(job);
   }
   k_moments<<<nblocks, 64 * kMomWaves, 0, s>>>(job);
 }
-bool use_tile_search() {
-  static const bool tile = [] {
-    const char* v = std::getenv("DDLO_SEARCH");
-    return v && std::strcmp(v, "tile") == 0;
-  }();
-  return tile;
+int search_queries_per_wave() { return kSearchQ; }
+int task_cap_per_region(int nsrc) {
+  const long groups = (nsrc + kTaskQ - 1) / kTaskQ;
+  return (int)std::max<long>(1024, (groups * kTasksPerGroup + kTaskRegions - 1) / kTaskRegions);
 }
-int search_queries_per_wave() { return use_tile_search() ? 64 : kSearchQ; }
 int moment_blocks(int nsrc) {
   const int groups = (nsrc + 63) / 64;
   return std::max(1, std::min((groups + kMomWaves - 1) / kMomWaves, kMomBlocksMax));

@@ -12,6 +12,7 @@ void launch_pack_bbox(hipStream_t s, const unsigned char* raw, size_t stride, in
 void launch_bbox_final(hipStream_t s, const float* partial, int nparts, float* quant);
 void launch_morton(hipStream_t s, const float4* pts, int n, const float* quant, unsigned long long* keys, int* vals);
 void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, int npad, float4* sorted, int* inv_perm);
+void launch_leaf_soa(hipStream_t s, const float4* pts, int npad, float* soa);
 void launch_leaf_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float4* lo, float4* hi);
 void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int nchild, int nparent, float4* plo,
                         float4* phi);
@@ -24,7 +25,7 @@ void launch_align_init(hipStream_t s, const AlignJob* job);
 // tgt_upper: number of upper-level (>= 1) boxes of the target (LDS cache size)
 void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int tgt_upper);
 int search_queries_per_wave();
-bool use_tile_search();  // DDLO_SEARCH=tile selects the experimental 64-query tile search
+int task_cap_per_region(int nsrc);   // task-list slots per region for nsrc source points
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
 void launch_lm_step(hipStream_t s, const AlignJob* job);
 void launch_mom_reduce(hipStream_t s, const AlignJob* job);  // sharded align: slab -> job->mom

@@ -55,18 +55,32 @@ __device__ __forceinline__ float uniform_f(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 
-// wave-wide min/max; the result is uniform but deliberately left in a VGPR
-// (SGPRs are the scarce resource in the traversal kernels)
-__device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = fminf(v, __shfl_xor(v, m));
-  return v;
+// Wave-wide min/max with DPP (no LDS round trips): quad xor 1 / 2, half-row
+// and row mirrors give every lane its 16-lane row's value, then row_bcast15
+// / row_bcast31 fold the rows into lane 63, which is read back.
+template <bool MAX>
+__device__ __forceinline__ float dpp_fold(float v, int ctrl_sel) {
+  const int x = __float_as_int(v);
+  int r;
+  switch (ctrl_sel) {
+    case 0: r = __builtin_amdgcn_update_dpp(x, x, 0xb1, 0xf, 0xf, false); break;   // quad_perm [1,0,3,2]
+    case 1: r = __builtin_amdgcn_update_dpp(x, x, 0x4e, 0xf, 0xf, false); break;   // quad_perm [2,3,0,1]
+    case 2: r = __builtin_amdgcn_update_dpp(x, x, 0x141, 0xf, 0xf, false); break;  // row_half_mirror
+    case 3: r = __builtin_amdgcn_update_dpp(x, x, 0x140, 0xf, 0xf, false); break;  // row_mirror
+    case 4: r = __builtin_amdgcn_update_dpp(x, x, 0x142, 0xa, 0xf, false); break;  // row_bcast15 -> rows 1, 3
+    default: r = __builtin_amdgcn_update_dpp(x, x, 0x143, 0xc, 0xf, false); break; // row_bcast31 -> rows 2, 3
+  }
+  const float o = __int_as_float(r);
+  return MAX ? fmaxf(v, o) : fminf(v, o);
 }
-__device__ __forceinline__ float wave_max(float v) {
+template <bool MAX>
+__device__ __forceinline__ float wave_fold(float v) {
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
-  return v;
+  for (int c = 0; c < 6; ++c) v = dpp_fold<MAX>(v, c);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
+__device__ __forceinline__ float wave_min(float v) { return wave_fold<false>(v); }
+__device__ __forceinline__ float wave_max(float v) { return wave_fold<true>(v); }
 
 // squared distance, nanoflann L2_Simple_Adaptor order (no contraction)
 __device__ __forceinline__ float dist2(float qx, float qy, float qz, float px, float py, float pz) {

@@ -251,3 +251,40 @@ def test_swap_and_share(s2s_golden):
     # copy-on-write: new covariances on b do not change a's
     b.set_covariances(SOURCE, g["cov_tgt"] * 2.0)
     np.testing.assert_array_equal(a.get_covariances(SOURCE), g["cov_tgt"])
+
+
+def test_align_sequence_on_one_ctx_matches_fresh_ctx(s2s_golden):
+    """Aligns whose iteration counts go up and down on ONE ctx (the launch
+    prediction and speculation adapt to the previous align) give the same
+    pose, iteration count, LM trials and flags as each align on a fresh ctx
+    and as the oracle."""
+    g = s2s_golden
+    c = s2s_ctx(g)
+    o = O.Gicp(g["src"], g["tgt"], O.default_params(**S2S))
+    o.set_covariances(0, g["cov_src_PLANE"])
+    o.set_covariances(1, g["cov_tgt"])
+    # small -> large -> tiny -> large -> medium -> identity
+    offsets = [(0.02, 0.002), (0.35, 0.03), (0.0, 0.0), (0.45, 0.04), (0.1, 0.01), (0.3, 0.0)]
+    rng = np.random.default_rng(41)
+    seen = []
+    for dt, dr in offsets:
+        guess = np.eye(4, dtype=np.float32)
+        guess[:3, :3] = NP.so3_exp(rng.normal(0, 1, 3) * dr)
+        guess[:3, 3] = rng.normal(0, 1, 3) * dt
+        pose, res = c.align(guess)
+        f = s2s_ctx(g)
+        fpose, fres = f.align(guess)
+        f.close()
+        opose, ores = o.align(guess)
+        assert (res.iterations_run, res.nr_iterations, res.converged, res.lm_failed, res.lm_trials) == \
+            (fres.iterations_run, fres.nr_iterations, fres.converged, fres.lm_failed, fres.lm_trials)
+        np.testing.assert_array_equal(pose, fpose)
+        assert (res.iterations_run, res.converged, res.lm_trials) == (ores.iterations_run, ores.converged, ores.lm_trials)
+        np.testing.assert_allclose(pose, opose, atol=1e-6)
+        # state read after the align (the trailing chunk may still be queued)
+        out = c.transform_source()
+        ref = (g["src"].astype(np.float64) @ pose[:3, :3].T.astype(np.float64) + pose[:3, 3]).astype(np.float32)
+        np.testing.assert_allclose(out, ref, atol=2e-5)
+        seen.append(res.iterations_run)
+    # the sequence really exercised rising and falling iteration counts
+    assert any(b > a for a, b in zip(seen, seen[1:])) and any(b < a for a, b in zip(seen, seen[1:])), seen

@@ -3,10 +3,13 @@
 usage: python tools/profile_summary.py <rocprof dir> [prefix=run] > profiles/<name>.md
 
 Besides rocprof's own per-kernel stats it splits every align() into its outer
-iterations (k_align_init, then k_nn_search / k_moments / k_lm_step triples)
-and separates ACTIVE iterations from the no-op launches of the speculative
-graph chunk (an iteration after convergence exits at its first instruction:
-k_nn_search < NOOP_US).  The "linearize" average (k_nn_search + k_moments of
+iterations (k_align_init, then per iteration the search kernels — k_nn_collect +
+k_nn_scan, or the single-kernel k_nn_search — k_moments and k_lm_step)
+and separates ACTIVE iterations from no-op launches (an iteration after
+convergence exits at its first instruction: search kernels < NOOP_US).  No-ops
+are counted per origin: the eager profiled path (gicp_set_profiling)
+launches all max_iterations iterations of an align, a graph align launches
+at most one speculative chunk after the converged one.  The "linearize" average (search + k_moments of
 an active iteration) is the quantity bench.py's roofline reports from HIP
 events.
 """
@@ -14,7 +17,7 @@ import csv
 import sys
 from collections import defaultdict
 
-NOOP_US = 8.0
+NOOP_US = 20.0   # summed search kernels of an iteration that exits at once (three launches, ~4-6 us each)
 
 
 def short(name):
@@ -35,48 +38,66 @@ def main():
     trace = list(csv.DictReader(open(f"{d}/{pre}_kernel_trace.csv")))
     trace.sort(key=lambda x: int(x["Start_Timestamp"]))
     seq = [(short(x["Kernel_Name"]).split("<")[0], (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3) for x in trace]
+    SEARCH = ("k_nn_search", "k_nn_seed", "k_nn_collect", "k_nn_scan")
+    LOOP = SEARCH + ("k_moments", "k_lm_step")
     aligns = []
     cur = None
     for n, us in seq:
         if n == "k_align_init":
             cur = []
             aligns.append(cur)
-        elif cur is not None and n in ("k_nn_search", "k_moments", "k_lm_step"):
+        elif cur is not None and n in LOOP:
             cur.append((n, us))
-        elif cur is not None and n not in ("k_nn_search", "k_moments", "k_lm_step"):
+        else:
             cur = None
     per_pos = defaultdict(lambda: defaultdict(list))
     active_lin, active_search, active_mom, active_lm = [], [], [], []
-    noop = []
+    noop, noop_eager = [], []
+    eager_aligns = 0
     for a in aligns:
+        # iterations: search kernels..., k_moments, k_lm_step
+        iters, it_k = [], defaultdict(float)
+        for n, us in a:
+            it_k[n] += us
+            if n == "k_lm_step":
+                iters.append(it_k)
+                it_k = defaultdict(float)
+        # a graph align launches <= kMaxFirstChunk (8) + a few single-iteration
+        # chunks; an eager profiled align launches every iteration
+        eager = len(iters) > 12
+        eager_aligns += eager
         it = 0
-        for i in range(0, len(a) - 2, 3):
-            (n0, s), (n1, m), (n2, l) = a[i], a[i + 1], a[i + 2]
-            if (n0, n1, n2) != ("k_nn_search", "k_moments", "k_lm_step"):
-                break
-            if s < NOOP_US:
-                noop.append(s + m + l)
+        for k in iters:
+            s_us = sum(k[n] for n in SEARCH)
+            m, l = k["k_moments"], k["k_lm_step"]
+            if s_us < NOOP_US:
+                (noop_eager if eager else noop).append(s_us + m + l)
                 continue
-            per_pos[it]["search"].append(s)
+            per_pos[it]["search"].append(s_us)
+            per_pos[it]["seed"].append(k["k_nn_seed"])
+            per_pos[it]["collect"].append(k["k_nn_collect"])
+            per_pos[it]["scan"].append(k["k_nn_scan"])
             per_pos[it]["moments"].append(m)
             per_pos[it]["lm"].append(l)
-            active_lin.append(s + m)
-            active_search.append(s)
+            active_lin.append(s_us + m)
+            active_search.append(s_us)
             active_mom.append(m)
             active_lm.append(l)
             it += 1
     avg = lambda v: sum(v) / len(v) if v else float("nan")
-    print(f"\n## Active outer iterations ({len(aligns)} aligns, {len(active_lin)} active iterations, "
-          f"{len(noop)} no-op iterations of the speculative chunk)\n")
-    print("| iteration | n | k_nn_search us | k_moments us | k_lm_step us |")
+    print(f"\n## Active outer iterations ({len(aligns)} aligns, {len(active_lin)} active iterations; no-op "
+          f"iterations: {len(noop)} in {len(aligns) - eager_aligns} graph aligns (speculative chunk), "
+          f"{len(noop_eager)} in {eager_aligns} eager profiled aligns)\n")
+    print("| iteration | n | search us (seed + collect + scan) | k_moments us | k_lm_step us |")
     print("|---:|---:|---:|---:|---:|")
     for it in sorted(per_pos):
         p = per_pos[it]
-        print(f"| {it} | {len(p['search'])} | {avg(p['search']):.1f} | {avg(p['moments']):.1f} | {avg(p['lm']):.1f} |")
-    print(f"\n- linearize (k_nn_search + k_moments) average over active iterations: **{avg(active_lin):.1f} us** "
+        print(f"| {it} | {len(p['search'])} | {avg(p['search']):.1f} ({avg(p['seed']):.1f} + {avg(p['collect']):.1f} + {avg(p['scan']):.1f}) | "
+              f"{avg(p['moments']):.1f} | {avg(p['lm']):.1f} |")
+    print(f"\n- linearize (search kernels + k_moments) average over active iterations: **{avg(active_lin):.1f} us** "
           f"(search {avg(active_search):.1f} + moments {avg(active_mom):.1f})")
     print(f"- k_lm_step average over active iterations: {avg(active_lm):.1f} us")
-    print(f"- no-op iteration (3 launches) average: {avg(noop):.1f} us")
+    print(f"- no-op iteration (3 launches) average: {avg(noop + noop_eager):.1f} us")
 
 
 if __name__ == "__main__":
