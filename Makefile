@@ -18,7 +18,7 @@ $(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/search.hpp $(CSRC)/nn_tasks.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h
+$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/runtime.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -13,6 +13,7 @@ namespace ddlo {
 constexpr int kLeafSize = 32;
 constexpr int kFanout = 64;
 constexpr int kMaxLevels = 5;   // leaves + 4 internal levels: n <= 32*64^4
+constexpr int kDirBits = 18;    // key directory: top 18 of the 63 Morton-key bits (1 MB per cloud)
 
 // Number of moment slots the linearize kernel reduces per source point
 // (see DESIGN.md "Normal-equation moments"): 6 (sum M) + 18 (sum q_k M) +
@@ -41,6 +42,7 @@ struct CloudDev {
   const float4* box_hi;
   const float* quant;             // device [lo.x, lo.y, lo.z, scale]
   const float* soa;               // per leaf: x[32], y[32], z[32] (sorted, sentinel-padded)
+  const int* dir;                 // key directory [2^kDirBits + 1] (see search.hpp dir_range)
   int n;
   int nlevels;
   // per-level node offset/count, kept as scalars (no array => no scratch
@@ -121,9 +123,12 @@ struct AlignJob {
   int task_cap_r;
   int* hard_list;                // [kHardMax] sub-groups with a wide union box
   unsigned char* hard_flag;      // [n_src / 16] 1 = listed (walked by the first waves)
-  float hard_extent;             // union-box extent (m) above which a sub-group is hard
+  float hard_extent;             // union-box extent (m) above which a sub-group is hard (first iteration)
+  unsigned short* grp_blocks;    // [n_src / 16] blocks the last collect walked per sub-group
+  int hard_blocks;               // later iterations: hard if the last walk took more blocks
   int xcd_scan;                  // scan: one spatial eighth of the tasks per XCD (speed only)
-  int prev_window;         // search: seed a large pose step from the window around the previous match
+  int prev_window;         // seed after a large pose step: 0 previous match only, 1 + Morton window around it,
+                           // 2 + Morton window at the new position (default)
 };
 
 }  // namespace ddlo

@@ -136,6 +136,18 @@ __global__ __launch_bounds__(256) void k_gather(const float4* __restrict__ raw, 
 }
 
 // one 32-lane half-wave per leaf
+// Key directory (search.hpp dir_range): thread i of the sorted keys fills
+// the prefixes in (prefix(i - 1), prefix(i)] with i; the last thread also
+// fills the prefixes past the largest key with n.
+__global__ __launch_bounds__(256) void k_key_dir(const unsigned long long* __restrict__ keys, int n, int* __restrict__ dir) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  constexpr int sh = 63 - kDirBits;
+  const long pa = i == 0 ? -1 : (long)(keys[i - 1] >> sh);
+  const long pb = i == n ? (1l << kDirBits) : (long)(keys[i] >> sh);
+  for (long p = pa + 1; p <= pb; ++p) dir[p] = i;
+}
+
 // Per-leaf SoA copy of the sorted points: leaf l = x[32], y[32], z[32], so
 // that a lane's 8 consecutive coordinates are two 16-B loads per axis and
 // pairs of them feed the packed-math distance directly (k_nn_scan).
@@ -778,6 +790,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     vis.skip_hi = 0;
     bool seeded = false;
     bool large_step = false;   // previous match exists but the pose moved >= 2 cm since
+    bool rewindow = false;     // mode 2: previous match's distance AND the Morton window at the new position
     // coordinates of the point behind vis.bestj when it is already in registers
     float bpx = 0.f, bpy = 0.f, bpz = 0.f;
     bool have_bp = true;
@@ -799,9 +812,10 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
             vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
             seeded = true;
           }
-        } else if (prev_window) {
+        } else if (prev_window == 1) {
           large_step = true;   // exact distances to the Morton window around p_prev (below)
-        } else {  // large pose step: the exact distance to the previous match
+        } else {  // large pose step: the exact distance to the previous match (+ mode 2: the Morton window below)
+          rewindow = prev_window == 2;
           const float4 p = ldg4(tgt.pts, j);
           const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
           if (d < cap2) {
@@ -821,14 +835,17 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     // pose step the window is centred on the previous match instead (its
     // sorted position IS a Morton position next to the new nearest point,
     // and no key search is needed); the window contains the previous match.
-    const bool need_seed = active && !seeded && !large_step;
+    const bool need_seed = active && ((!seeded && !large_step) || rewindow);
     const bool use_window = need_seed || large_step;
     bool again = false;
     if (__any(use_window)) {
       // Morton window of kSeedW points per slice lane (64/Q * kSeedW per query)
       int pos = large_step ? jprev : 0;
       if (__any(need_seed)) {
-        const int lb = group_lower_bound<Q>(tgt.keys, tgt.n, morton_key(qx, qy, qz, tgt.quant));
+        const unsigned long long qk = morton_key(qx, qy, qz, tgt.quant);
+        int dlo, dhi;
+        dir_range(tgt.dir, qk, dlo, dhi);   // one load instead of ~5 dependent search steps
+        const int lb = group_lower_bound<Q>(tgt.keys, tgt.n, qk, dlo, dhi);
         if (need_seed) pos = lb;
       }
       const int s = lane / Q;
@@ -888,7 +905,10 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     // hard sub-group: a wide union box (a query far from every target point
     // drags many blocks into the walk) -> listed, walked first
     const WaveBox whole = make_wave_box(active, qx, qy, qz, active ? vis.best : -1.f);
-    const bool hard = box_extent(whole) > job->hard_extent;
+    // hard: the previous outer iteration walked many blocks for this
+    // sub-group (same source points, a nearby pose), else -- first
+    // iteration -- a wide union box
+    const bool hard = have_prev ? job->grp_blocks[g] > job->hard_blocks : box_extent(whole) > job->hard_extent;
     if (lane == 0) {
       int slot = -1;
       if (hard) {
@@ -966,6 +986,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __rest
   col.sg = g;
   col.run(tgt, tl, skey, job->split_extent);
   if (inrange && lane < Q && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
+  if (lane == 0) job->grp_blocks[g] = (unsigned short)min(col.st_blocks, 65535u);
   if (stats && lane == 0) {
     const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
     unsigned int* o = stats + (size_t)g * kStatFields;
@@ -978,11 +999,12 @@ __global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __rest
   }
 }
 
-// K3b: leaf scans of the task list.  The waves of region r split its tasks
-// into contiguous chunks (XCD-aware, see below).  A wave stages a batch of
-// kScanBatch tasks in LDS with LDS-DMA — per task the leaf's 32 SoA points
-// (384 B) and the sub-group's 16 query states (256 B) — waits once, and
-// scans them from LDS (lane = query qi x quarter s of the leaf).  A
+// K3c: leaf scans of the task list.  The waves of region r split its tasks
+// into contiguous chunks (XCD-aware, see below).  A wave loads up to 64
+// task words at once and stages batches of kScanBatch tasks in LDS with
+// LDS-DMA — per task the leaf's 32 SoA points (384 B) and the sub-group's 16
+// query states (256 B) — double-buffered: batch k + 1 is in flight while
+// batch k is scanned from LDS (lane = query qi x quarter s of the leaf).  A
 // sub-group's tasks sit next to each other in the list (one collect flush),
 // so the per-query minimum is kept in registers across a run of the same
 // sub-group and merged into the result with one 64-bit atomicMin per query.
@@ -992,7 +1014,7 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
   return ((unsigned long long)hi << 32) | lo;
 }
 
-constexpr int kScanBatch = 16;                        // tasks per LDS batch
+constexpr int kScanBatch = 8;                         // tasks per LDS batch (two batches in flight)
 constexpr int kScanTaskBytes = 3 * kLeafSize * 4 + kTaskQ * 16;   // 384 B points + 256 B queries
 constexpr int kScanWaves = 4;                         // waves per block
 
@@ -1006,8 +1028,10 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   const int cap_r = job->task_cap_r;
   const int lane = lane_id();
   const int qi = lane & 15, s = lane >> 4;
-  __shared__ __attribute__((aligned(16))) unsigned char lds_all[kScanWaves][kScanBatch * kScanTaskBytes];
-  unsigned char* const L = lds_all[threadIdx.x >> 6];
+  constexpr int kBatchBytes = kScanBatch * kScanTaskBytes;   // 5 KB = 5 LDS-DMA wave-instructions
+  __shared__ __attribute__((aligned(16))) unsigned char lds_all[kScanWaves][2][kBatchBytes];
+  unsigned char* const L0 = lds_all[threadIdx.x >> 6][0];
+  unsigned char* const L1 = lds_all[threadIdx.x >> 6][1];
   const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
   const int wpr = nwaves / kTaskRegions;   // the grid is a multiple of 8 * kTaskRegions waves
   // (region, chunk) of this wave.  A region's tasks were appended roughly in
@@ -1033,66 +1057,79 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   int run_sg = -1;
   unsigned long long acc = ~0ull;   // lane's query minimum over the current run
   float run_bound = -1.f;
-  for (int base = lo; base < hi; base += kScanBatch) {
-    const int cnt = min(kScanBatch, hi - base);
-    const unsigned long long tl = lane < cnt ? rt[base + lane] : 0ull;
-    // LDS-DMA the batch: 16 B per lane per instruction, 1 KB per wave-instruction
+  for (int wbase = lo; wbase < hi; wbase += 64) {
+    const int wcnt = min(64, hi - wbase);
+    const unsigned long long tl = lane < wcnt ? rt[wbase + lane] : 0ull;   // up to 64 task words at once
+    // LDS-DMA tasks [b0, b0 + kScanBatch) of the window: 16 B per lane per
+    // instruction, 1 KB per wave-instruction (past the window: the last task
+    // again, never read)
+    auto issue = [&](int b0, unsigned char* buf) {
 #pragma unroll
-    for (int i = 0; i < kScanBatch * kScanTaskBytes / 1024; ++i) {
-      const int o = i * 1024 + lane * 16;
-      const int k = o / kScanTaskBytes, w = o % kScanTaskBytes;
-      const int kk = min(k, cnt - 1);   // past the batch: reload the last task (never read)
-      const unsigned long long tk = __shfl(tl, kk);
-      const char* src = w < 3 * kLeafSize * 4
-                            ? (const char*)(tgt.soa + (size_t)(tk >> 40) * (3 * kLeafSize)) + w
-                            : (const char*)(qstate + (size_t)((tk >> 16) & 0xffffffull) * kTaskQ) + (w - 3 * kLeafSize * 4);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(L + i * 1024), 16, 0, 0);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the batch has landed in LDS
-    __builtin_amdgcn_wave_barrier();
-    for (int k = 0; k < cnt; ++k) {
-      const unsigned long long t = readlane_u64(tl, k);
-      const int sg = (int)((t >> 16) & 0xffffffull);
-      if (sg != run_sg) {   // uniform: a new sub-group's run starts
-        if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound))
-          atomicMin(key + (size_t)run_sg * kTaskQ + qi, acc);
-        run_sg = sg;
-        acc = ~0ull;
-        run_bound = -1.f;
+      for (int i = 0; i < kBatchBytes / 1024; ++i) {
+        const int o = i * 1024 + lane * 16;
+        const int k = min(b0 + o / kScanTaskBytes, wcnt - 1), w = o % kScanTaskBytes;
+        const unsigned long long tk = __shfl(tl, k);
+        const char* src = w < 3 * kLeafSize * 4
+                              ? (const char*)(tgt.soa + (size_t)(tk >> 40) * (3 * kLeafSize)) + w
+                              : (const char*)(qstate + (size_t)((tk >> 16) & 0xffffffull) * kTaskQ) + (w - 3 * kLeafSize * 4);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
       }
-      const unsigned char* T = L + k * kScanTaskBytes;
-      const f4v x0 = *(const f4v*)(T + s * 32), x1 = *(const f4v*)(T + s * 32 + 16);
-      const f4v y0 = *(const f4v*)(T + 128 + s * 32), y1 = *(const f4v*)(T + 128 + s * 32 + 16);
-      const f4v z0 = *(const f4v*)(T + 256 + s * 32), z1 = *(const f4v*)(T + 256 + s * 32 + 16);
-      const f4v q = *(const f4v*)(T + 384 + qi * 16);
-      const float X[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      const float Y[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
-      const float Z[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
-      // same IEEE ops as dist2(), two points per packed instruction; the
-      // lane's points come in increasing position, so strict < keeps the
-      // lowest position among equal distances
-      const f2v qx2 = {q.x, q.x}, qy2 = {q.y, q.y}, qz2 = {q.z, q.z};
-      float bd = INFINITY;
-      int bh = 0;
+    };
+    issue(0, L0);
+    for (int b0 = 0; b0 < wcnt; b0 += kScanBatch) {
+      unsigned char* const cur = ((b0 / kScanBatch) & 1) ? L1 : L0;
+      if (b0 + kScanBatch < wcnt) {
+        issue(b0 + kScanBatch, ((b0 / kScanBatch) & 1) ? L0 : L1);
+        __builtin_amdgcn_s_waitcnt(0x0F75);  // vmcnt(5): all but the 5 just issued -> the current batch landed
+      } else {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int nb = min(kScanBatch, wcnt - b0);
+      for (int k = 0; k < nb; ++k) {
+        const unsigned long long t = readlane_u64(tl, b0 + k);
+        const int sg = (int)((t >> 16) & 0xffffffull);
+        if (sg != run_sg) {   // uniform: a new sub-group's run starts
+          if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound))
+            atomicMin(key + (size_t)run_sg * kTaskQ + qi, acc);
+          run_sg = sg;
+          acc = ~0ull;
+          run_bound = -1.f;
+        }
+        const unsigned char* T = cur + k * kScanTaskBytes;
+        const f4v x0 = *(const f4v*)(T + s * 32), x1 = *(const f4v*)(T + s * 32 + 16);
+        const f4v y0 = *(const f4v*)(T + 128 + s * 32), y1 = *(const f4v*)(T + 128 + s * 32 + 16);
+        const f4v z0 = *(const f4v*)(T + 256 + s * 32), z1 = *(const f4v*)(T + 256 + s * 32 + 16);
+        const f4v q = *(const f4v*)(T + 384 + qi * 16);
+        const float X[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const float Y[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+        const float Z[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+        // same IEEE ops as dist2(), two points per packed instruction; the
+        // lane's points come in increasing position, so strict < keeps the
+        // lowest position among equal distances
+        const f2v qx2 = {q.x, q.x}, qy2 = {q.y, q.y}, qz2 = {q.z, q.z};
+        float bd = INFINITY;
+        int bh = 0;
 #pragma unroll
-      for (int h = 0; h < 8; h += 2) {
-        const f2v dx = qx2 - f2v{X[h], X[h + 1]};
-        const f2v dy = qy2 - f2v{Y[h], Y[h + 1]};
-        const f2v dz = qz2 - f2v{Z[h], Z[h + 1]};
-        const f2v d = (dx * dx + dy * dy) + dz * dz;
-        if (d.x < bd) { bd = d.x; bh = h; }
-        if (d.y < bd) { bd = d.y; bh = h + 1; }
+        for (int h = 0; h < 8; h += 2) {
+          const f2v dx = qx2 - f2v{X[h], X[h + 1]};
+          const f2v dy = qy2 - f2v{Y[h], Y[h + 1]};
+          const f2v dz = qz2 - f2v{Z[h], Z[h + 1]};
+          const f2v d = (dx * dx + dy * dy) + dz * dz;
+          if (d.x < bd) { bd = d.x; bh = h; }
+          if (d.y < bd) { bd = d.y; bh = h + 1; }
+        }
+        unsigned long long bk = dkey(bd, (int)(t >> 40) * kLeafSize + s * 8 + bh);
+        bk = xor_min64<16>(bk);
+        bk = xor_min64<32>(bk);
+        if (((t >> qi) & 1ull) != 0ull) {
+          acc = umin64(acc, bk);
+          run_bound = q.w;
+        }
       }
-      unsigned long long bk = dkey(bd, (int)(t >> 40) * kLeafSize + s * 8 + bh);
-      bk = xor_min64<16>(bk);
-      bk = xor_min64<32>(bk);
-      if (((t >> qi) & 1ull) != 0ull) {
-        acc = umin64(acc, bk);
-        run_bound = q.w;
-      }
+      __builtin_amdgcn_wave_barrier();   // reads of `cur` done before it is refilled
     }
-    __builtin_amdgcn_wave_barrier();   // LDS reads done before the next batch overwrites it
   }
   if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound))
     atomicMin(key + (size_t)run_sg * kTaskQ + qi, acc);
@@ -1223,7 +1260,10 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
       // Morton window of kSeedW points per slice lane (64/Q * kSeedW per query)
       int pos = large_step ? jprev : 0;
       if (__any(need_seed)) {
-        const int lb = group_lower_bound<Q>(tgt.keys, tgt.n, morton_key(qx, qy, qz, tgt.quant));
+        const unsigned long long qk = morton_key(qx, qy, qz, tgt.quant);
+        int dlo, dhi;
+        dir_range(tgt.dir, qk, dlo, dhi);   // one load instead of ~5 dependent search steps
+        const int lb = group_lower_bound<Q>(tgt.keys, tgt.n, qk, dlo, dhi);
         if (need_seed) pos = lb;
       }
       const int s = lane / Q;
@@ -1987,6 +2027,9 @@ void launch_morton(hipStream_t s, const float4* pts, int n, const float* quant, 
 }
 void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, int npad, float4* sorted, int* inv_perm) {
   k_gather<<<cdiv(npad, 256), 256, 0, s>>>(raw, perm, n, npad, sorted, inv_perm);
+}
+void launch_key_dir(hipStream_t s, const unsigned long long* keys, int n, int* dir) {
+  k_key_dir<<<cdiv(n + 1, 256), 256, 0, s>>>(keys, n, dir);
 }
 void launch_leaf_soa(hipStream_t s, const float4* pts, int npad, float* soa) {
   k_leaf_soa<<<cdiv(npad, 256), 256, 0, s>>>(pts, npad, soa);

@@ -1,0 +1,345 @@
+// runtime.hpp — device-side objects of the GICP runtime shared by the C-ABI
+// (capi.hip) and the odometry driver (odom.hip): the caching device
+// allocator, ref-counted device clouds (Morton-sorted points + search
+// hierarchy) and covariance sets, and the per-ctx state behind gicp_ctx.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>  // types only (ncclComm_t)
+
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/ddlo_gicp.h"
+#include "gicp_types.hpp"
+#include "launch.hpp"
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return ::ddlo::rt::fail(_e == hipErrorOutOfMemory ? GICP_ENOMEM : GICP_EHIP,          \
+                              std::string(#expr) + ": " + hipGetErrorString(_e));           \
+  } while (0)
+
+namespace ddlo {
+namespace rt {
+
+
+inline thread_local std::string g_last_error;
+
+inline gicp_status fail(gicp_status s, const std::string& msg) {
+  g_last_error = msg;
+  return s;
+}
+
+
+
+// Caching device allocator.  hipFree synchronizes the whole device, which
+// would serialize every ctx of a multi-stream batch (a new cloud index and
+// covariance set per scan); released blocks go to a per-(device, size class)
+// free list instead and are handed out again.  Safe because every entry
+// point that enqueues work on a buffer waits for it before returning, so a
+// buffer is idle whenever its owner releases it (the speculative no-op
+// iteration of an align touches only ctx-owned state, freed at ctx
+// destruction after a stream synchronize).
+struct DevicePool {
+  std::mutex m;
+  std::multimap<std::pair<int, size_t>, void*> free_blocks;
+  static size_t size_class(size_t b) {  // <= 12.5 % rounding, so same-shape clouds share a class
+    b = std::max<size_t>(b, 256);
+    size_t top = 1;
+    while ((top << 1) <= b) top <<= 1;
+    const size_t g = std::max<size_t>(top / 8, 256);
+    return (b + g - 1) / g * g;
+  }
+  hipError_t alloc(size_t cls, void** p) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+      std::lock_guard<std::mutex> lk(m);
+      auto it = free_blocks.find({dev, cls});
+      if (it != free_blocks.end()) {
+        *p = it->second;
+        free_blocks.erase(it);
+        return hipSuccess;
+      }
+    }
+    e = hipMalloc(p, cls);
+    if (e == hipErrorOutOfMemory) {  // give the cached blocks back and retry once
+      trim();
+      e = hipMalloc(p, cls);
+    }
+    return e;
+  }
+  void release(int dev, size_t cls, void* p) {
+    std::lock_guard<std::mutex> lk(m);
+    free_blocks.insert({{dev, cls}, p});
+  }
+  void trim() {
+    std::lock_guard<std::mutex> lk(m);
+    for (auto& kv : free_blocks) (void)hipFree(kv.second);
+    free_blocks.clear();
+  }
+};
+inline DevicePool& device_pool() {
+  static DevicePool* pool = new DevicePool();  // never destroyed: blocks live until exit
+  return *pool;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int dev = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { reset(); }
+  void reset() {
+    if (p) device_pool().release(dev, bytes, p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t b) {
+    if (b <= bytes && p) return hipSuccess;
+    reset();
+    const size_t cls = DevicePool::size_class(b);
+    hipError_t e = device_pool().alloc(cls, &p);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    (void)hipGetDevice(&dev);
+    bytes = cls;
+    return e;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+// Immutable device cloud + search hierarchy (shared between ctxs/sides).
+struct CloudData {
+  int n = 0;
+  DevBuf pts, keys, perm, inv_perm, box_lo, box_hi, quant, soa, dir;
+  int nlevels = 0;
+  int lvl_off[kMaxLevels] = {0};
+  int lvl_cnt[kMaxLevels] = {0};
+  int upper_count() const {
+    return nlevels <= 1 ? 0 : lvl_off[nlevels - 1] + lvl_cnt[nlevels - 1] - lvl_off[1];
+  }
+  CloudDev dev() const {
+    CloudDev c;
+    c.pts = pts.as<float4>();
+    c.keys = keys.as<unsigned long long>();
+    c.perm = perm.as<int>();
+    c.inv_perm = inv_perm.as<int>();
+    c.box_lo = box_lo.as<float4>();
+    c.box_hi = box_hi.as<float4>();
+    c.quant = quant.as<float>();
+    c.soa = soa.as<float>();
+    c.dir = dir.as<int>();
+    c.n = n;
+    c.nlevels = nlevels;
+    c.off0 = lvl_off[0]; c.off1 = lvl_off[1]; c.off2 = lvl_off[2]; c.off3 = lvl_off[3]; c.off4 = lvl_off[4];
+    c.cnt0 = lvl_cnt[0]; c.cnt1 = lvl_cnt[1]; c.cnt2 = lvl_cnt[2]; c.cnt3 = lvl_cnt[3]; c.cnt4 = lvl_cnt[4];
+    return c;
+  }
+};
+
+struct CovData {
+  int n = 0;
+  DevBuf cov6;  // sym6 per SORTED point
+};
+
+struct Side {
+  std::shared_ptr<CloudData> cloud;
+  std::shared_ptr<CovData> cov;
+  bool has_cov() const { return cloud && cov && cov->n == cloud->n; }
+};
+
+inline int levels_for(int n, int* cnt, int* off) {
+  int c = (n + kLeafSize - 1) / kLeafSize;
+  int L = 0, o = 0;
+  for (;;) {
+    if (L >= kMaxLevels) return -1;
+    cnt[L] = c;
+    off[L] = o;
+    o += c;
+    ++L;
+    if (c <= kFanout) break;
+    c = (c + kFanout - 1) / kFanout;
+  }
+  return L;
+}
+
+}  // namespace rt
+}  // namespace ddlo
+
+using namespace ddlo;
+using namespace ddlo::rt;
+
+// one captured chunk: the graph and its executable instance
+struct hipExecGraphPair {
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+};
+
+constexpr int kDefaultPredictedIters = 4;
+
+struct gicp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  gicp_params params{};
+  Side src, tgt;
+  // build scratch
+  DevBuf raw_bytes, raw_pts, partial, nonfinite, keys_tmp, vals_tmp, sort_tmp;
+  // align buffers
+  DevBuf corr, sqd, slab, job_dev, state_dev, tmp_out, stats;
+  bool stats_on = false;
+  AlignJob* job_host = nullptr;   // pinned
+  // pinned, two slots: chunk k publishes its end state to slot k % 2, so the
+  // (at most one) chunk queued behind the one the host is reading never
+  // writes the bytes being read (no torn pose / done / iter)
+  AlignState* state_host = nullptr;
+  int state_slot = 0;              // slot holding the state of the last align / linearize
+  hipEvent_t tail_ev = nullptr;    // last chunk launched by the last align (may still be queued)
+  bool tail_pending = false;
+  int* flag_host = nullptr;       // pinned
+  bool have_align = false;        // a linearize ran against the current src/tgt
+  int last_nsrc = 0;
+  // chunk graphs: [init + n iterations + state copy to slot 0] for the
+  // predicted iteration count n (one per n, index n - 1) and [1 iteration +
+  // state copy to slot s] for s = 0, 1
+  std::vector<hipExecGraphPair> g_first;
+  hipExecGraphPair g_rest[2];
+  std::tuple<int, int, const void*> graph_key{-1, -1, nullptr};
+  int predicted_iters = kDefaultPredictedIters;   // iterations of the previous align on this ctx
+  std::vector<hipEvent_t> chunk_ev;
+  hipStream_t copy_stream = nullptr;
+  bool profiling = false;
+  std::vector<hipEvent_t> prof_ev;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // spatial sharding: ownership slab + RCCL communicator
+  int own_axis = -1;
+  float own_lo = -INFINITY, own_hi = INFINITY;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  DevBuf mom;          // [kSlabStride] reduced moments, all-reduced in place
+  DevBuf search;       // correspondence search: [qstate f4 x n][key u64 x n][counters][tasks]
+  bool speculate = true;    // queue a follow-on chunk before the first one's flag is seen
+  bool comm_graphs = true;  // RCCL captured into the chunk graphs (else eager chunks)
+};
+
+namespace ddlo {
+namespace rt {
+
+
+inline const AlignState& final_state(const gicp_ctx* c) { return c->state_host[c->state_slot]; }
+
+// Wait for the align's trailing no-op chunk (if one is still queued) before
+// a ctx-owned buffer it touches may be released to the device pool.
+inline gicp_status drain_tail(gicp_ctx* c) {
+  if (c->tail_pending) {
+    HIP_TRY(hipEventSynchronize(c->tail_ev));
+    c->tail_pending = false;
+  }
+  return GICP_OK;
+}
+
+inline gicp_status set_device(const gicp_ctx* c) {
+  HIP_TRY(hipSetDevice(c->device));
+  return GICP_OK;
+}
+
+inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, std::shared_ptr<CloudData>* out) {
+  if (!xyz || n == 0 || stride < 12 || (stride % 4) != 0) return fail(GICP_EINVAL, "invalid cloud (null, empty or bad stride)");
+  if (n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "cloud too large");
+  auto cd = std::make_shared<CloudData>();
+  const int N = (int)n;
+  cd->n = N;
+  cd->nlevels = levels_for(N, cd->lvl_cnt, cd->lvl_off);
+  if (cd->nlevels < 0) return fail(GICP_EINVAL, "cloud too large for the search hierarchy");
+  if (cd->upper_count() > 2048)  // LDS cache of levels >= 1 (64 KB): <= 4.2M points
+    return fail(GICP_EINVAL, "cloud too large for the search hierarchy's LDS cache (max ~4.2M points)");
+  const int total_boxes = cd->lvl_off[cd->nlevels - 1] + cd->lvl_cnt[cd->nlevels - 1];
+  hipStream_t s = c->stream;
+  const size_t raw_sz = (n - 1) * stride + 12;
+  HIP_TRY(c->raw_bytes.ensure(raw_sz));
+  HIP_TRY(hipMemcpyAsync(c->raw_bytes.p, xyz, raw_sz, hipMemcpyHostToDevice, s));
+  const int nb = (N + 255) / 256;
+  HIP_TRY(c->raw_pts.ensure(sizeof(float4) * n));
+  HIP_TRY(c->partial.ensure(sizeof(float) * 6 * nb));
+  HIP_TRY(c->nonfinite.ensure(sizeof(int)));
+  HIP_TRY(hipMemsetAsync(c->nonfinite.p, 0, sizeof(int), s));
+  HIP_TRY(cd->quant.ensure(sizeof(float) * 8));
+  launch_pack_bbox(s, c->raw_bytes.as<unsigned char>(), stride, N, c->raw_pts.as<float4>(), c->partial.as<float>(),
+                   c->nonfinite.as<int>(), nb);
+  launch_bbox_final(s, c->partial.as<float>(), nb, cd->quant.as<float>());
+  HIP_TRY(c->keys_tmp.ensure(sizeof(unsigned long long) * n));
+  HIP_TRY(c->vals_tmp.ensure(sizeof(int) * n));
+  HIP_TRY(cd->keys.ensure(sizeof(unsigned long long) * n));
+  HIP_TRY(cd->perm.ensure(sizeof(int) * n));
+  launch_morton(s, c->raw_pts.as<float4>(), N, cd->quant.as<float>(), c->keys_tmp.as<unsigned long long>(),
+                c->vals_tmp.as<int>());
+  size_t tmp_bytes = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, c->keys_tmp.as<unsigned long long>(),
+                                             cd->keys.as<unsigned long long>(), c->vals_tmp.as<int>(),
+                                             cd->perm.as<int>(), N, 0, 63, s));
+  HIP_TRY(c->sort_tmp.ensure(tmp_bytes));
+  tmp_bytes = c->sort_tmp.bytes;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp_bytes, c->keys_tmp.as<unsigned long long>(),
+                                             cd->keys.as<unsigned long long>(), c->vals_tmp.as<int>(),
+                                             cd->perm.as<int>(), N, 0, 63, s));
+  const int npad = cd->lvl_cnt[0] * kLeafSize;  // whole leaves, sentinel-padded
+  HIP_TRY(cd->pts.ensure(sizeof(float4) * npad));
+  HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
+  launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
+  HIP_TRY(cd->dir.ensure(sizeof(int) * ((1u << kDirBits) + 1)));
+  launch_key_dir(s, cd->keys.as<unsigned long long>(), N, cd->dir.as<int>());
+  HIP_TRY(cd->soa.ensure(sizeof(float) * 3 * (size_t)npad));
+  launch_leaf_soa(s, cd->pts.as<float4>(), npad, cd->soa.as<float>());
+  HIP_TRY(cd->box_lo.ensure(sizeof(float4) * total_boxes));
+  HIP_TRY(cd->box_hi.ensure(sizeof(float4) * total_boxes));
+  launch_leaf_boxes(s, cd->pts.as<float4>(), N, cd->lvl_cnt[0], cd->box_lo.as<float4>(), cd->box_hi.as<float4>());
+  for (int l = 1; l < cd->nlevels; ++l)
+    launch_level_boxes(s, cd->box_lo.as<float4>() + cd->lvl_off[l - 1], cd->box_hi.as<float4>() + cd->lvl_off[l - 1],
+                       cd->lvl_cnt[l - 1], cd->lvl_cnt[l], cd->box_lo.as<float4>() + cd->lvl_off[l],
+                       cd->box_hi.as<float4>() + cd->lvl_off[l]);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(c->flag_host, c->nonfinite.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (*c->flag_host) return fail(GICP_ENONFINITE, "cloud contains non-finite coordinates");
+  *out = cd;
+  return GICP_OK;
+}
+
+inline gicp_status compute_cov(gicp_ctx* c, Side& side) {
+  if (!side.cloud) return fail(GICP_ESTATE, "no cloud on this side");
+  const int k = c->params.k_correspondences;
+  if (k <= 0 || k > 64) return fail(GICP_EINVAL, "k_correspondences must be in [1, 64]");
+  if (side.cloud->n < k) return fail(GICP_ETOOFEW, "cloud has fewer points than k_correspondences");
+  auto cv = std::make_shared<CovData>();
+  cv->n = side.cloud->n;
+  HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * (size_t)cv->n));
+  if (!launch_covariances(c->stream, side.cloud->dev(), k, c->params.regularization, cv->cov6.as<double>()))
+    return fail(GICP_EINVAL, "unsupported k");
+  HIP_TRY(hipGetLastError());
+  side.cov = cv;
+  return GICP_OK;
+}
+
+inline void invalidate_align(gicp_ctx* c) { c->have_align = false; }
+
+}  // namespace rt
+}  // namespace ddlo

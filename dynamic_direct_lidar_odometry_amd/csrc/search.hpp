@@ -116,6 +116,15 @@ __device__ __forceinline__ unsigned long long morton_key(float x, float y, float
          (spread21(quant21(z, quant[2], quant[3])) << 2);
 }
 
+// Key directory of a sorted cloud: dir[p] = first sorted position whose
+// Morton key has top kDirBits bits >= p (p = 0 .. 2^kDirBits), so the
+// lower_bound of any key lies in [dir[p], dir[p + 1]] for its prefix p.
+__device__ __forceinline__ void dir_range(const int* dir, unsigned long long key, int& lo, int& hi) {
+  const unsigned p = (unsigned)(key >> (63 - kDirBits));
+  lo = gp(dir)[p];
+  hi = gp(dir)[p + 1];
+}
+
 // Wave-parallel lower_bound of a (uniform) key in the sorted key array:
 // 64 pivots per step, 4 dependent loads for 500k keys instead of 19.
 __device__ __forceinline__ int wave_lower_bound(const unsigned long long* keys, int n, unsigned long long key) {
@@ -153,11 +162,12 @@ __device__ __forceinline__ int wave_lower_bound_lane(const unsigned long long* k
 // Per-query lower_bound for Q-query groups: the S = 64/Q lanes of a query
 // test S pivots per step ((S+1)-ary search), ~log_{S+1}(n) dependent loads.
 template <int Q>
-__device__ __forceinline__ int group_lower_bound(const unsigned long long* keys, int n, unsigned long long key) {
+__device__ __forceinline__ int group_lower_bound(const unsigned long long* keys, int n, unsigned long long key,
+                                                 int lo0 = 0, int hi0 = -1) {
   constexpr int S = 64 / Q;
   const int lane = lane_id();
   const int s = lane / Q, qi = lane % Q;
-  int lo = 0, hi = n;  // answer in [lo, hi]
+  int lo = lo0, hi = hi0 < 0 ? n : hi0;  // answer in [lo, hi]
   while (__any(hi - lo > 0)) {
     const int len = hi - lo;
     // pivots lo + (t+1)*len/(S+1), t = 0..S-1
