@@ -8,7 +8,7 @@ PKG := dynamic_direct_lidar_odometry_amd
 CSRC := $(PKG)/csrc
 LIBDIR := $(PKG)/_lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
-OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/capi.o
+OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o
 
 all: lib oracle facade
 
@@ -19,6 +19,14 @@ $(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/search.hpp $(CSRC)/nn_tasks.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/runtime.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/preprocess.o: $(CSRC)/preprocess.hip $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/odom.o: $(CSRC)/odom.hip $(CSRC)/runtime.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h include/ddlo_odom.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

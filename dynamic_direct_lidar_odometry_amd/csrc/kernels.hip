@@ -759,7 +759,6 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     const float4 a = ldg4(src.pts, ic);
     const int jprev = have_prev ? corr[ic] : -1;
     const float sqprev = have_prev ? sqd[ic] : 0.f;
-    const unsigned long long skey = gp(src.keys)[ic];
     // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
@@ -837,7 +836,6 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     // and no key search is needed); the window contains the previous match.
     const bool need_seed = active && ((!seeded && !large_step) || rewindow);
     const bool use_window = need_seed || large_step;
-    bool again = false;
     if (__any(use_window)) {
       // Morton window of kSeedW points per slice lane (64/Q * kSeedW per query)
       int pos = large_step ? jprev : 0;
@@ -870,7 +868,6 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
           have_bp = false;   // the winning window point may sit in another slice lane
         }
       }
-      again = need_seed;
     }
     // Group sharing: every query also takes the exact distance to the other
     // queries' candidate points (Morton-adjacent queries are spatially

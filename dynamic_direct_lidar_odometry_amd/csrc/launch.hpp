@@ -38,4 +38,19 @@ void launch_transform(hipStream_t s, const float4* pts, int n, const int* perm, 
                       size_t stride_floats);
 void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr, float* sqd);
 
+// preprocess.hip (odometry driver): see the kernels there for the reference
+// filters they restate.  Scratch sizes: *_tmp_bytes (hipcub temporaries).
+void launch_pack4(hipStream_t s, const unsigned char* raw, size_t stride, int n, float4* out);
+int crop_box(hipStream_t s, const float4* in, int n, float size, float4* out, int* keep, int* pos, void* tmp,
+             size_t tmp_bytes, int* count_host);
+size_t crop_box_tmp_bytes(int n);
+int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, int* scratch, void* tmp, size_t tmp_bytes,
+               int* count_host);
+size_t voxel_tmp_bytes(int n);
+constexpr size_t voxel_scratch_ints(int n) { return 7 * (size_t)n + 16 + 6 * 64; }
+float median_range(hipStream_t s, const float4* in, int n, float* d, float* d_sorted, void* tmp, size_t tmp_bytes);
+size_t median_tmp_bytes(int n);
+void launch_transform4(hipStream_t s, const float4* pts, const int* perm, int n, const float* T12, float4* out);
+void launch_gather_cov6(hipStream_t s, const double* cov_sorted, const int* perm, int n, double* out);
+
 }  // namespace ddlo

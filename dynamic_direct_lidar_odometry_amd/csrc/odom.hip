@@ -1,0 +1,807 @@
+// odom.hip — odometry driver around the GICP core (include/ddlo_odom.h;
+// SURVEY.md §8(f) rank 1, device voxel filter = rank 3).
+//
+// Restates the registration half of OdomNode (reference
+// dynamic_direct_lidar_odometry/src/odometry/odom.cc) with every point set
+// on the device:
+//   icpCB                 :614-729   process()
+//   preprocessPoints      :442-478   crop box + voxel filter (preprocess.hip)
+//   computeSpaciousness   :981-1001  device ranges + sort, host low-pass
+//   setAdaptiveParams     :1156-1178
+//   initializeInputTarget :480-516
+//   setInputSources       :518-532   one device cloud shared by S2S and S2M
+//   scanMatching          :745-851   S2S, propagateS2S, cov reuse, swap,
+//                                    getSubmapKeyframes, S2M, propagateS2M
+//   transformScans        :941-947   device transform to the world frame
+//   updateKeyframes       :1067-1154 keyframe decision; the keyframe cloud
+//                                    (submap voxel filter) and its k-NN
+//                                    covariances stay on the device
+//   getSubmapKeyframes    :1215-1315 k nearest + convex-hull + concave-hull
+//                                    keyframes; the submap cloud is the
+//                                    device concatenation of the keyframes'
+//                                    points and covariances (no host copies)
+// Deliberate differences, all where the reference reads unsynchronised or
+// out-of-range data: the spaciousness metric is computed before the
+// adaptive threshold reads it (the reference starts it on a detached thread
+// right before, :656-660) and over the scan's n points (its loop reads one
+// past the end, :986).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <queue>
+#include <vector>
+
+#include "../../include/ddlo_gicp.h"
+#include "../../include/ddlo_odom.h"
+#include "gicp_types.hpp"
+#include "launch.hpp"
+#include "runtime.hpp"
+
+namespace {
+
+using namespace ddlo;
+using namespace ddlo::rt;
+
+// ---- small host math (float like the reference's Matrix4f / Quaternionf) ----
+void mat4_identity(float* T) {
+  for (int i = 0; i < 16; ++i) T[i] = (i % 5 == 0) ? 1.f : 0.f;
+}
+void mat4_mul(const float* A, const float* B, float* C) {  // C = A * B, row-major
+  float R[16];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c)
+      R[4 * r + c] = ((A[4 * r] * B[c] + A[4 * r + 1] * B[4 + c]) + A[4 * r + 2] * B[8 + c]) + A[4 * r + 3] * B[12 + c];
+  std::memcpy(C, R, sizeof(R));
+}
+
+struct Quatf {
+  float x = 0.f, y = 0.f, z = 0.f, w = 1.f;
+};
+
+// Eigen::Quaternionf(const Matrix3f&) (quaternionbase_assign_impl), then the
+// normalisation of propagateS2M (odom.cc:928-937: double norm, float /=)
+Quatf quat_from_R(const float* T) {
+  auto m = [&](int r, int c) { return T[4 * r + c]; };
+  Quatf q;
+  float t = m(0, 0) + m(1, 1) + m(2, 2);
+  if (t > 0.f) {
+    t = std::sqrt(t + 1.0f);
+    q.w = 0.5f * t;
+    t = 0.5f / t;
+    q.x = (m(2, 1) - m(1, 2)) * t;
+    q.y = (m(0, 2) - m(2, 0)) * t;
+    q.z = (m(1, 0) - m(0, 1)) * t;
+  } else {
+    int i = 0;
+    if (m(1, 1) > m(0, 0)) i = 1;
+    if (m(2, 2) > m(i, i)) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = std::sqrt(m(i, i) - m(j, j) - m(k, k) + 1.0f);
+    float c[3];
+    c[i] = 0.5f * t;
+    t = 0.5f / t;
+    q.w = (m(k, j) - m(j, k)) * t;
+    c[j] = (m(j, i) + m(i, j)) * t;
+    c[k] = (m(k, i) + m(i, k)) * t;
+    q.x = c[0];
+    q.y = c[1];
+    q.z = c[2];
+  }
+  const double norm = std::sqrt(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  q.w = (float)(q.w / norm);
+  q.x = (float)(q.x / norm);
+  q.y = (float)(q.y / norm);
+  q.z = (float)(q.z / norm);
+  return q;
+}
+
+Quatf quat_mul(const Quatf& a, const Quatf& b) {
+  Quatf r;
+  r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+  r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+  r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+  r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+  return r;
+}
+Quatf quat_inverse(const Quatf& q) {  // Eigen: conjugate / squaredNorm
+  const float n2 = q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z;
+  Quatf r;
+  r.w = q.w / n2;
+  r.x = -q.x / n2;
+  r.y = -q.y / n2;
+  r.z = -q.z / n2;
+  return r;
+}
+
+// ---- hulls over the keyframe positions (computeConvexHull / computeConcaveHull) ----
+// pcl::ConvexHull / ConcaveHull pick the dimension from the covariance of the
+// input (calculateInputDimension): planar (2) when the smallest eigenvalue is
+// ~0 or below 1e-3 of the largest, else 3.
+void sym_eig3(const double* A, double* lam, double* V) {  // Jacobi; V columns = eigenvectors
+  double a[9];
+  std::memcpy(a, A, sizeof(a));
+  for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    const double off = a[1] * a[1] + a[2] * a[2] + a[5] * a[5];
+    if (off < 1e-300) break;
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        const double apq = a[3 * p + q];
+        if (std::fabs(apq) < 1e-300) continue;
+        const double theta = (a[3 * q + q] - a[3 * p + p]) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < 3; ++k) {  // A <- J^T A J
+          const double akp = a[3 * k + p], akq = a[3 * k + q];
+          a[3 * k + p] = c * akp - s * akq;
+          a[3 * k + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double apk = a[3 * p + k], aqk = a[3 * q + k];
+          a[3 * p + k] = c * apk - s * aqk;
+          a[3 * q + k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double vkp = V[3 * k + p], vkq = V[3 * k + q];
+          V[3 * k + p] = c * vkp - s * vkq;
+          V[3 * k + q] = s * vkp + c * vkq;
+        }
+      }
+  }
+  for (int i = 0; i < 3; ++i) lam[i] = a[4 * i];
+}
+
+// returns the dimension; u, v: the in-plane orthonormal basis (2D case)
+int hull_frame(const float* xyz, int n, double* c, double* u, double* v) {
+  c[0] = c[1] = c[2] = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a) c[a] += xyz[3 * i + a];
+  for (int a = 0; a < 3; ++a) c[a] /= n;
+  double C[9] = {0};
+  for (int i = 0; i < n; ++i) {
+    const double d[3] = {xyz[3 * i] - c[0], xyz[3 * i + 1] - c[1], xyz[3 * i + 2] - c[2]};
+    for (int r = 0; r < 3; ++r)
+      for (int q = 0; q < 3; ++q) C[3 * r + q] += d[r] * d[q];
+  }
+  for (int e = 0; e < 9; ++e) C[e] /= n;
+  double lam[3], V[9];
+  sym_eig3(C, lam, V);
+  int ord[3] = {0, 1, 2};
+  std::sort(ord, ord + 3, [&](int a, int b) { return lam[a] < lam[b]; });
+  for (int a = 0; a < 3; ++a) {
+    u[a] = V[3 * a + ord[2]];
+    v[a] = V[3 * a + ord[1]];
+  }
+  const double l0 = lam[ord[0]], l2 = lam[ord[2]];
+  return (std::fabs(l0) < DBL_EPSILON || std::fabs(l0 / l2) < 1.0e-3) ? 2 : 3;
+}
+
+double cross2(const double* o, const double* a, const double* b) {
+  return (a[0] - o[0]) * (b[1] - o[1]) - (a[1] - o[1]) * (b[0] - o[0]);
+}
+
+// vertex set of the convex hull (collinear / coplanar boundary points are not
+// vertices, as qhull reports them)
+std::vector<int> convex_hull(const float* xyz, int n) {
+  std::vector<int> out;
+  if (n <= 0) return out;
+  if (n <= 2) {
+    for (int i = 0; i < n; ++i) out.push_back(i);
+    return out;
+  }
+  double c[3], u[3], v[3];
+  const int dim = hull_frame(xyz, n, c, u, v);
+  if (dim == 2) {
+    std::vector<std::array<double, 3>> p(n);  // (s, t, index)
+    for (int i = 0; i < n; ++i) {
+      const double d[3] = {xyz[3 * i] - c[0], xyz[3 * i + 1] - c[1], xyz[3 * i + 2] - c[2]};
+      p[i] = {d[0] * u[0] + d[1] * u[1] + d[2] * u[2], d[0] * v[0] + d[1] * v[1] + d[2] * v[2], (double)i};
+    }
+    std::sort(p.begin(), p.end());
+    std::vector<std::array<double, 3>> h(2 * n);
+    int k = 0;
+    for (int i = 0; i < n; ++i) {  // Andrew's monotone chain, strict turns
+      while (k >= 2 && cross2(h[k - 2].data(), h[k - 1].data(), p[i].data()) <= 0) --k;
+      h[k++] = p[i];
+    }
+    for (int i = n - 2, t = k + 1; i >= 0; --i) {
+      while (k >= t && cross2(h[k - 2].data(), h[k - 1].data(), p[i].data()) <= 0) --k;
+      h[k++] = p[i];
+    }
+    for (int i = 0; i < k - 1; ++i) out.push_back((int)h[i][2]);
+  } else {
+    // 3D: incremental hull; a point is a vertex of the final hull if it
+    // remains on a facet
+    struct F {
+      int a, b, c;
+      double n[3], d;
+      bool alive;
+    };
+    auto P = [&](int i) { return std::array<double, 3>{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]}; };
+    auto make = [&](int a, int b, int cc) {
+      const auto A = P(a), B = P(b), Cc = P(cc);
+      const double e1[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, e2[3] = {Cc[0] - A[0], Cc[1] - A[1], Cc[2] - A[2]};
+      F f{a, b, cc, {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]}, 0, true};
+      f.d = f.n[0] * A[0] + f.n[1] * A[1] + f.n[2] * A[2];
+      return f;
+    };
+    double scale = 0;
+    for (int i = 0; i < 3 * n; ++i) scale = std::max(scale, (double)std::fabs(xyz[i]));
+    const double eps = 1e-9 * std::max(1.0, scale * scale);
+    // initial tetrahedron: farthest-apart picks
+    int i0 = 0, i1 = -1, i2 = -1, i3 = -1;
+    double best = -1;
+    for (int i = 1; i < n; ++i) {
+      const auto a = P(i0), b = P(i);
+      const double d = (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+      if (d > best) { best = d; i1 = i; }
+    }
+    best = -1;
+    for (int i = 0; i < n; ++i) {
+      if (i == i0 || i == i1) continue;
+      const F f = make(i0, i1, i);
+      const double a2 = f.n[0] * f.n[0] + f.n[1] * f.n[1] + f.n[2] * f.n[2];
+      if (a2 > best) { best = a2; i2 = i; }
+    }
+    best = -1;
+    const F base = make(i0, i1, i2);
+    for (int i = 0; i < n; ++i) {
+      if (i == i0 || i == i1 || i == i2) continue;
+      const auto p = P(i);
+      const double s = std::fabs(base.n[0] * p[0] + base.n[1] * p[1] + base.n[2] * p[2] - base.d);
+      if (s > best) { best = s; i3 = i; }
+    }
+    std::vector<F> fs;
+    auto add_oriented = [&](int a, int b, int cc, int inside) {
+      F f = make(a, b, cc);
+      const auto q = P(inside);
+      if (f.n[0] * q[0] + f.n[1] * q[1] + f.n[2] * q[2] - f.d > 0) f = make(a, cc, b);
+      fs.push_back(f);
+    };
+    add_oriented(i0, i1, i2, i3);
+    add_oriented(i0, i1, i3, i2);
+    add_oriented(i0, i2, i3, i1);
+    add_oriented(i1, i2, i3, i0);
+    for (int i = 0; i < n; ++i) {
+      if (i == i0 || i == i1 || i == i2 || i == i3) continue;
+      const auto p = P(i);
+      std::vector<std::pair<int, int>> edges;
+      bool any = false;
+      for (auto& f : fs) {
+        if (!f.alive) continue;
+        if (f.n[0] * p[0] + f.n[1] * p[1] + f.n[2] * p[2] - f.d > eps) {
+          f.alive = false;
+          any = true;
+          edges.push_back({f.a, f.b});
+          edges.push_back({f.b, f.c});
+          edges.push_back({f.c, f.a});
+        }
+      }
+      if (!any) continue;
+      // horizon: directed edges whose reverse was not removed
+      for (const auto& e : edges) {
+        bool twin = false;
+        for (const auto& g : edges)
+          if (g.first == e.second && g.second == e.first) { twin = true; break; }
+        if (!twin) fs.push_back(make(e.first, e.second, i));
+      }
+    }
+    std::vector<char> on(n, 0);
+    for (const auto& f : fs)
+      if (f.alive) on[f.a] = on[f.b] = on[f.c] = 1;
+    for (int i = 0; i < n; ++i)
+      if (on[i]) out.push_back(i);
+  }
+  std::sort(out.begin(), out.end());
+  out.erase(std::unique(out.begin(), out.end()), out.end());
+  return out;
+}
+
+// Vertex set of the concave hull (pcl::ConcaveHull, alpha).  Its planar
+// branch keeps every edge of a Delaunay triangle whose circumradius is
+// <= alpha and every other Delaunay edge of half-length <= alpha; an edge of
+// a triangle is never longer than the circumcircle's diameter, so the kept
+// edges are exactly the Delaunay edges of length <= 2 alpha, and a point is
+// a vertex iff its shortest Delaunay edge — the one to its nearest neighbour
+// — is that short.  (Parity unpinned: PCL is not in this image; the 3D
+// branch, for non-planar keyframe sets, is restated with the same criterion.)
+std::vector<int> concave_hull(const float* xyz, int n, double alpha) {
+  std::vector<int> out;
+  for (int i = 0; i < n; ++i) {
+    double nn = INFINITY;
+    for (int j = 0; j < n; ++j) {
+      if (j == i) continue;
+      const double dx = (double)xyz[3 * i] - xyz[3 * j], dy = (double)xyz[3 * i + 1] - xyz[3 * j + 1],
+                   dz = (double)xyz[3 * i + 2] - xyz[3 * j + 2];
+      nn = std::min(nn, std::sqrt(dx * dx + dy * dy + dz * dz));
+    }
+    if (nn / 2 <= alpha) out.push_back(i);
+  }
+  return out;
+}
+
+// OdomNode::pushSubmapIndices (odom.cc:1180-1213): the k smallest distances
+// (max-heap of at most k), then every frame at or below the k-th
+void push_submap_indices(const std::vector<float>& dists, int k, const std::vector<int>& frames, std::vector<int>& out) {
+  if (dists.empty()) return;
+  std::priority_queue<float> pq;
+  for (float d : dists) {
+    if ((int)pq.size() >= k && pq.top() > d) {
+      pq.push(d);
+      pq.pop();
+    } else if ((int)pq.size() < k) {
+      pq.push(d);
+    }
+  }
+  const float kth = pq.top();
+  for (size_t i = 0; i < dists.size(); ++i)
+    if (dists[i] <= kth) out.push_back(frames[i]);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+struct Keyframe {
+  float pose[3];
+  Quatf q;
+  int n = 0;
+  DevBuf pts;   // float4, world frame, original order (after the submap voxel filter)
+  DevBuf cov;   // sym6 doubles, original order
+};
+
+struct ddlo_odom {
+  int device = 0;
+  ddlo_odom_params p{};
+  gicp_ctx* s2s = nullptr;
+  gicp_ctx* s2m = nullptr;
+  hipStream_t s = nullptr;
+  // scratch (device)
+  DevBuf up, a, b, keep, pos, vscratch, cubtmp, rng, rng_sorted, cat_pts, cat_cov;
+  // state
+  bool have_target = false;
+  float T[16], T_s2s[16], T_s2s_prev[16];
+  float pose[3] = {0.f, 0.f, 0.f};
+  Quatf rotq;
+  std::vector<std::unique_ptr<Keyframe>> keyframes;
+  std::vector<int> submap_prev, keyframe_convex, keyframe_concave;
+  bool have_median = false;
+  float median_prev = 0.f;
+  double thresh_dist = 1.0;
+  int64_t submap_points = 0;
+};
+
+namespace {
+
+gicp_status ensure_tmp(ddlo_odom* o, int n) {
+  const size_t t = std::max({crop_box_tmp_bytes(n), voxel_tmp_bytes(n), median_tmp_bytes(n)});
+  HIP_TRY(o->cubtmp.ensure(t));
+  return GICP_OK;
+}
+
+// crop box + voxel filter of the float4 points in o->a (n) -> o->a; returns count
+gicp_status preprocess(ddlo_odom* o, int n, bool crop, double crop_size, bool vox, double leaf, int* nout) {
+  HIP_TRY(o->b.ensure(sizeof(float4) * (size_t)std::max(n, 1)));
+  HIP_TRY(o->keep.ensure(sizeof(int) * (size_t)std::max(n, 1)));
+  HIP_TRY(o->pos.ensure(sizeof(int) * (size_t)std::max(n, 1)));
+  HIP_TRY(o->vscratch.ensure(sizeof(int) * voxel_scratch_ints(std::max(n, 1))));
+  gicp_status st = ensure_tmp(o, std::max(n, 1));
+  if (st) return st;
+  int m = n;
+  if (crop && m > 0) {
+    if (crop_box(o->s, o->a.as<float4>(), m, (float)crop_size, o->b.as<float4>(), o->keep.as<int>(), o->pos.as<int>(),
+                 o->cubtmp.p, o->cubtmp.bytes, &m))
+      return fail(GICP_EHIP, "crop box scratch too small");
+    std::swap(o->a.p, o->b.p);
+    std::swap(o->a.bytes, o->b.bytes);
+  }
+  if (vox && m > 0) {
+    int c = 0;
+    if (voxel_grid(o->s, o->a.as<float4>(), m, (float)leaf, o->b.as<float4>(), o->vscratch.as<int>(), o->cubtmp.p,
+                   o->cubtmp.bytes, &c))
+      return fail(GICP_EHIP, "voxel filter scratch too small");
+    if (c >= 0) {  // -1: grid overflow, the reference keeps the cloud unchanged
+      m = c;
+      std::swap(o->a.p, o->b.p);
+      std::swap(o->a.bytes, o->b.bytes);
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  *nout = m;
+  return GICP_OK;
+}
+
+// device cloud from float4 points
+gicp_status cloud_from(ddlo_odom* o, gicp_ctx* c, const float4* pts, int n, std::shared_ptr<CloudData>* out) {
+  (void)o;
+  return build_cloud(c, reinterpret_cast<const float*>(pts), (size_t)n, sizeof(float4), out, true);
+}
+
+// keyframe = world-frame copy of the (preprocessed) scan cloud, submap voxel
+// filter, k-NN covariances with the S2S parameters (odom.cc:1129-1149)
+gicp_status make_keyframe(ddlo_odom* o, const std::shared_ptr<CloudData>& scan) {
+  auto kf = std::make_unique<Keyframe>();
+  kf->pose[0] = o->pose[0];
+  kf->pose[1] = o->pose[1];
+  kf->pose[2] = o->pose[2];
+  kf->q = o->rotq;
+  const int n = scan->n;
+  HIP_TRY(o->a.ensure(sizeof(float4) * (size_t)n));
+  launch_transform4(o->s, scan->pts.as<float4>(), scan->perm.as<int>(), n, o->T, o->a.as<float4>());
+  int m = n;
+  gicp_status st = preprocess(o, n, false, 0.0, o->p.vf_submap_use != 0, o->p.vf_submap_res, &m);
+  if (st) return st;
+  if (m < o->p.s2s.k_correspondences) return fail(GICP_ETOOFEW, "keyframe has fewer points than k_correspondences");
+  kf->n = m;
+  HIP_TRY(kf->pts.ensure(sizeof(float4) * (size_t)m));
+  HIP_TRY(hipMemcpyAsync(kf->pts.p, o->a.p, sizeof(float4) * (size_t)m, hipMemcpyDeviceToDevice, o->s));
+  Side side;
+  st = cloud_from(o, o->s2s, kf->pts.as<float4>(), m, &side.cloud);
+  if (st) return st;
+  st = compute_cov(o->s2s, side);   // s2s->params: the S2S k (gicp_s2s_.calculateSourceCovariances)
+  if (st) return st;
+  HIP_TRY(kf->cov.ensure(sizeof(double) * 6 * (size_t)m));
+  launch_gather_cov6(o->s, side.cov->cov6.as<double>(), side.cloud->perm.as<int>(), m, kf->cov.as<double>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(o->s));
+  o->keyframes.push_back(std::move(kf));
+  return GICP_OK;
+}
+
+// OdomNode::getSubmapKeyframes (odom.cc:1215-1315); returns whether it changed
+gicp_status submap_keyframes(ddlo_odom* o, bool* changed) {
+  const int nk = (int)o->keyframes.size();
+  std::vector<int> cur;
+  std::vector<float> ds;
+  std::vector<int> nn;
+  const float cx = o->T_s2s[3], cy = o->T_s2s[7], cz = o->T_s2s[11];
+  for (int i = 0; i < nk; ++i) {
+    const float* k = o->keyframes[i]->pose;
+    ds.push_back((float)std::sqrt(std::pow(cx - k[0], 2) + std::pow(cy - k[1], 2) + std::pow(cz - k[2], 2)));
+    nn.push_back(i);
+  }
+  push_submap_indices(ds, o->p.submap_knn, nn, cur);
+  std::vector<float> kpos(3 * (size_t)nk);
+  for (int i = 0; i < nk; ++i)
+    for (int a = 0; a < 3; ++a) kpos[3 * i + a] = o->keyframes[i]->pose[a];
+  if (nk >= 4) o->keyframe_convex = convex_hull(kpos.data(), nk);  // computeConvexHull: >= 4 keyframes
+  std::vector<float> cds;
+  for (int c : o->keyframe_convex) cds.push_back(ds[c]);
+  push_submap_indices(cds, o->p.submap_kcv, o->keyframe_convex, cur);
+  if (nk >= 5) o->keyframe_concave = concave_hull(kpos.data(), nk, o->thresh_dist);  // >= 5 keyframes
+  std::vector<float> kds;
+  for (int c : o->keyframe_concave) kds.push_back(ds[c]);
+  push_submap_indices(kds, o->p.submap_kcc, o->keyframe_concave, cur);
+  std::sort(cur.begin(), cur.end());
+  cur.erase(std::unique(cur.begin(), cur.end()), cur.end());
+  *changed = cur != o->submap_prev;
+  if (!*changed) return GICP_OK;
+  // submap cloud + normals: the selected keyframes concatenated in index
+  // order, all on the device
+  int64_t total = 0;
+  for (int k : cur) total += o->keyframes[k]->n;
+  if (total > INT32_MAX / 2) return fail(GICP_EINVAL, "submap too large");
+  HIP_TRY(o->cat_pts.ensure(sizeof(float4) * (size_t)total));
+  HIP_TRY(o->cat_cov.ensure(sizeof(double) * 6 * (size_t)total));
+  int64_t off = 0;
+  for (int k : cur) {
+    const Keyframe& kf = *o->keyframes[k];
+    HIP_TRY(hipMemcpyAsync(o->cat_pts.as<float4>() + off, kf.pts.p, sizeof(float4) * kf.n, hipMemcpyDeviceToDevice, o->s));
+    HIP_TRY(hipMemcpyAsync(o->cat_cov.as<double>() + 6 * off, kf.cov.p, sizeof(double) * 6 * kf.n,
+                           hipMemcpyDeviceToDevice, o->s));
+    off += kf.n;
+  }
+  Side tgt;
+  gicp_status st = cloud_from(o, o->s2m, o->cat_pts.as<float4>(), (int)total, &tgt.cloud);
+  if (st) return st;
+  auto cv = std::make_shared<CovData>();
+  cv->n = (int)total;
+  HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * (size_t)total));
+  launch_cov_import(o->s, o->cat_cov.as<double>(), GICP_COV_SYM6, (int)total, tgt.cloud->inv_perm.as<int>(),
+                    cv->cov6.as<double>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(o->s));
+  tgt.cov = cv;
+  o->s2m->tgt = tgt;        // setInputTarget + setTargetCovariances (odom.cc:780-783)
+  invalidate_align(o->s2m);
+  o->submap_prev = cur;
+  o->submap_points = total;
+  return GICP_OK;
+}
+
+void copy_pose(const float* T, float* out) { std::memcpy(out, T, sizeof(float) * 16); }
+
+}  // namespace
+
+extern "C" {
+
+gicp_status ddlo_odom_default_params(ddlo_odom_params* p) {
+  if (!p) return fail(GICP_EINVAL, "null params");
+  std::memset(p, 0, sizeof(*p));
+  gicp_default_params(&p->s2s);
+  gicp_default_params(&p->s2m);
+  // cfg/ddlo.yaml:185-204
+  p->s2s.k_correspondences = 10;
+  p->s2s.max_correspondence_distance = 1.0;
+  p->s2s.max_iterations = 32;
+  p->s2s.transformation_epsilon = 0.01;
+  p->s2m.k_correspondences = 20;
+  p->s2m.max_correspondence_distance = 2.0;
+  p->s2m.max_iterations = 32;
+  p->s2m.transformation_epsilon = 0.01;
+  p->min_num_points = 10;
+  p->keyframe_thresh_dist = 1.0;
+  p->keyframe_thresh_rot = 0.1;
+  p->submap_knn = p->submap_kcv = p->submap_kcc = 10;
+  p->adaptive = 1;
+  p->crop_use = 1;
+  p->crop_size = 1.0;
+  p->vf_scan_use = 1;
+  p->vf_scan_res = 0.1;
+  p->vf_submap_use = 1;
+  p->vf_submap_res = 0.1;
+  return GICP_OK;
+}
+
+gicp_status ddlo_odom_create(int device, const ddlo_odom_params* p, ddlo_odom** out) {
+  if (!out) return fail(GICP_EINVAL, "null out");
+  *out = nullptr;
+  auto o = std::make_unique<ddlo_odom>();
+  if (p) {
+    o->p = *p;
+  } else {
+    ddlo_odom_default_params(&o->p);
+  }
+  if (o->p.submap_knn < 1 || o->p.submap_kcv < 1 || o->p.submap_kcc < 1) return fail(GICP_EINVAL, "submap k must be >= 1");
+  if ((o->p.vf_scan_use && !(o->p.vf_scan_res > 0)) || (o->p.vf_submap_use && !(o->p.vf_submap_res > 0)))
+    return fail(GICP_EINVAL, "voxel resolution must be positive");
+  o->device = device;
+  gicp_status st = gicp_ctx_create(device, &o->s2s);
+  if (!st) st = gicp_ctx_create(device, &o->s2m);
+  if (!st) st = gicp_set_params(o->s2s, &o->p.s2s);
+  if (!st) st = gicp_set_params(o->s2m, &o->p.s2m);
+  if (st) {
+    if (o->s2s) gicp_ctx_destroy(o->s2s);
+    if (o->s2m) gicp_ctx_destroy(o->s2m);
+    return st;
+  }
+  o->s = o->s2s->stream;  // one stream: the driver's work is one dependent chain
+  mat4_identity(o->T);
+  mat4_identity(o->T_s2s);
+  mat4_identity(o->T_s2s_prev);
+  o->thresh_dist = o->p.keyframe_thresh_dist;
+  *out = o.release();
+  return GICP_OK;
+}
+
+gicp_status ddlo_odom_destroy(ddlo_odom* o) {
+  if (!o) return GICP_OK;
+  (void)hipSetDevice(o->device);
+  (void)hipStreamSynchronize(o->s2m->stream);
+  (void)hipStreamSynchronize(o->s);
+  o->keyframes.clear();
+  gicp_ctx_destroy(o->s2m);
+  gicp_ctx_destroy(o->s2s);
+  delete o;
+  return GICP_OK;
+}
+
+gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t stride, ddlo_odom_result* res) {
+  if (!o || !res || (!xyz && n) || stride < 12 || stride % 4) return fail(GICP_EINVAL, "invalid argument");
+  if (n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "scan too large");
+  gicp_status st = set_device(o->s2s);
+  if (st) return st;
+  std::memset(res, 0, sizeof(*res));
+  copy_pose(o->T, res->T);
+  copy_pose(o->T_s2s, res->T_s2s);
+  mat4_identity(res->T_s2s_local);
+  res->num_keyframes = (int)o->keyframes.size();
+  // icpCB: too few points -> return (odom.cc:635-639)
+  if ((int64_t)n < o->p.min_num_points) {
+    res->status = DDLO_ODOM_SKIPPED;
+    return GICP_OK;
+  }
+  // upload + preprocessPoints (odom.cc:442-478)
+  const int N = (int)n;
+  HIP_TRY(o->up.ensure((n - 1) * stride + 12));
+  HIP_TRY(hipMemcpyAsync(o->up.p, xyz, (n - 1) * stride + 12, hipMemcpyHostToDevice, o->s));
+  HIP_TRY(o->a.ensure(sizeof(float4) * n));
+  launch_pack4(o->s, o->up.as<unsigned char>(), stride, N, o->a.as<float4>());
+  int m = N;
+  st = preprocess(o, N, o->p.crop_use != 0, o->p.crop_size, o->p.vf_scan_use != 0, o->p.vf_scan_res, &m);
+  if (st) return st;
+  res->scan_points = m;
+  // computeSpaciousness (odom.cc:981-1001): median range, low-passed
+  HIP_TRY(o->rng.ensure(sizeof(float) * (size_t)std::max(m, 1)));
+  HIP_TRY(o->rng_sorted.ensure(sizeof(float) * (size_t)std::max(m, 1)));
+  const float median_curr = median_range(o->s, o->a.as<float4>(), m, o->rng.as<float>(), o->rng_sorted.as<float>(),
+                                         o->cubtmp.p, o->cubtmp.bytes);
+  if (!o->have_median) {  // static float median_prev = median_curr (first call)
+    o->median_prev = median_curr;
+    o->have_median = true;
+  }
+  const float median_lpf = (float)(0.95 * o->median_prev + 0.05 * median_curr);
+  o->median_prev = median_lpf;
+  res->spaciousness = median_lpf;
+  // setAdaptiveParams (odom.cc:1156-1178)
+  if (o->p.adaptive) {
+    if (median_lpf > 20.0) o->thresh_dist = 10.0;
+    else if (median_lpf > 10.0 && median_lpf <= 20.0) o->thresh_dist = 5.0;
+    else if (median_lpf > 5.0 && median_lpf <= 10.0) o->thresh_dist = 1.0;
+    else if (median_lpf <= 5.0) o->thresh_dist = 0.5;
+  }
+  res->keyframe_thresh_dist = o->thresh_dist;
+  if (m < std::max(o->p.s2s.k_correspondences, o->p.s2m.k_correspondences))
+    return fail(GICP_ETOOFEW, "preprocessed scan has fewer points than k_correspondences");
+  // the preprocessed scan as a device cloud
+  std::shared_ptr<CloudData> scan;
+  st = cloud_from(o, o->s2s, o->a.as<float4>(), m, &scan);
+  if (st) return st;
+
+  if (!o->have_target) {
+    // initializeInputTarget (odom.cc:480-516)
+    o->s2s->tgt = Side();
+    o->s2s->tgt.cloud = scan;
+    invalidate_align(o->s2s);
+    st = compute_cov(o->s2s, o->s2s->tgt);   // calculateTargetCovariances
+    if (st) return st;
+    st = make_keyframe(o, scan);              // T_ = identity: the scan itself
+    if (st) return st;
+    o->have_target = true;
+    res->status = DDLO_ODOM_FIRST;
+    res->keyframe_added = 1;
+    res->num_keyframes = (int)o->keyframes.size();
+    return GICP_OK;
+  }
+  // setInputSources (odom.cc:518-532): one device cloud for both
+  o->s2s->src = Side();
+  o->s2s->src.cloud = scan;
+  invalidate_align(o->s2s);
+  o->s2m->src = Side();
+  o->s2m->src.cloud = scan;
+  invalidate_align(o->s2m);
+
+  // scanMatching (odom.cc:745-851)
+  float T_S2S[16];
+  st = gicp_align(o->s2s, nullptr, T_S2S, &res->s2s);
+  if (st) return st;
+  copy_pose(T_S2S, res->T_s2s_local);
+  mat4_mul(o->T_s2s_prev, T_S2S, o->T_s2s);   // propagateS2S
+  copy_pose(o->T_s2s, o->T_s2s_prev);
+  o->s2m->src.cov = o->s2s->src.cov;          // gicp_s2m_.source_covs_ = gicp_s2s_.source_covs_
+  gicp_swap_source_target(o->s2s);            // the scan becomes the next S2S target
+  bool changed = false;
+  st = submap_keyframes(o, &changed);
+  if (st) return st;
+  st = gicp_align(o->s2m, o->T_s2s, o->T, &res->s2m);
+  if (st) return st;
+  copy_pose(o->T, o->T_s2s_prev);             // T_s2s_prev_ = T_
+  o->pose[0] = o->T[3];                       // propagateS2M
+  o->pose[1] = o->T[7];
+  o->pose[2] = o->T[11];
+  o->rotq = quat_from_R(o->T);
+
+  // updateKeyframes (odom.cc:1067-1154)
+  {
+    float closest_d = INFINITY;
+    int closest = 0, idx = 0, num_nearby = 0;
+    for (const auto& k : o->keyframes) {
+      const float dd = (float)std::sqrt(std::pow(o->pose[0] - k->pose[0], 2) + std::pow(o->pose[1] - k->pose[1], 2) +
+                                        std::pow(o->pose[2] - k->pose[2], 2));
+      if (dd <= o->thresh_dist * 1.5) ++num_nearby;
+      if (dd < closest_d) {
+        closest_d = dd;
+        closest = idx;
+      }
+      ++idx;
+    }
+    const Keyframe& ck = *o->keyframes[closest];
+    const float dd = (float)std::sqrt(std::pow(o->pose[0] - ck.pose[0], 2) + std::pow(o->pose[1] - ck.pose[1], 2) +
+                                      std::pow(o->pose[2] - ck.pose[2], 2));
+    const Quatf dq = quat_mul(o->rotq, quat_inverse(ck.q));
+    const float theta_rad = (float)(2. * std::atan2(std::sqrt(std::pow(dq.x, 2) + std::pow(dq.y, 2) + std::pow(dq.z, 2)), dq.w));
+    const float theta_deg = (float)(theta_rad * (180.0 / M_PI));
+    bool add = false;
+    if (std::fabs(dd) > o->thresh_dist || std::fabs(theta_deg) > o->p.keyframe_thresh_rot) add = true;
+    if (std::fabs(dd) <= o->thresh_dist) add = false;
+    if (std::fabs(dd) <= o->thresh_dist && std::fabs(theta_deg) > o->p.keyframe_thresh_rot && num_nearby <= 1) add = true;
+    if (add) {
+      st = make_keyframe(o, scan);   // registration_scan_t_ = T_ * scan (transformScans)
+      if (st) return st;
+      res->keyframe_added = 1;
+    }
+  }
+  res->status = DDLO_ODOM_TRACKED;
+  copy_pose(o->T, res->T);
+  copy_pose(o->T_s2s, res->T_s2s);
+  res->submap_changed = changed ? 1 : 0;
+  res->num_keyframes = (int)o->keyframes.size();
+  res->submap_keyframes = (int)o->submap_prev.size();
+  res->submap_points = o->submap_points;
+  return GICP_OK;
+}
+
+gicp_status ddlo_odom_keyframe(const ddlo_odom* o, int k, float pose7[7], size_t* npoints) {
+  if (!o || k < 0 || k >= (int)o->keyframes.size()) return fail(GICP_EINVAL, "invalid keyframe index");
+  const Keyframe& kf = *o->keyframes[k];
+  if (pose7) {
+    pose7[0] = kf.pose[0];
+    pose7[1] = kf.pose[1];
+    pose7[2] = kf.pose[2];
+    pose7[3] = kf.q.x;
+    pose7[4] = kf.q.y;
+    pose7[5] = kf.q.z;
+    pose7[6] = kf.q.w;
+  }
+  if (npoints) *npoints = (size_t)kf.n;
+  return GICP_OK;
+}
+
+gicp_status ddlo_odom_submap(const ddlo_odom* o, int32_t* idx, size_t cap, size_t* n) {
+  if (!o || !n) return fail(GICP_EINVAL, "null argument");
+  *n = o->submap_prev.size();
+  if (idx)
+    for (size_t i = 0; i < std::min(cap, o->submap_prev.size()); ++i) idx[i] = o->submap_prev[i];
+  return GICP_OK;
+}
+
+gicp_status ddlo_odom_ctx(ddlo_odom* o, int which, gicp_ctx** ctx) {
+  if (!o || !ctx || (which != 0 && which != 1)) return fail(GICP_EINVAL, "invalid argument");
+  *ctx = which == 0 ? o->s2s : o->s2m;
+  return GICP_OK;
+}
+
+gicp_status ddlo_preprocess(int device, const float* xyz, size_t n, size_t stride, double crop_size, double leaf,
+                            float* out, size_t cap, size_t* nout) {
+  if ((!xyz && n) || !nout || stride < 12 || stride % 4 || n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "invalid argument");
+  ddlo_odom_params p;
+  ddlo_odom_default_params(&p);
+  ddlo_odom* o = nullptr;
+  gicp_status st = ddlo_odom_create(device, &p, &o);
+  if (st) return st;
+  std::unique_ptr<ddlo_odom, gicp_status (*)(ddlo_odom*)> guard(o, ddlo_odom_destroy);
+  *nout = 0;
+  if (n == 0) return GICP_OK;
+  HIP_TRY(o->up.ensure((n - 1) * stride + 12));
+  HIP_TRY(hipMemcpyAsync(o->up.p, xyz, (n - 1) * stride + 12, hipMemcpyHostToDevice, o->s));
+  HIP_TRY(o->a.ensure(sizeof(float4) * n));
+  launch_pack4(o->s, o->up.as<unsigned char>(), stride, (int)n, o->a.as<float4>());
+  int m = 0;
+  st = preprocess(o, (int)n, crop_size > 0, crop_size, leaf > 0, leaf, &m);
+  if (st) return st;
+  *nout = (size_t)m;
+  if (out && m > 0) {
+    if ((size_t)m > cap) return fail(GICP_EINVAL, "output capacity too small");
+    std::vector<float4> h(m);
+    HIP_TRY(hipMemcpyAsync(h.data(), o->a.p, sizeof(float4) * m, hipMemcpyDeviceToHost, o->s));
+    HIP_TRY(hipStreamSynchronize(o->s));
+    for (int i = 0; i < m; ++i) {
+      out[3 * i] = h[i].x;
+      out[3 * i + 1] = h[i].y;
+      out[3 * i + 2] = h[i].z;
+    }
+  }
+  return GICP_OK;
+}
+
+gicp_status ddlo_convex_hull(const float* xyz, int n, int32_t* idx, int* nidx) {
+  if ((!xyz && n) || !idx || !nidx || n < 0) return fail(GICP_EINVAL, "invalid argument");
+  const std::vector<int> h = convex_hull(xyz, n);
+  for (size_t i = 0; i < h.size(); ++i) idx[i] = h[i];
+  *nidx = (int)h.size();
+  return GICP_OK;
+}
+
+gicp_status ddlo_concave_hull(const float* xyz, int n, double alpha, int32_t* idx, int* nidx) {
+  if ((!xyz && n) || !idx || !nidx || n < 0) return fail(GICP_EINVAL, "invalid argument");
+  const std::vector<int> h = concave_hull(xyz, n, alpha);
+  for (size_t i = 0; i < h.size(); ++i) idx[i] = h[i];
+  *nidx = (int)h.size();
+  return GICP_OK;
+}
+
+}  // extern "C"

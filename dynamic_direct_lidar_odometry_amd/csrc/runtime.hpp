@@ -262,7 +262,10 @@ inline gicp_status set_device(const gicp_ctx* c) {
   return GICP_OK;
 }
 
-inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, std::shared_ptr<CloudData>* out) {
+// xyz: host memory (copied to the device first), or device memory when
+// on_device (e.g. a preprocessed scan or a keyframe of the odometry driver)
+inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, std::shared_ptr<CloudData>* out,
+                               bool on_device = false) {
   if (!xyz || n == 0 || stride < 12 || (stride % 4) != 0) return fail(GICP_EINVAL, "invalid cloud (null, empty or bad stride)");
   if (n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "cloud too large");
   auto cd = std::make_shared<CloudData>();
@@ -275,15 +278,19 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   const int total_boxes = cd->lvl_off[cd->nlevels - 1] + cd->lvl_cnt[cd->nlevels - 1];
   hipStream_t s = c->stream;
   const size_t raw_sz = (n - 1) * stride + 12;
-  HIP_TRY(c->raw_bytes.ensure(raw_sz));
-  HIP_TRY(hipMemcpyAsync(c->raw_bytes.p, xyz, raw_sz, hipMemcpyHostToDevice, s));
+  const unsigned char* raw = reinterpret_cast<const unsigned char*>(xyz);
+  if (!on_device) {
+    HIP_TRY(c->raw_bytes.ensure(raw_sz));
+    HIP_TRY(hipMemcpyAsync(c->raw_bytes.p, xyz, raw_sz, hipMemcpyHostToDevice, s));
+    raw = c->raw_bytes.as<unsigned char>();
+  }
   const int nb = (N + 255) / 256;
   HIP_TRY(c->raw_pts.ensure(sizeof(float4) * n));
   HIP_TRY(c->partial.ensure(sizeof(float) * 6 * nb));
   HIP_TRY(c->nonfinite.ensure(sizeof(int)));
   HIP_TRY(hipMemsetAsync(c->nonfinite.p, 0, sizeof(int), s));
   HIP_TRY(cd->quant.ensure(sizeof(float) * 8));
-  launch_pack_bbox(s, c->raw_bytes.as<unsigned char>(), stride, N, c->raw_pts.as<float4>(), c->partial.as<float>(),
+  launch_pack_bbox(s, raw, stride, N, c->raw_pts.as<float4>(), c->partial.as<float>(),
                    c->nonfinite.as<int>(), nb);
   launch_bbox_final(s, c->partial.as<float>(), nb, cd->quant.as<float>());
   HIP_TRY(c->keys_tmp.ensure(sizeof(unsigned long long) * n));

@@ -269,6 +269,16 @@ def s2m_problem(rows: int, cols: int, n_keyframes: int, submap_size: int, cfg_id
     return {"source": src, "keyframes": kfs, "subset": subset, "T_true": cur, "guess": guess}
 
 
+def odometry_sequence(rows: int, cols: int, n_frames: int, cfg_id: int = 5, moving: bool = True):
+    """Consecutive ray-cast frames along the ground-truth trajectory (forward
+    only), with moving pedestrians: the input of the odometry driver (cfg 5's
+    S2M chain).  Returns (frames, world poses)."""
+    seed = 1000 + cfg_id
+    scene = make_scene(seed, moving=moving)
+    poses = trajectory(n_frames, seed)
+    return [raycast(scene, poses[k], rows, cols, seed=seed + k, t=0.1 * k) for k in range(n_frames)], poses
+
+
 def sequence(rows: int, cols: int, n_frames: int, n_unique: int, cfg_id: int = 5):
     """Scan sequence for the batched-odometry case (SURVEY.md §8(d) cfg 5):
     ``n_unique`` consecutive ray-cast frames of the plaza with MOVING

@@ -1003,6 +1003,74 @@ int oref_gicp_trace(oref_gicp* h, double* out, int max_entries) {
   return n;
 }
 
+// pcl::VoxelGrid<PointXYZI>::applyFilter (PCL 1.10, filters/impl/voxel_grid.hpp;
+// used at odom.cc:469-475 and :1133-1137), xyz part: finite points only,
+// min/max box, int voxel index (ijk - min_b) . divb_mul, std::sort of the
+// (idx, point) pairs by idx (the SAME libstdc++ introsort, so equal-index
+// points keep the reference's summation order), one centroid per run:
+// float sum / count (CentroidPoint's AccumulatorXYZ).  Returns the output
+// count, or -1 when the grid overflows an int (the reference then copies
+// the input unchanged).
+int oref_voxel_grid(const float* xyz, int n, float leaf, float* out) {
+  const float inv = 1.0f / leaf;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  bool any = false;
+  for (int i = 0; i < n; ++i) {
+    const float* p = xyz + 3 * i;
+    if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]))) continue;
+    any = true;
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = std::min(mn[a], p[a]);
+      mx[a] = std::max(mx[a], p[a]);
+    }
+  }
+  if (!any) return 0;
+  long long d[3];
+  for (int a = 0; a < 3; ++a) d[a] = static_cast<long long>((mx[a] - mn[a]) * inv) + 1;
+  if ((d[0] * d[1] * d[2]) > static_cast<long long>(std::numeric_limits<int>::max())) return -1;
+  int minb[3], divb[3];
+  for (int a = 0; a < 3; ++a) {
+    minb[a] = static_cast<int>(std::floor(mn[a] * inv));
+    const int maxb = static_cast<int>(std::floor(mx[a] * inv));
+    divb[a] = maxb - minb[a] + 1;
+  }
+  const int mul[3] = {1, divb[0], divb[0] * divb[1]};
+  struct Idx {
+    unsigned idx, pt;
+    bool operator<(const Idx& o) const { return idx < o.idx; }
+  };
+  std::vector<Idx> v;
+  v.reserve(n);
+  for (int i = 0; i < n; ++i) {
+    const float* p = xyz + 3 * i;
+    if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]))) continue;
+    int ijk[3];
+    for (int a = 0; a < 3; ++a) ijk[a] = static_cast<int>(std::floor(p[a] * inv) - static_cast<float>(minb[a]));
+    v.push_back({static_cast<unsigned>(ijk[0] * mul[0] + ijk[1] * mul[1] + ijk[2] * mul[2]), (unsigned)i});
+  }
+  std::sort(v.begin(), v.end(), std::less<Idx>());
+  int m = 0;
+  size_t k = 0;
+  while (k < v.size()) {
+    size_t e = k + 1;
+    while (e < v.size() && v[e].idx == v[k].idx) ++e;
+    float sx = 0.f, sy = 0.f, sz = 0.f;
+    for (size_t q = k; q < e; ++q) {
+      const float* p = xyz + 3 * v[q].pt;
+      sx += p[0];
+      sy += p[1];
+      sz += p[2];
+    }
+    const float c = static_cast<float>(e - k);
+    out[3 * m] = sx / c;
+    out[3 * m + 1] = sy / c;
+    out[3 * m + 2] = sz / c;
+    ++m;
+    k = e;
+  }
+  return m;
+}
+
 // Known-answer helpers
 void oref_so3_exp(const double* w, double* R9) { oref::so3_exp(w, R9); }
 void oref_ldlt_solve6(const double* A, const double* b, double* x) { oref::ldlt_solve6(A, b, x); }

@@ -99,6 +99,7 @@ def lib():
         L.oref_gicp_compute_error.argtypes = [C.c_void_p, C.c_void_p]
         L.oref_gicp_last_correspondences.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.oref_gicp_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.oref_voxel_grid.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_void_p]
         L.oref_so3_exp.argtypes = [C.c_void_p, C.c_void_p]
         L.oref_ldlt_solve6.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.oref_regularize.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
@@ -246,6 +247,23 @@ def regularize(C9, reg):
     C9 = np.ascontiguousarray(C9, np.float64); out = np.zeros(9)
     lib().oref_regularize(_fp(C9), REG[reg] if isinstance(reg, str) else reg, _fp(out))
     return out.reshape(3, 3)
+
+
+def voxel_grid(points, leaf):
+    """pcl::VoxelGrid (oracle/cpu_ref.cpp oref_voxel_grid): centroids in voxel-index order."""
+    a = _xyz(points)
+    out = np.zeros((max(len(a), 1), 3), np.float32)
+    m = lib().oref_voxel_grid(_fp(a), len(a), float(leaf), _fp(out))
+    return a.copy() if m < 0 else out[:m]
+
+
+def crop_box_negative(points, size):
+    """pcl::CropBox with setNegative(true), min (-s,-s,-s), max (s,s,s) (odom.cc:114-119):
+    keeps the finite points with a coordinate below -s or above s, in order."""
+    a = _xyz(points)
+    fin = np.isfinite(a).all(axis=1)
+    out = (a < -size).any(axis=1) | (a > size).any(axis=1)
+    return a[fin & out]
 
 
 def residual_image(points, residuals, theta_min=-np.pi / 3, theta_max=np.pi / 3, width=512, height=512):
