@@ -219,6 +219,83 @@ def batched_leg(dist, rank, world, local_rank, args):
             "per_pair_work": "H2D + index build + covariances + align", "collective": "none (frames split by rank)"}
 
 
+def s2s_gn_leg(local_rank, args):
+    """BASELINE.json configs[1] / SURVEY.md §8(d) cfg 2: S2S GICP of two
+    64x2048 (131,072-pt) scans, 20 fixed Gauss-Newton outer iterations
+    (optimizer GN, fixed_iterations 20, convergence off), k=10 covariances
+    resident.  One step = one align of 20 iterations."""
+    import dynamic_direct_lidar_odometry_amd as P
+    from dynamic_direct_lidar_odometry_amd import scene, SOURCE, TARGET
+    src, tgt, _ = scene.s2s_pair(64, 2048, 2)
+    c = P.Context(local_rank)
+    c.set_params(P.default_params(k_correspondences=10, max_correspondence_distance=1.0, optimizer=P.GAUSS_NEWTON,
+                                  fixed_iterations=20, max_iterations=20))
+    c.set_target(tgt)
+    c.set_source(src)
+    c.compute_covariances(SOURCE)
+    c.compute_covariances(TARGET)
+    for _ in range(2):
+        c.align()
+    c.synchronize()
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(args.gn_steps):
+        _, r = c.align()
+        iters += r.iterations_run
+    c.synchronize()
+    el = time.perf_counter() - t0
+    c.close()
+    return {"workload": f"cfg2 S2S GICP: {len(src)}-pt -> {len(tgt)}-pt 64x2048 scans, 20 fixed GN iterations, "
+                        "k=10, maxCorr 1.0 m", "iters_per_s": round(iters / el, 2),
+            "ms_per_align": round(1e3 * el / args.gn_steps, 4), "iterations_per_align": iters // args.gn_steps}
+
+
+def odometry_leg(dist, rank, world, local_rank, args, frames=None):
+    """BASELINE.json configs[4], the S2M half (SURVEY.md §8(e) cfg 5): the
+    odometry driver (include/ddlo_odom.h, cfg/ddlo.yaml parameters) over the
+    64x2048 scan sequence — per frame upload, crop box + voxel filter,
+    spaciousness, S2S, submap selection / assembly, S2M, keyframe insertion.
+    The S2M chain is sequential, so with N GPUs the sequence is cut into N
+    contiguous segments, each an independent chain (its own keyframe map)."""
+    from dynamic_direct_lidar_odometry_amd import scene
+    from dynamic_direct_lidar_odometry_amd import odometry as OD
+    if frames is None:
+        frames, _ = scene.sequence(64, 2048, args.batch_frames, args.batch_unique)
+    a = len(frames) * rank // world
+    b = len(frames) * (rank + 1) // world
+    mine = frames[a:b]
+    warm = OD.Odometry(local_rank)
+    for f in mine[:4]:
+        warm.process(f)
+    warm.close()
+    odo = OD.Odometry(local_rank)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    kfs, tracked, s2m_it, pts = 0, 0, 0, 0
+    for f in mine:
+        r = odo.process(f)
+        kfs += r.keyframe_added
+        tracked += r.status == OD.TRACKED
+        s2m_it += r.s2m.iterations_run
+        pts += r.scan_points
+    el = time.perf_counter() - t0
+    nk = r.num_keyframes
+    sub_pts = int(r.submap_points)
+    odo.close()
+    el, nframes = reduce_over_ranks(dist, el, len(mine), f"cuda:{local_rank}")
+    return {"workload": f"cfg5 S2M chain: odometry driver over {len(frames)} 64x2048 frames "
+                        f"({args.batch_unique} ray-cast frames replayed forward/backward), ddlo.yaml parameters "
+                        "(crop 1 m, voxel 0.1 m, S2S k=10 / S2M k=20, adaptive keyframes, knn/kcv/kcc 10)",
+            "n_gpus": world, "frames": int(nframes), "frames_per_s": round(nframes / el, 2),
+            "ms_per_frame": round(1e3 * el / nframes, 4),
+            "per_frame_work": "H2D + crop + voxel + metrics + S2S (index, covariances, align) + submap + S2M + keyframes",
+            "rank0": {"keyframes": nk, "last_submap_points": sub_pts, "tracked": tracked,
+                      "mean_scan_points": round(pts / max(len(mine), 1), 1),
+                      "mean_s2m_iterations": round(s2m_it / max(tracked, 1), 2)},
+            "segments": f"{world} independent chains (contiguous frame ranges)"}
+
+
 def main():
     # Native libraries (RCCL's version banner) print to fd 1; the contract is
     # ONE JSON line on stdout, so route fd 1 to stderr and keep the real
@@ -237,6 +314,9 @@ def main():
     ap.add_argument("--batch-frames", type=int, default=201)
     ap.add_argument("--batch-unique", type=int, default=20)
     ap.add_argument("--batch-streams", type=int, default=2)
+    ap.add_argument("--no-gn", action="store_true", help="skip the cfg2 S2S 20-GN-iteration leg")
+    ap.add_argument("--gn-steps", type=int, default=10)
+    ap.add_argument("--no-odom", action="store_true", help="skip the cfg5 odometry-driver (S2M chain) leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -330,7 +410,7 @@ def main():
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_unit": "bytes per linearize launch (L2->fabric, Infinity-Cache hits included)",
                      "traffic_source": traffic_src,
-                     "kernel": "linearize = k_nn_search + k_moments (per outer iteration)",
+                     "kernel": "linearize = k_nn_seed + k_nn_collect + k_nn_scan + k_moments (per outer iteration)",
                      "avg_launch_us": round(avg_launch_s * 1e6, 2),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch)},
     }
@@ -358,8 +438,12 @@ def main():
     ctx.close()
     if not args.no_sharded:
         result["sharded_s2m"] = sharded_leg(dist, rank, world, local_rank, args)
+    if not args.no_gn:
+        result["s2s_gn"] = s2s_gn_leg(local_rank, args)
     if not args.no_batch:
         result["batched_s2s"] = batched_leg(dist, rank, world, local_rank, args)
+    if not args.no_odom:
+        result["odometry"] = odometry_leg(dist, rank, world, local_rank, args)
     if rank == 0:
         print(json.dumps(result), file=json_out, flush=True)
     if dist:

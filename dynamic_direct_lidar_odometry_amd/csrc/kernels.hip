@@ -140,12 +140,19 @@ __global__ __launch_bounds__(256) void k_gather(const float4* __restrict__ raw, 
 // the prefixes in (prefix(i - 1), prefix(i)] with i; the last thread also
 // fills the prefixes past the largest key with n.
 __global__ __launch_bounds__(256) void k_key_dir(const unsigned long long* __restrict__ keys, int n, int* __restrict__ dir) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > n) return;
+  // dir[p] = first sorted position whose top kDirBits Morton bits are >= p
+  // (p in [0, 2^kDirBits]); one thread per entry, a lower-bound search each,
+  // so empty stretches of the Morton space cost no serial fill
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > (1 << kDirBits)) return;
   constexpr int sh = 63 - kDirBits;
-  const long pa = i == 0 ? -1 : (long)(keys[i - 1] >> sh);
-  const long pb = i == n ? (1l << kDirBits) : (long)(keys[i] >> sh);
-  for (long p = pa + 1; p <= pb; ++p) dir[p] = i;
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((long)(keys[mid] >> sh) < (long)p) lo = mid + 1;
+    else hi = mid;
+  }
+  dir[p] = lo;
 }
 
 // Per-leaf SoA copy of the sorted points: leaf l = x[32], y[32], z[32], so
@@ -2026,7 +2033,7 @@ void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, int
   k_gather<<<cdiv(npad, 256), 256, 0, s>>>(raw, perm, n, npad, sorted, inv_perm);
 }
 void launch_key_dir(hipStream_t s, const unsigned long long* keys, int n, int* dir) {
-  k_key_dir<<<cdiv(n + 1, 256), 256, 0, s>>>(keys, n, dir);
+  k_key_dir<<<cdiv((1 << kDirBits) + 1, 256), 256, 0, s>>>(keys, n, dir);
 }
 void launch_leaf_soa(hipStream_t s, const float4* pts, int npad, float* soa) {
   k_leaf_soa<<<cdiv(npad, 256), 256, 0, s>>>(pts, npad, soa);
