@@ -85,7 +85,7 @@ float env_float(const char* name, float dflt) {
   if (!v || !*v) return dflt;
   char* end = nullptr;
   const float f = std::strtof(v, &end);
-  return (end && end != v && f > 0.f) ? f : dflt;
+  return (end && end != v && f >= 0.f) ? f : dflt;
 }
 
 int env_int(const char* name, int dflt) {
@@ -95,7 +95,7 @@ int env_int(const char* name, int dflt) {
 
 // byte layout of ctx->search for ns source points
 struct SearchLayout {
-  size_t qstate, key, ctr, hard_list, hard_flag, grp_blocks, tasks, total;
+  size_t qstate, key, ctr, hard_list, hard_flag, grp_blocks, ref, ref_p, sec, tasks, total;
   int cap_r;
   explicit SearchLayout(int ns) {
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -106,7 +106,10 @@ struct SearchLayout {
     hard_list = ctr + al(sizeof(unsigned) * kTaskCounters * kCtrStride);
     hard_flag = hard_list + al(sizeof(int) * kHardMax);
     grp_blocks = hard_flag + al((size_t)ns / 16 + 16);
-    tasks = grp_blocks + al(sizeof(unsigned short) * ((size_t)ns / 16 + 16));
+    ref = grp_blocks + al(sizeof(unsigned short) * ((size_t)ns / 16 + 16));
+    ref_p = ref + al(sizeof(float4) * (size_t)ns);
+    sec = ref_p + al(sizeof(float4) * (size_t)ns);
+    tasks = sec + al(sizeof(unsigned) * (size_t)ns);
     total = tasks + sizeof(unsigned long long) * (size_t)kTaskRegions * cap_r;
   }
 };
@@ -157,12 +160,20 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
     j.hard_list = reinterpret_cast<int*>(u + sl.hard_list);
     j.hard_flag = reinterpret_cast<unsigned char*>(u + sl.hard_flag);
     j.grp_blocks = reinterpret_cast<unsigned short*>(u + sl.grp_blocks);
+    j.ref = reinterpret_cast<float4*>(u + sl.ref);
+    j.ref_p = reinterpret_cast<float4*>(u + sl.ref_p);
+    j.sec = reinterpret_cast<unsigned*>(u + sl.sec);
   }
   j.list_flush = (int)env_float("DDLO_LIST_FLUSH", 16.f);
   j.xcd_scan = env_int("DDLO_XCD_SCAN", 1);
   j.hard_extent = env_float("DDLO_HARD_EXTENT", 4.0f);
   j.hard_blocks = env_int("DDLO_HARD_BLOCKS", 10);
   j.prev_window = env_int("DDLO_PREV_WINDOW", 2);
+  j.reuse = search_uses_tasks() ? env_int("DDLO_REUSE", 1) : 0;
+  j.reuse_gap = env_float("DDLO_REUSE_GAP", 0.05f);
+  j.reuse_gap0 = env_float("DDLO_REUSE_GAP0", 0.f);
+  j.reuse_rec0 = env_int("DDLO_REUSE_REC0", 0);
+  j.reuse_rec_eps = env_float("DDLO_REUSE_REC_EPS", 0.05f);
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   return GICP_OK;
 }

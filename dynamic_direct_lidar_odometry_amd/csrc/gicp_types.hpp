@@ -77,7 +77,9 @@ struct AlignState {
   int lm_trials;
   int num_corr;
   int have_prev;         // correspondences of a previous linearize are valid
-  int pad[4];
+  int rec;               // the next search records reuse references (AlignJob::ref)
+  float src_radius;      // max |p| over the source cloud's root boxes (reuse step bound)
+  int pad[2];
 };
 
 // Everything a kernel needs for one align, written by the host before launch.
@@ -129,6 +131,21 @@ struct AlignJob {
   int xcd_scan;                  // scan: one spatial eighth of the tasks per XCD (speed only)
   int prev_window;         // seed after a large pose step: 0 previous match only, 1 + Morton window around it,
                            // 2 + Morton window at the new position (default)
+  // Verified match reuse across outer iterations: per query
+  // the position q_ref of its last search, its match p1 there and a lower
+  // bound B^2 on the fp32 squared distance from q_ref to every OTHER target
+  // point.  At a later iteration, with the query moved by eps, p1 is still
+  // the exact nearest point if d(q, p1) < B - eps (with fp32 rounding
+  // margins); then no walk or scan runs for the query.
+  int reuse;                     // 1 = check / record references (task search only)
+  float reuse_gap;               // walk-radius inflation (m) at iterations >= 1: widens B beyond d1
+  float reuse_gap0;              // the same at iteration 0
+  int reuse_rec0;                // iteration 0 records references
+  float reuse_rec_eps;           // later iterations record them only after an LM step that moved
+                                 // every source point by less than this (m): the next one is smaller
+  float4* ref;                   // [n_src] q_ref (x, y, z) + B^2 (< 0: no reference)
+  float4* ref_p;                 // [n_src] p1 (x, y, z) + its sorted target position as int bits (-1: none within the bound)
+  unsigned* sec;                 // [n_src] fp32 bits: smallest squared distance of an examined non-best point
 };
 
 }  // namespace ddlo

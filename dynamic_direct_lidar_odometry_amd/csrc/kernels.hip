@@ -695,6 +695,23 @@ constexpr int kSeedW = 8;           // Morton-window seed points per slice lane
 __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (threadIdx.x < kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;
+  if (threadIdx.x < 64) {   // source radius from the top-level boxes (<= 64 of them)
+    const CloudDev& c = job->src;
+    const int top = c.nlevels - 1;
+    const int off = lvl_off(c, top), cnt = lvl_cnt(c, top);
+    float r = 0.f;
+    if ((int)threadIdx.x < cnt) {
+      const float4 lo = c.box_lo[off + threadIdx.x], hi = c.box_hi[off + threadIdx.x];
+      const float mx = fmaxf(fabsf(lo.x), fabsf(hi.x)), my = fmaxf(fabsf(lo.y), fabsf(hi.y)),
+                  mz = fmaxf(fabsf(lo.z), fabsf(hi.z));
+      r = sqrtf(mx * mx + my * my + mz * mz) * 1.0001f;
+    }
+    for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m));
+    if (threadIdx.x == 0) {
+      st->src_radius = r;
+      st->rec = job->reuse && job->reuse_rec0;
+    }
+  }
   if (threadIdx.x == 0) {
     for (int i = 0; i < 9; ++i) st->R[i] = job->guess_R[i];
     for (int i = 0; i < 3; ++i) st->t[i] = job->guess_t[i];
@@ -757,6 +774,9 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   float Rp[9], tp[3];
   for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
   for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
+  const int reuse = job->reuse;
+  const bool check_ref = reuse && have_prev;
+  const int rec = st->rec;   // this search records references
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const int i = g * Q + qi;
@@ -766,22 +786,61 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     const float4 a = ldg4(src.pts, ic);
     const int jprev = have_prev ? corr[ic] : -1;
     const float sqprev = have_prev ? sqd[ic] : 0.f;
+    const float4 rf = check_ref ? ldg4(job->ref, ic) : make_float4(0.f, 0.f, 0.f, -1.f);
+    const float4 rp = check_ref ? ldg4(job->ref_p, ic) : make_float4(0.f, 0.f, 0.f, 0.f);
     // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
     // spatial sharding: search only the queries this rank owns
     const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
-    const bool active = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi));
+    const bool owned = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi));
+    // Verified reuse (AlignJob::ref): every target point other than p1 was
+    // at fp32 squared distance >= B^2 from q_ref, so (relative 1e-6 covers
+    // the fp32 rounding of a squared distance) its true distance from q is
+    // >= sqrt(B^2 / (1 + 1e-6)) - eps, eps = |q - q_ref|, and its fp32
+    // squared distance >= lb2.  p1 at dn < lb2 is then the exact minimum
+    // (no tie possible); with no p1, lb2 > cap2 means no point within the
+    // bound.  The key is what the full search returns: min((cap2, none),
+    // (dn, p1)).
+    bool passed = false;
+    unsigned long long pass_key = dkey(cap2, -1);
+    int rj = -1;
+    float dn = INFINITY;
+    if (owned && rf.w >= 0.f) {
+      rj = __float_as_int(rp.w);
+      const double ex = (double)qx - rf.x, ey = (double)qy - rf.y, ez = (double)qz - rf.z;
+      const double eps = sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + 1e-9) + 1e-12;
+      const double b = sqrt((double)rf.w / (1.0 + 1e-6));
+      const double lb2 = b > eps ? (b - eps) * (b - eps) * (1.0 - 1e-6) : -1.0;
+      if (rj >= 0) {
+        dn = dist2(qx, qy, qz, rp.x, rp.y, rp.z);
+        if ((double)dn < lb2) {
+          passed = true;
+          pass_key = umin64(pass_key, dkey(dn, rj));
+        }
+      } else if (lb2 > (double)cap2) {
+        passed = true;
+      }
+    }
+    const bool active = owned && !passed;
     if (!__any(active)) {
       if (inrange && lane < Q) {
-        keyout[i] = dkey(INFINITY, -1);
+        keyout[i] = passed ? pass_key : dkey(INFINITY, -1);
         qstate[i] = make_float4(qx, qy, qz, -1.f);
+        if (reuse && !have_prev) job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);   // not searched: no reference
       }
-      if (lane == 0) job->hard_flag[g] = 0;
-      if (stats && lane == 0) {
-        unsigned int* o = stats + (size_t)g * kStatFields;
-        for (int f = 0; f < kStatFields; ++f) o[f] = 0;
+      if (lane == 0) {
+        job->hard_flag[g] = 2;   // nothing to search: k_nn_collect skips the sub-group
+        job->grp_blocks[g] = 0;
+      }
+      if (stats) {
+        const unsigned npass = (unsigned)__popcll(__ballot(passed && lane < Q));
+        if (lane == 0) {
+          unsigned int* o = stats + (size_t)g * kStatFields;
+          for (int f = 0; f < kStatFields; ++f) o[f] = 0;
+          o[6] = npass << 8;
+        }
       }
       continue;
     }
@@ -834,6 +893,16 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
           }
         }
       }
+    }
+    // the reference's match at the new position is a real candidate
+    if (active && rj >= 0 && dn < vis.best) {
+      vis.best = dn;
+      vis.bestj = rj;
+      bpx = rp.x;
+      bpy = rp.y;
+      bpz = rp.z;
+      have_bp = true;
+      seeded = true;
     }
     // Exact seeding for queries without a usable previous correspondence:
     // the real target points around the query's Morton position give an
@@ -902,13 +971,22 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         }
       }
     }
+    // walk radius: the seed bound, widened by the reuse gap so that the
+    // reference recorded from this search has B well above d1
+    float wr = vis.best;
+    const float gap = have_prev ? job->reuse_gap : job->reuse_gap0;
+    if (rec && active && gap > 0.f) {
+      const double r = sqrt((double)vis.best) + (double)gap;
+      wr = __uint_as_float(__float_as_uint((float)(r * r)) + 1);   // rounded up
+    }
     if (inrange && lane < Q) {
-      qstate[i] = make_float4(qx, qy, qz, active ? vis.best : -1.f);
-      keyout[i] = active ? dkey(vis.best, vis.bestj) : dkey(INFINITY, -1);
+      qstate[i] = make_float4(qx, qy, qz, active ? wr : -1.f);
+      keyout[i] = active ? dkey(vis.best, vis.bestj) : passed ? pass_key : dkey(INFINITY, -1);
+      if (reuse && !have_prev && !active) job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);
     }
     // hard sub-group: a wide union box (a query far from every target point
     // drags many blocks into the walk) -> listed, walked first
-    const WaveBox whole = make_wave_box(active, qx, qy, qz, active ? vis.best : -1.f);
+    const WaveBox whole = make_wave_box(active, qx, qy, qz, active ? wr : -1.f);
     // hard: the previous outer iteration walked many blocks for this
     // sub-group (same source points, a nearby pose), else -- first
     // iteration -- a wide union box
@@ -921,10 +999,13 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       }
       job->hard_flag[g] = (unsigned char)(hard && slot < kHardMax);
     }
-    if (stats && lane == 0) {
-      unsigned int* o = stats + (size_t)g * kStatFields;
-      o[1] = min(((unsigned)__builtin_amdgcn_s_memtime() - (unsigned)tm0) >> 4, 65535u);
-      o[6] = (unsigned)hard;
+    if (stats) {
+      const unsigned npass = (unsigned)__popcll(__ballot(passed && lane < Q));
+      if (lane == 0) {
+        unsigned int* o = stats + (size_t)g * kStatFields;
+        o[1] = min(((unsigned)__builtin_amdgcn_s_memtime() - (unsigned)tm0) >> 4, 65535u);
+        o[6] = (unsigned)hard | (npass << 8);   // queries proven by their reuse reference
+      }
     }
   }
 }
@@ -968,6 +1049,12 @@ __global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __rest
     if (g >= ngroups || job->hard_flag[g]) g = -1;
   }
   g = __builtin_amdgcn_readfirstlane(g);
+  if (wave >= kHardMax) {
+    // no sub-group of this block has work: skip the box cache fill (every
+    // wave reads the block's kLinWaves flags itself: block-uniform, no barrier)
+    const int gk = (int)blockIdx.x * kLinWaves + lane - kHardMax;
+    if (!__any(lane < kLinWaves && gk < ngroups && !job->hard_flag[gk])) return;
+  }
   fill_upper(tgt, upper);
   __syncthreads();
   if (g < 0) return;
@@ -987,9 +1074,11 @@ __global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __rest
   col.qz = q.z;
   col.active = inrange && q.w >= 0.f;
   col.bk = k0;
+  col.wr = q.w;
   col.sg = g;
   col.run(tgt, tl, skey, job->split_extent);
   if (inrange && lane < Q && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
+  if (st->rec && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further
   if (lane == 0) job->grp_blocks[g] = (unsigned short)min(col.st_blocks, 65535u);
   if (stats && lane == 0) {
     const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
@@ -1058,9 +1147,48 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   const int chunk = (n + wpr - 1) / wpr;
   const int lo = c * chunk, hi = min(n, lo + chunk);
   const unsigned long long* rt = job->tasks + (size_t)r * cap_r;
+  unsigned* const sec = job->sec;
+  const bool reuse = st->rec != 0;   // this search records reuse references
   int run_sg = -1;
   unsigned long long acc = ~0ull;   // lane's query minimum over the current run
+  float acc2 = INFINITY;            // smallest distance of the run's other points (reuse)
   float run_bound = -1.f;
+  // A run's merge into the result: the key's atomicMin, then (reuse) the
+  // smallest distance of every examined point except the final best — the
+  // run's other points and whichever of (old key, run minimum) lost.  The
+  // second push needs the atomicMin's return value: it is issued at the
+  // NEXT run's merge, so the return trip overlaps the scan of that run.
+  bool pend = false;
+  size_t pend_q = 0;
+  unsigned long long pend_acc = 0ull, pend_old = 0ull;
+  float pend_acc2 = 0.f, pend_bound = 0.f;
+  auto resolve = [&]() {
+    if (pend) {
+      float push = pend_acc2;
+      if (pend_old != pend_acc) {
+        const unsigned long long lost = pend_old < pend_acc ? pend_acc : pend_old;
+        if (key_real(lost)) push = fminf(push, key_dist(lost));
+      }
+      if (push < pend_bound) atomicMin(sec + pend_q, __float_as_uint(push));
+      pend = false;
+    }
+  };
+  auto flush_run = [&]() {
+    if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound)) {
+      const size_t qidx = (size_t)run_sg * kTaskQ + qi;
+      if (reuse) {
+        resolve();
+        pend_old = atomicMin(key + qidx, acc);
+        pend = true;
+        pend_q = qidx;
+        pend_acc = acc;
+        pend_acc2 = acc2;
+        pend_bound = run_bound;
+      } else {
+        atomicMin(key + qidx, acc);
+      }
+    }
+  };
   for (int wbase = lo; wbase < hi; wbase += 64) {
     const int wcnt = min(64, hi - wbase);
     const unsigned long long tl = lane < wcnt ? rt[wbase + lane] : 0ull;   // up to 64 task words at once
@@ -1095,10 +1223,10 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
         const unsigned long long t = readlane_u64(tl, b0 + k);
         const int sg = (int)((t >> 16) & 0xffffffull);
         if (sg != run_sg) {   // uniform: a new sub-group's run starts
-          if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound))
-            atomicMin(key + (size_t)run_sg * kTaskQ + qi, acc);
+          flush_run();
           run_sg = sg;
           acc = ~0ull;
+          acc2 = INFINITY;
           run_bound = -1.f;
         }
         const unsigned char* T = cur + k * kScanTaskBytes;
@@ -1113,7 +1241,7 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
         // lane's points come in increasing position, so strict < keeps the
         // lowest position among equal distances
         const f2v qx2 = {q.x, q.x}, qy2 = {q.y, q.y}, qz2 = {q.z, q.z};
-        float bd = INFINITY;
+        float bd = INFINITY, sd = INFINITY;
         int bh = 0;
 #pragma unroll
         for (int h = 0; h < 8; h += 2) {
@@ -1121,22 +1249,27 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
           const f2v dy = qy2 - f2v{Y[h], Y[h + 1]};
           const f2v dz = qz2 - f2v{Z[h], Z[h + 1]};
           const f2v d = (dx * dx + dy * dy) + dz * dz;
-          if (d.x < bd) { bd = d.x; bh = h; }
-          if (d.y < bd) { bd = d.y; bh = h + 1; }
+          if (d.x < bd) { sd = bd; bd = d.x; bh = h; } else { sd = fminf(sd, d.x); }
+          if (d.y < bd) { sd = bd; bd = d.y; bh = h + 1; } else { sd = fminf(sd, d.y); }
         }
         unsigned long long bk = dkey(bd, (int)(t >> 40) * kLeafSize + s * 8 + bh);
-        bk = xor_min64<16>(bk);
-        bk = xor_min64<32>(bk);
+        if (reuse) {
+          xor_top2<16>(bk, sd);
+          xor_top2<32>(bk, sd);
+        } else {
+          bk = xor_min64<16>(bk);
+          bk = xor_min64<32>(bk);
+        }
         if (((t >> qi) & 1ull) != 0ull) {
-          acc = umin64(acc, bk);
+          fold_top2(acc, acc2, bk, sd);
           run_bound = q.w;
         }
       }
       __builtin_amdgcn_wave_barrier();   // reads of `cur` done before it is refilled
     }
   }
-  if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound))
-    atomicMin(key + (size_t)run_sg * kTaskQ + qi, acc);
+  flush_run();
+  resolve();
 }
 
 template <int Q, int MINW>
@@ -1367,6 +1500,8 @@ __global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ j
   const auto sqd = gpw(job->sqd);
   const auto slab = gpw(job->slab);
   const double max_corr2 = job->max_corr2;
+  const int reuse = job->reuse;
+  const int rec = st->rec;
   double R[9], t[3];
   for (int e = 0; e < 9; ++e) R[e] = st->R[e];
   for (int e = 0; e < 3; ++e) t[e] = st->t[e];
@@ -1392,6 +1527,22 @@ __global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ j
       j = (kj != 0xffffffffu && (double)kd < max_corr2) ? (int)kj : -1;
       corr[i] = j;
       sqd[i] = kj != 0xffffffffu ? kd : INFINITY;
+      // reuse reference of a query searched in this iteration: its position,
+      // B^2 = min(smallest distance of an examined non-best point, walk
+      // radius) — every unexamined point lies in a leaf farther than the
+      // walk radius — and its match
+      if (reuse) {
+        const float4 qs = ldg4(job->qstate, i);
+        if (qs.w >= 0.f) {
+          job->ref[i] = make_float4(qs.x, qs.y, qs.z, rec ? fminf(__uint_as_float(job->sec[i]), qs.w) : -1.f);
+          float4 pp = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+          if (kj != 0xffffffffu) {
+            const float4 p = ldg4(tgt.pts, (int)kj);
+            pp = make_float4(p.x, p.y, p.z, __int_as_float((int)kj));
+          }
+          job->ref_p[i] = pp;
+        }
+      }
     }
     Contrib C;
     if (j >= 0) {
@@ -1858,13 +2009,27 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
       st->lambda = tr_lambda[ntr - 1] * 2.0;  // not observable: the align ends
     }
   }
+  int rec = job->reuse;
   if (accept) {
     double Rn[9], tn[3];
     compose(tr_R[chosen], tr_t[chosen], R, t, Rn, tn);
     for (int e = 0; e < 9; ++e) st->R[e] = Rn[e];
     for (int e = 0; e < 3; ++e) st->t[e] = tn[e];
     for (int e = 0; e < 36; ++e) st->final_hessian[e] = Hs[e];
+    // how far the step moved a source point: |dR q + dt - q| <= |dR - I|_F |q| + |dt|,
+    // |q| <= src_radius + |t|; the next search records references only
+    // after a small step (the one after it is expected to be smaller)
+    double fro = 0.0;
+    for (int e = 0; e < 9; ++e) {
+      const double d = tr_R[chosen][e] - ((e % 4 == 0) ? 1.0 : 0.0);
+      fro += d * d;
+    }
+    const double* dt = tr_t[chosen];
+    const double mv = sqrt(fro) * ((double)st->src_radius + sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2])) +
+                      sqrt(dt[0] * dt[0] + dt[1] * dt[1] + dt[2] * dt[2]);
+    rec = rec && mv < (double)job->reuse_rec_eps;
   }
+  st->rec = rec;
   st->iter = it + 1;
   st->have_prev = 1;
   if (!ok) {
@@ -2094,14 +2259,17 @@ static int scan_blocks(int nsrc) {
   waves = (waves + 8 * kTaskRegions - 1) / (8 * kTaskRegions) * (8 * kTaskRegions);
   return waves / kScanWaves;
 }
-void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int job_upper_count) {
-  const int search_groups = (nsrc + kSearchQ - 1) / kSearchQ;
-  const int sb = std::max(1, (search_groups + kLinWaves - 1) / kLinWaves);
+bool search_uses_tasks() {
   static const bool old_search = [] {   // DDLO_SEARCH=collect: the single-kernel collect-then-scan search (A/B)
     const char* v = std::getenv("DDLO_SEARCH");
     return v && std::strcmp(v, "collect") == 0;
   }();
-  if (old_search) {
+  return !old_search;
+}
+void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int job_upper_count) {
+  const int search_groups = (nsrc + kSearchQ - 1) / kSearchQ;
+  const int sb = std::max(1, (search_groups + kLinWaves - 1) / kLinWaves);
+  if (!search_uses_tasks()) {
     k_nn_search<kSearchQ, 3><<<sb, 64 * kLinWaves, search_lds_bytes(job_upper_count), s>>>(job);
   } else {
     static const int occ_seed = env_knob("DDLO_OCC_SEED", 4), occ_col = env_knob("DDLO_OCC_COLLECT", 3),

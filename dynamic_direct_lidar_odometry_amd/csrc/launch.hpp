@@ -26,6 +26,7 @@ void launch_align_init(hipStream_t s, const AlignJob* job);
 // tgt_upper: number of upper-level (>= 1) boxes of the target (LDS cache size)
 void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int tgt_upper);
 int search_queries_per_wave();
+bool search_uses_tasks();   // false under DDLO_SEARCH=collect (the single-kernel search)
 int task_cap_per_region(int nsrc);   // task-list slots per region for nsrc source points
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
 void launch_lm_step(hipStream_t s, const AlignJob* job);

@@ -43,30 +43,48 @@ __device__ __forceinline__ unsigned long long make_task(int leaf, int sg, unsign
 
 // Scan one task: lane = (query qi = lane & 15, quarter s = lane >> 4), each
 // lane takes 8 of the leaf's 32 points; returns, in every lane of query qi,
-// the minimum (distance, position) key over the leaf.  `q` = the lane's
+// the minimum (distance, position) key over the leaf, and in sd the
+// smallest squared distance of the leaf's other points.  `q` = the lane's
 // query (x, y, z), loaded by the caller.
-__device__ __forceinline__ unsigned long long scan_leaf16(const CloudDev& tgt, int leaf, float qx, float qy, float qz) {
+__device__ __forceinline__ unsigned long long scan_leaf16(const CloudDev& tgt, int leaf, float qx, float qy, float qz,
+                                                          float& sd) {
   const int s = lane_id() >> 4;
   const long b = (long)leaf * kLeafSize + s * 8;
   f3v pt[8];
 #pragma unroll
   for (int h = 0; h < 8; ++h) pt[h] = ldg3(tgt.pts, b + h);
-  unsigned long long bk = ~0ull;
   const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+  float bd = INFINITY;
+  int bh = 0;
+  sd = INFINITY;
 #pragma unroll
   for (int h = 0; h < 8; h += 2) {
-    // two points at once (v_pk_* ops), same IEEE ops as dist2()
+    // two points at once (v_pk_* ops), same IEEE ops as dist2(); increasing
+    // position, so strict < keeps the lowest position among equal distances
     const f2v dx = qx2 - f2v{pt[h].x, pt[h + 1].x};
     const f2v dy = qy2 - f2v{pt[h].y, pt[h + 1].y};
     const f2v dz = qz2 - f2v{pt[h].z, pt[h + 1].z};
     const f2v d = (dx * dx + dy * dy) + dz * dz;
-    const int pj = (int)b + h;
-    bk = umin64(bk, dkey(d.x, pj));
-    bk = umin64(bk, dkey(d.y, pj + 1));
+    if (d.x < bd) { sd = bd; bd = d.x; bh = h; } else { sd = fminf(sd, d.x); }
+    if (d.y < bd) { sd = bd; bd = d.y; bh = h + 1; } else { sd = fminf(sd, d.y); }
   }
-  bk = xor_min64<16>(bk);   // quarters s and s ^ 1
-  bk = xor_min64<32>(bk);   // quarters s and s ^ 2
+  unsigned long long bk = dkey(bd, (int)b + bh);
+  xor_top2<16>(bk, sd);   // quarters s and s ^ 1
+  xor_top2<32>(bk, sd);   // quarters s and s ^ 2
   return bk;
+}
+
+// Fold a leaf's (best key k2, second distance sd2) into a query's running
+// (key, sec): every examined point except the final best ends up <= sec.
+// The displaced key counts only if it names a real point, and a point met
+// twice (a block reached by two walk entries) is not its own second.
+__device__ __forceinline__ void fold_top2(unsigned long long& key, float& sec, unsigned long long k2, float sd2) {
+  if (k2 != key) {
+    const unsigned long long hi = k2 < key ? key : k2;
+    if (key_real(hi)) sec = fminf(sec, key_dist(hi));
+  }
+  sec = fminf(sec, sd2);
+  key = umin64(key, k2);
 }
 
 // Per-wave LDS of the collect kernel.
@@ -97,6 +115,8 @@ struct TaskCollector {
   float qx, qy, qz;
   bool active;
   unsigned long long bk;   // the lane's query key (seed; lowered by inline scans)
+  float wr;                // walk radius (squared): leaves farther than this are skipped
+  float sec = INFINITY;    // smallest squared distance of an inline-scanned non-best point
   int sg;                  // sub-group index (this wave's 16 queries)
   unsigned st_blocks = 0, st_tasks = 0, st_inline = 0, st_splits = 0;
   unsigned tm_walk = 0;   // s_memtime after the walk (diagnostics)
@@ -121,8 +141,9 @@ struct TaskCollector {
     st_tasks += fit;
     for (int k = fit; k < n; ++k) {
       const unsigned long long t = L->tasks[k];
-      const unsigned long long k2 = scan_leaf16(c, (int)(t >> 40), qx, qy, qz);
-      if (active && ((t >> (lane & 15)) & 1ull)) bk = umin64(bk, k2);
+      float sd2;
+      const unsigned long long k2 = scan_leaf16(c, (int)(t >> 40), qx, qy, qz, sd2);
+      if (active && ((t >> (lane & 15)) & 1ull)) fold_top2(bk, sec, k2, sd2);
     }
     st_inline += n - fit;
     __builtin_amdgcn_wave_barrier();
@@ -299,7 +320,7 @@ struct TaskCollector {
   __device__ __forceinline__ void run(const CloudDev& c, const TaskList& tl, unsigned long long key, float split_extent) {
     const int lane = lane_id();
     const int qi = lane & 15;
-    if (lane < kTaskQ) L->q[lane] = f4v{qx, qy, qz, active ? bound() : -1.f};
+    if (lane < kTaskQ) L->q[lane] = f4v{qx, qy, qz, active ? wr : -1.f};
     if (lane < kMaxLevels) {
       L->lvl_off[lane] = lane == 0 ? c.off0 : lane == 1 ? c.off1 : lane == 2 ? c.off2 : lane == 3 ? c.off3 : c.off4;
       L->lvl_cnt[lane] = lane == 0 ? c.cnt0 : lane == 1 ? c.cnt1 : lane == 2 ? c.cnt2 : lane == 3 ? c.cnt3 : c.cnt4;
@@ -308,7 +329,7 @@ struct TaskCollector {
     __builtin_amdgcn_wave_barrier();
     unsigned long long rng = 0xffffull;   // up to 4 query masks, 16 bits each (no scratch array)
     int nr = 1;
-    const WaveBox whole = make_wave_box(active, qx, qy, qz, bound());
+    const WaveBox whole = make_wave_box(active, qx, qy, qz, wr);
     if (box_extent(whole) > split_extent) {
       st_splits += 1;
       const int sp = morton_jump_split<kTaskQ>(key, 0, kTaskQ);
@@ -319,7 +340,7 @@ struct TaskCollector {
         if (lo >= hi) continue;
         const unsigned half = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
         const bool act = active && qi >= lo && qi < hi;
-        const WaveBox hb = make_wave_box(act, qx, qy, qz, bound());
+        const WaveBox hb = make_wave_box(act, qx, qy, qz, wr);
         if (box_extent(hb) > split_extent && hi - lo > 4) {
           st_splits += 1;
           const int s2 = morton_jump_split<kTaskQ>(key, lo, hi);
@@ -335,7 +356,7 @@ struct TaskCollector {
     for (int e = 0; e < nr; ++e) {
       const unsigned em = (unsigned)(rng >> (16 * e)) & 0xffffu;
       if (!__any(active && ((em >> qi) & 1u))) continue;
-      box = make_wave_box(active && ((em >> qi) & 1u), qx, qy, qz, bound());
+      box = make_wave_box(active && ((em >> qi) & 1u), qx, qy, qz, wr);
       walk(c, tl, em);
     }
     tm_walk = (unsigned)__builtin_amdgcn_s_memtime();

@@ -485,6 +485,37 @@ __device__ __forceinline__ unsigned long long xor_min64(unsigned long long v) {
   return umin64(((unsigned long long)a1 << 32) | a0, ((unsigned long long)b1 << 32) | b0);
 }
 
+// squared distance of a (distance, position) key
+__device__ __forceinline__ float key_dist(unsigned long long k) { return __uint_as_float((unsigned)(k >> 32)); }
+// a key names a real point (not a bound without one: position 0xffffffff)
+__device__ __forceinline__ bool key_real(unsigned long long k) { return (unsigned)k != 0xffffffffu; }
+
+// Top-2 merge across lanes l and l ^ M (M = 16 / 32, permlane swaps): k =
+// the smaller key of the two lanes, sd = the smallest distance of every
+// other point either lane holds (both seconds and the larger key).  The two
+// lanes hold disjoint point sets.
+template <int M>
+__device__ __forceinline__ void xor_top2(unsigned long long& k, float& sd) {
+  const unsigned lo = (unsigned)k, hi = (unsigned)(k >> 32), sb = __float_as_uint(sd);
+  unsigned a0, a1, b0, b1, s0, s1;
+  if constexpr (M == 32) {
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const auto rs = __builtin_amdgcn_permlane32_swap(sb, sb, false, false);
+    a0 = rl[0]; b0 = rl[1]; a1 = rh[0]; b1 = rh[1]; s0 = rs[0]; s1 = rs[1];
+  } else {
+    static_assert(M == 16, "xor_top2: M = 16 or 32");
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const auto rs = __builtin_amdgcn_permlane16_swap(sb, sb, false, false);
+    a0 = rl[0]; b0 = rl[1]; a1 = rh[0]; b1 = rh[1]; s0 = rs[0]; s1 = rs[1];
+  }
+  const unsigned long long ka = ((unsigned long long)a1 << 32) | a0, kb = ((unsigned long long)b1 << 32) | b0;
+  const unsigned long long kmax = ka < kb ? kb : ka;
+  sd = fminf(fminf(__uint_as_float(s0), __uint_as_float(s1)), key_dist(kmax));
+  k = umin64(ka, kb);
+}
+
 typedef float f3v __attribute__((ext_vector_type(3)));
 __device__ __forceinline__ f3v ldg3(const float4* p, long i) {
   return ((const __attribute__((address_space(1))) f3v*)(p + i))[0];
