@@ -8,13 +8,17 @@ PKG := dynamic_direct_lidar_odometry_amd
 CSRC := $(PKG)/csrc
 LIBDIR := $(PKG)/_lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
-OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o
+OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o
 
 all: lib oracle facade
 
 lib: $(LIBDIR)/libddlo_gicp.so
 
-$(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/search.hpp $(CSRC)/nn_tasks.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
+$(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/search.hpp $(CSRC)/nn_tasks.hpp $(CSRC)/cov_math.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/knn_tasks.o: $(CSRC)/knn_tasks.hip $(CSRC)/search.hpp $(CSRC)/nn_tasks.hpp $(CSRC)/cov_math.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

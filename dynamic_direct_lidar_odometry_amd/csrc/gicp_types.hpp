@@ -148,4 +148,27 @@ struct AlignJob {
   unsigned* sec;                 // [n_src] fp32 bits: smallest squared distance of an examined non-best point
 };
 
+// Task-based kNN-k of a cloud's own points (covariances, knn_tasks.hip).
+struct KnnJob {
+  CloudDev c;
+  int k;
+  int method;                    // regularisation
+  double* cov6;                  // [n] sym6 per sorted point (output)
+  float4* qstate;                // [n] point (x, y, z) + squared ball bound (>= the k-th neighbour's)
+  unsigned long long* cand;      // [cap][n] candidate (distance, position) keys, slot-major
+  unsigned* cnt;                 // [n] candidates appended (> cap: overflow)
+  int cap;
+  unsigned long long* tasks;     // [kTaskRegions][task_cap_r]
+  unsigned* task_ctr;            // [kTaskRegions * kCtrStride]
+  int task_cap_r;
+  unsigned char* redo;           // [ceil(n / 64)] 1 = recomputed by the lane-per-query kernel
+  unsigned char* again;          // [n] 1 = second round (its candidates overflowed in the first)
+  int round;                     // 1 or 2
+  int* slot2;                    // [n] second-round candidate list of the point
+  unsigned long long* cand2;     // [max2][cap2] second-round candidate keys
+  unsigned* n2;                  // second-round lists handed out
+  int cap2, max2;
+  float split_extent;
+};
+
 }  // namespace ddlo

@@ -23,6 +23,7 @@
 #include "gicp_types.hpp"
 #include "search.hpp"
 #include "nn_tasks.hpp"
+#include "cov_math.hpp"
 #include "launch.hpp"
 
 #include <algorithm>
@@ -219,121 +220,6 @@ __global__ __launch_bounds__(256) void k_level_boxes(const float4* __restrict__ 
 }
 
 // ============================================================================
-// small fp64 linear algebra (per lane)
-// ============================================================================
-// Symmetric 3x3 cyclic Jacobi eigen-decomposition: lam[j], V[j][i] = v_j[i]
-__device__ void sym_eig3(const double A[9], double lam[3], double V[3][3]) {
-  double a00 = A[0], a01 = A[1], a02 = A[2], a11 = A[4], a12 = A[5], a22 = A[8];
-  double v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
-  for (int sweep = 0; sweep < 50; ++sweep) {
-    const double off = fabs(a01) + fabs(a02) + fabs(a12);
-    const double scale = fabs(a00) + fabs(a11) + fabs(a22);
-    if (off <= 1e-300 || off <= scale * 1e-18) break;
-#pragma unroll
-    for (int pq = 0; pq < 3; ++pq) {
-      const int p = pq == 2 ? 1 : 0;
-      const int q = pq == 0 ? 1 : 2;
-      double m[3][3] = {{a00, a01, a02}, {a01, a11, a12}, {a02, a12, a22}};
-      const double apq = m[p][q];
-      if (apq == 0.0) continue;
-      const double theta = (m[q][q] - m[p][p]) / (2.0 * apq);
-      const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-      const double c = 1.0 / sqrt(t * t + 1.0);
-      const double s = t * c;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double akp = m[k][p], akq = m[k][q];
-        m[k][p] = c * akp - s * akq;
-        m[k][q] = s * akp + c * akq;
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double apk = m[p][k], aqk = m[q][k];
-        m[p][k] = c * apk - s * aqk;
-        m[q][k] = s * apk + c * aqk;
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double vkp = v[k][p], vkq = v[k][q];
-        v[k][p] = c * vkp - s * vkq;
-        v[k][q] = s * vkp + c * vkq;
-      }
-      a00 = m[0][0]; a01 = m[0][1]; a02 = m[0][2];
-      a11 = m[1][1]; a12 = m[1][2]; a22 = m[2][2];
-    }
-  }
-  lam[0] = a00; lam[1] = a11; lam[2] = a22;
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) V[j][i] = v[i][j];
-}
-
-// 3x3 inverse by adjugate (general, row-major)
-__device__ __forceinline__ void inv3(const double m[9], double r[9]) {
-  const double c00 = m[4] * m[8] - m[5] * m[7];
-  const double c01 = m[5] * m[6] - m[3] * m[8];
-  const double c02 = m[3] * m[7] - m[4] * m[6];
-  const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
-  const double id = 1.0 / det;
-  r[0] = c00 * id;
-  r[1] = (m[2] * m[7] - m[1] * m[8]) * id;
-  r[2] = (m[1] * m[5] - m[2] * m[4]) * id;
-  r[3] = c01 * id;
-  r[4] = (m[0] * m[8] - m[2] * m[6]) * id;
-  r[5] = (m[2] * m[3] - m[0] * m[5]) * id;
-  r[6] = c02 * id;
-  r[7] = (m[1] * m[6] - m[0] * m[7]) * id;
-  r[8] = (m[0] * m[4] - m[1] * m[3]) * id;
-}
-
-// regularisation of a covariance (nano_gicp_impl.hpp:401-437)
-__device__ void regularize(const double C[9], int method, double out[6]) {
-  double R[9];
-  if (method == 0) {  // NONE
-    for (int i = 0; i < 9; ++i) R[i] = C[i];
-  } else if (method == 4) {  // FROBENIUS: ((C + 1e-3 I)^-1 / ||.||_F)^-1
-    double Cl[9], Ci[9];
-    for (int i = 0; i < 9; ++i) Cl[i] = C[i] + ((i % 4 == 0) ? 1e-3 : 0.0);
-    inv3(Cl, Ci);
-    double nrm = 0;
-    for (int i = 0; i < 9; ++i) nrm += Ci[i] * Ci[i];
-    nrm = sqrt(nrm);
-    for (int i = 0; i < 9; ++i) Ci[i] /= nrm;
-    inv3(Ci, R);
-  } else {  // JacobiSVD route: U diag(vals) V^T with U col = sign(lambda) V col
-    double lam[3], V[3][3];
-    sym_eig3(C, lam, V);
-    // order by |lambda| descending (stable for equal values: index order)
-    int o0 = 0, o1 = 1, o2 = 2;
-    if (fabs(lam[o1]) > fabs(lam[o0])) { int t = o0; o0 = o1; o1 = t; }
-    if (fabs(lam[o2]) > fabs(lam[o1])) {
-      int t = o1; o1 = o2; o2 = t;
-      if (fabs(lam[o1]) > fabs(lam[o0])) { t = o0; o0 = o1; o1 = t; }
-    }
-    const int ord[3] = {o0, o1, o2};
-    double sv[3], vals[3];
-    for (int i = 0; i < 3; ++i) sv[i] = fabs(lam[ord[i]]);
-    if (method == 3) {  // PLANE
-      vals[0] = 1; vals[1] = 1; vals[2] = 1e-3;
-    } else if (method == 1) {  // MIN_EIG
-      for (int i = 0; i < 3; ++i) vals[i] = fmax(sv[i], 1e-3);
-    } else {  // NORMALIZED_MIN_EIG
-      for (int i = 0; i < 3; ++i) vals[i] = fmax(sv[i] / sv[0], 1e-3);
-    }
-    for (int i = 0; i < 9; ++i) R[i] = 0.0;
-    for (int j = 0; j < 3; ++j) {
-      const int oj = ord[j];
-      const double sgn = lam[oj] < 0 ? -1.0 : 1.0;
-      for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) R[3 * r + c] += sgn * V[oj][r] * vals[j] * V[oj][c];
-    }
-  }
-  out[0] = R[0]; out[1] = R[1]; out[2] = R[2];
-  out[3] = R[4]; out[4] = R[5]; out[5] = R[8];
-}
-
-// ============================================================================
 // K2: exact kNN-k (self queries) + covariance
 // ============================================================================
 template <int KCAP, bool EXACT>
@@ -428,13 +314,15 @@ __device__ __forceinline__ void knn_self_search(const CloudDev& c, KnnVisitor<KC
 
 // covariances of a cloud: wave w handles sorted points [64w, 64w+64) (leaves 2w, 2w+1)
 template <int KCAP, bool EXACT>
-__global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int method, double* __restrict__ cov6) {
+__global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int method, double* __restrict__ cov6,
+                                                     const unsigned char* __restrict__ redo) {
   __shared__ WaveLds lds[4];
   WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
   const int ngroups = (c.n + 63) >> 6;
   for (int g = wave; g < ngroups; g += nwaves_total) {
+    if (redo && !redo[g]) continue;   // only the groups the task path could not finish
     const int i = g * 64 + lane_id();
     KnnVisitor<KCAP, EXACT> vis;
     vis.init(k);
@@ -513,11 +401,12 @@ __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __r
   }
 }
 
-template __global__ void k_covariances<10, true>(CloudDev, int, int, double*);
-template __global__ void k_covariances<20, true>(CloudDev, int, int, double*);
-template __global__ void k_covariances<16, false>(CloudDev, int, int, double*);
-template __global__ void k_covariances<32, false>(CloudDev, int, int, double*);
-template __global__ void k_covariances<64, false>(CloudDev, int, int, double*);
+
+template __global__ void k_covariances<10, true>(CloudDev, int, int, double*, const unsigned char*);
+template __global__ void k_covariances<20, true>(CloudDev, int, int, double*, const unsigned char*);
+template __global__ void k_covariances<16, false>(CloudDev, int, int, double*, const unsigned char*);
+template __global__ void k_covariances<32, false>(CloudDev, int, int, double*, const unsigned char*);
+template __global__ void k_covariances<64, false>(CloudDev, int, int, double*, const unsigned char*);
 template __global__ void k_knn_query<1, true>(CloudDev, const float4*, int, int, int*, float*);
 template __global__ void k_knn_query<10, true>(CloudDev, const float4*, int, int, int*, float*);
 template __global__ void k_knn_query<20, true>(CloudDev, const float4*, int, int, int*, float*);
@@ -2210,13 +2099,17 @@ void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int
                         float4* phi) {
   k_level_boxes<<<cdiv(nparent, 4), 256, 0, s>>>(clo, chi, nchild, nparent, plo, phi);
 }
-bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6) {
+static int env_knob(const char* name, int dflt) {   // development knobs (A/B of launch shapes)
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo) {
   const int nb = group_blocks(c.n);
-  if (k == 10) k_covariances<10, true><<<nb, 256, 0, s>>>(c, k, method, cov6);
-  else if (k == 20) k_covariances<20, true><<<nb, 256, 0, s>>>(c, k, method, cov6);
-  else if (k <= 16) k_covariances<16, false><<<nb, 256, 0, s>>>(c, k, method, cov6);
-  else if (k <= 32) k_covariances<32, false><<<nb, 256, 0, s>>>(c, k, method, cov6);
-  else if (k <= 64) k_covariances<64, false><<<nb, 256, 0, s>>>(c, k, method, cov6);
+  if (k == 10) k_covariances<10, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
+  else if (k == 20) k_covariances<20, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
+  else if (k <= 16) k_covariances<16, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
+  else if (k <= 32) k_covariances<32, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
+  else if (k <= 64) k_covariances<64, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
   else return false;
   return true;
 }
@@ -2240,10 +2133,6 @@ void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, con
 void launch_align_init(hipStream_t s, const AlignJob* job) { k_align_init<<<1, 128, 0, s>>>(job); }
 size_t search_lds_bytes(int upper_count) {
   return (size_t)kLinWaves * kCollectLdsBytes + 2 * sizeof(f4v) * (size_t)upper_count;
-}
-static int env_knob(const char* name, int dflt) {   // development knobs (A/B of launch shapes)
-  const char* v = std::getenv(name);
-  return v && *v ? std::atoi(v) : dflt;
 }
 size_t collect_lds_bytes(int upper_count) {
   return (size_t)kLinWaves * kTaskLdsBytes + 2 * sizeof(f4v) * (size_t)upper_count;

@@ -18,7 +18,12 @@ void launch_leaf_boxes(hipStream_t s, const float4* pts, int n, int nleaves, flo
 void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int nchild, int nparent, float4* plo,
                         float4* phi);
 // returns false if k is unsupported (> 64)
-bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6);
+// redo: nullptr = every point, else only the 64-point groups flagged 1
+bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo);
+// task-based kNN-k covariances (knn_tasks.hip), k <= 32; groups it flags in
+// j.redo must then be recomputed with launch_covariances(..., j.redo)
+bool launch_knn_covariances(hipStream_t s, const KnnJob& j, int tgt_upper);
+int knn_task_cap_per_region(int n);
 bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq, int k, int* out_idx, float* out_d);
 void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6);
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);

@@ -121,6 +121,10 @@ struct TaskCollector {
   unsigned st_blocks = 0, st_tasks = 0, st_inline = 0, st_splits = 0;
   unsigned tm_walk = 0;   // s_memtime after the walk (diagnostics)
   unsigned st_iters = 0;
+  bool knn = false;        // kNN-k mode (knn_tasks.hip): a full region is an overflow, no inline scan
+  bool ovf = false;
+  int nfull = 0;           // kNN mode: leaves < nfull hold 32 real points
+  float tight = INFINITY;  // kNN mode: min over tested full leaves of the farthest-corner distance (squared)
 
   __device__ __forceinline__ float bound() const { return __uint_as_float((unsigned)(bk >> 32)); }
 
@@ -134,16 +138,21 @@ struct TaskCollector {
     if (lane == 0) base = (int)atomicAdd(tl.ctr + r * kCtrStride, (unsigned)n);
     base = __builtin_amdgcn_readfirstlane(base);
     // the slots that fit are published; the rest (region full) are scanned
-    // right here into the lane's own key (exact either way)
+    // right here into the lane's own key (exact either way) — in kNN mode
+    // the sub-group is flagged instead and recomputed by the fallback kernel
     const int fit = max(0, min(n, tl.cap_r - base));
     unsigned long long* dst = tl.tasks + (size_t)r * tl.cap_r + base;
     for (int k = lane; k < fit; k += 64) dst[k] = L->tasks[k];
     st_tasks += fit;
-    for (int k = fit; k < n; ++k) {
-      const unsigned long long t = L->tasks[k];
-      float sd2;
-      const unsigned long long k2 = scan_leaf16(c, (int)(t >> 40), qx, qy, qz, sd2);
-      if (active && ((t >> (lane & 15)) & 1ull)) fold_top2(bk, sec, k2, sd2);
+    if (knn) {
+      ovf = ovf || fit < n;
+    } else {
+      for (int k = fit; k < n; ++k) {
+        const unsigned long long t = L->tasks[k];
+        float sd2;
+        const unsigned long long k2 = scan_leaf16(c, (int)(t >> 40), qx, qy, qz, sd2);
+        if (active && ((t >> (lane & 15)) & 1ull)) fold_top2(bk, sec, k2, sd2);
+      }
     }
     st_inline += n - fit;
     __builtin_amdgcn_wave_barrier();
@@ -171,6 +180,20 @@ struct TaskCollector {
             m16 |= 1u << k;
         }
       }
+      if (knn) {   // per query: the nearest full leaf's farthest corner bounds its k-th neighbour
+        unsigned qm = qmask;
+        while (qm) {
+          const int k = __builtin_ctz(qm);
+          qm &= qm - 1;
+          float v = INFINITY;
+          if (lane < cm && L->sb_leaf[lane] < nfull) {
+            const f4v qk = L->q[k];
+            v = box_maxdist2(qk.x, qk.y, qk.z, L->sb_lo[lane], L->sb_hi[lane]);
+          }
+          v = wave_min(v);
+          if ((lane & 15) == k) tight = fminf(tight, v);
+        }
+      }
       const unsigned long long lm = __ballot(m16 != 0u);
       const int cl = __popcll(lm);
       if (cl == 0) return;
@@ -193,6 +216,7 @@ struct TaskCollector {
         const f4v blo = L->sb_lo[li], bhi = L->sb_hi[li];
         need = qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, make_float4(blo.x, blo.y, blo.z, 0.f),
                                         make_float4(bhi.x, bhi.y, bhi.z, 0.f)) <= qk.w;
+        if (knn && L->sb_leaf[li] < nfull) tight = fminf(tight, box_maxdist2(qk.x, qk.y, qk.z, blo, bhi));
       }
       const unsigned long long bal = __ballot(need);
       const unsigned m16 = (unsigned)((bal >> (lane & ~15)) & 0xffffull);

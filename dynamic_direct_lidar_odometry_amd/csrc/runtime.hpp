@@ -203,7 +203,7 @@ struct gicp_ctx {
   gicp_params params{};
   Side src, tgt;
   // build scratch
-  DevBuf raw_bytes, raw_pts, partial, nonfinite, keys_tmp, vals_tmp, sort_tmp;
+  DevBuf raw_bytes, raw_pts, partial, nonfinite, keys_tmp, vals_tmp, sort_tmp, knn;
   // align buffers
   DevBuf corr, sqd, slab, job_dev, state_dev, tmp_out, stats;
   bool stats_on = false;
@@ -339,8 +339,73 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side) {
   auto cv = std::make_shared<CovData>();
   cv->n = side.cloud->n;
   HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * (size_t)cv->n));
-  if (!launch_covariances(c->stream, side.cloud->dev(), k, c->params.regularization, cv->cov6.as<double>()))
+  // DDLO_COV_TASKS=1: the task-based kNN (knn_tasks.hip) — exact, but not
+  // faster than the lane-per-query kernel on the cfg 5 clouds
+  static const bool tasks = [] {
+    const char* v = std::getenv("DDLO_COV_TASKS");
+    return v && *v == '1';
+  }();
+  const CloudDev cd = side.cloud->dev();
+  if (tasks && k <= 32) {
+    // scratch of the task-based kNN; a queued covariance launch may still
+    // read the old block, so growing it waits for the stream
+    const int n = cv->n;
+    const int cap = std::max(64, 6 * k);
+    const int cap2 = 8 * cap, max2 = std::max(256, n / 64);   // second round: ~1 % of the points, longer lists
+    const int cap_r = knn_task_cap_per_region(n);
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t o_q = 0, o_cnt = o_q + al(sizeof(float4) * ((size_t)(n + 15) / 16 * 16)),
+                 o_redo = o_cnt + al(sizeof(unsigned) * (size_t)n), o_again = o_redo + al((size_t)(n + 63) / 64),
+                 o_slot2 = o_again + al((size_t)n), o_n2 = o_slot2 + al(sizeof(int) * (size_t)n),
+                 o_ctr = o_n2 + 256,
+                 o_tasks = o_ctr + al(sizeof(unsigned) * kTaskRegions * kCtrStride),
+                 o_cand = o_tasks + al(sizeof(unsigned long long) * (size_t)kTaskRegions * cap_r),
+                 o_cand2 = o_cand + al(sizeof(unsigned long long) * (size_t)n * cap),
+                 total = o_cand2 + sizeof(unsigned long long) * (size_t)max2 * cap2;
+    if (total > c->knn.bytes) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(c->knn.ensure(total));
+    }
+    char* u = c->knn.as<char>();
+    KnnJob j;
+    j.c = cd;
+    j.k = k;
+    j.method = c->params.regularization;
+    j.cov6 = cv->cov6.as<double>();
+    j.qstate = reinterpret_cast<float4*>(u + o_q);
+    j.cnt = reinterpret_cast<unsigned*>(u + o_cnt);
+    j.redo = reinterpret_cast<unsigned char*>(u + o_redo);
+    j.again = reinterpret_cast<unsigned char*>(u + o_again);
+    j.round = 1;
+    j.slot2 = reinterpret_cast<int*>(u + o_slot2);
+    j.n2 = reinterpret_cast<unsigned*>(u + o_n2);
+    j.cand2 = reinterpret_cast<unsigned long long*>(u + o_cand2);
+    j.cap2 = cap2;
+    j.max2 = max2;
+    j.task_ctr = reinterpret_cast<unsigned*>(u + o_ctr);
+    j.tasks = reinterpret_cast<unsigned long long*>(u + o_tasks);
+    j.cand = reinterpret_cast<unsigned long long*>(u + o_cand);
+    j.cap = cap;
+    j.task_cap_r = cap_r;
+    j.split_extent = 5.0f;
+    if (!launch_knn_covariances(c->stream, j, side.cloud->upper_count()))
+      return fail(GICP_EINVAL, "unsupported k");
+    launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), j.redo);
+    if (std::getenv("DDLO_COV_DEBUG")) {   // development: how many groups needed the fallback
+      std::vector<unsigned char> r((n + 63) / 64);
+      std::vector<unsigned> cn(n);
+      HIP_TRY(hipMemcpyAsync(r.data(), j.redo, r.size(), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipMemcpyAsync(cn.data(), j.cnt, sizeof(unsigned) * n, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      size_t nr = 0, over = 0, sum = 0, mx = 0;
+      for (auto v : r) nr += v;
+      for (auto v : cn) { over += v > (unsigned)cap; sum += v; mx = std::max<size_t>(mx, v); }
+      std::fprintf(stderr, "[cov] n %d k %d redo groups %zu / %zu, points over cap %zu, mean cand %.1f max %zu\n", n, k,
+                   nr, r.size(), over, (double)sum / n, mx);
+    }
+  } else if (!launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), nullptr)) {
     return fail(GICP_EINVAL, "unsupported k");
+  }
   HIP_TRY(hipGetLastError());
   side.cov = cv;
   return GICP_OK;

@@ -667,6 +667,16 @@ __device__ __forceinline__ void fill_upper(const CloudDev& c, f4v* U) {
   }
 }
 
+// Squared distance from q to the farthest corner of a box: an upper bound on
+// the fp32 squared distance to every point inside (same operation order as
+// dist2(), each axis term at least the point's).
+__device__ __forceinline__ float box_maxdist2(float qx, float qy, float qz, f4v lo, f4v hi) {
+  const float dx = fmaxf(fabsf(qx - lo.x), fabsf(qx - hi.x));
+  const float dy = fmaxf(fabsf(qy - lo.y), fabsf(qy - hi.y));
+  const float dz = fmaxf(fabsf(qz - lo.z), fabsf(qz - hi.z));
+  return (dx * dx + dy * dy) + dz * dz;
+}
+
 __device__ __forceinline__ bool box_overlap_v(const WaveBox& w, f4v lo, f4v hi) {
   return lo.x <= w.hx && hi.x >= w.lx && lo.y <= w.hy && hi.y >= w.ly && lo.z <= w.hz && hi.z >= w.lz;
 }
