@@ -341,10 +341,8 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side) {
   HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * (size_t)cv->n));
   // DDLO_COV_TASKS=1: the task-based kNN (knn_tasks.hip) — exact, but not
   // faster than the lane-per-query kernel on the cfg 5 clouds
-  static const bool tasks = [] {
-    const char* v = std::getenv("DDLO_COV_TASKS");
-    return v && *v == '1';
-  }();
+  const char* tv = std::getenv("DDLO_COV_TASKS");
+  const bool tasks = tv && *tv == '1';
   const CloudDev cd = side.cloud->dev();
   if (tasks && k <= 32) {
     // scratch of the task-based kNN; a queued covariance launch may still

@@ -57,6 +57,27 @@ def test_covariances_other_k_vs_oracle(s2s_golden, k):
     assert_cov_parity(src, k, c.get_covariances(TARGET), O.covariances(src, k))
 
 
+@pytest.mark.parametrize("k", [10, 20, 7, 32])
+def test_covariances_task_knn_matches(s2s_golden, k, monkeypatch):
+    """The opt-in task-based kNN (knn_tasks.hip, DDLO_COV_TASKS=1) is exact:
+    bit-identical covariances to the lane-per-query kernel, on the ray-cast
+    scan (dense near range, sparse far range: exercises the second round)
+    and on a sparse random cloud with exact ties (integer lattice)."""
+    rng = np.random.default_rng(7)
+    lattice = rng.integers(0, 40, size=(20000, 3)).astype(np.float32)
+    for cloud in (s2s_golden["src"], lattice):
+        out = []
+        for flag in ("0", "1"):
+            monkeypatch.setenv("DDLO_COV_TASKS", flag)
+            c = P.Context(0)
+            c.set_params(P.default_params(k_correspondences=k))
+            c.set_target(cloud)
+            c.compute_covariances(TARGET)
+            out.append(c.get_covariances(TARGET))
+            c.close()
+        np.testing.assert_array_equal(out[0], out[1])
+
+
 def test_covariance_layouts_roundtrip(s2s_golden):
     g = s2s_golden
     c = P.Context(0)

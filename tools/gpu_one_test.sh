@@ -1,0 +1,2 @@
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_gicp.py -k "task_knn" -x -q --timeout 200 --timeout-method thread 2>&1 | tail -5
