@@ -79,7 +79,8 @@ struct AlignState {
   int have_prev;         // correspondences of a previous linearize are valid
   int rec;               // the next search records reuse references (AlignJob::ref)
   float src_radius;      // max |p| over the source cloud's root boxes (reuse step bound)
-  int pad[2];
+  int any_rec;           // an iteration of this align recorded references
+  int pad[1];
 };
 
 // Everything a kernel needs for one align, written by the host before launch.

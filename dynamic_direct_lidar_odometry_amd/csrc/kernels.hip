@@ -599,6 +599,7 @@ __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__
     if (threadIdx.x == 0) {
       st->src_radius = r;
       st->rec = job->reuse && job->reuse_rec0;
+      st->any_rec = 0;
     }
   }
   if (threadIdx.x == 0) {
@@ -664,7 +665,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
   for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
   const int reuse = job->reuse;
-  const bool check_ref = reuse && have_prev;
+  const bool check_ref = reuse && have_prev && st->any_rec;   // references exist only after a recording iteration
   const int rec = st->rec;   // this search records references
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -717,7 +718,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       if (inrange && lane < Q) {
         keyout[i] = passed ? pass_key : dkey(INFINITY, -1);
         qstate[i] = make_float4(qx, qy, qz, -1.f);
-        if (reuse && !have_prev) job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);   // not searched: no reference
+        if (reuse && !have_prev) job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);   // a new align: no reference yet
       }
       if (lane == 0) {
         job->hard_flag[g] = 2;   // nothing to search: k_nn_collect skips the sub-group
@@ -871,7 +872,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     if (inrange && lane < Q) {
       qstate[i] = make_float4(qx, qy, qz, active ? wr : -1.f);
       keyout[i] = active ? dkey(vis.best, vis.bestj) : passed ? pass_key : dkey(INFINITY, -1);
-      if (reuse && !have_prev && !active) job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);
+      if (reuse && !have_prev) job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);   // a new align: no reference yet
     }
     // hard sub-group: a wide union box (a query far from every target point
     // drags many blocks into the walk) -> listed, walked first
@@ -1130,29 +1131,42 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
         // lane's points come in increasing position, so strict < keeps the
         // lowest position among equal distances
         const f2v qx2 = {q.x, q.x}, qy2 = {q.y, q.y}, qz2 = {q.z, q.z};
-        float bd = INFINITY, sd = INFINITY;
-        int bh = 0;
+        f2v d[4];
 #pragma unroll
         for (int h = 0; h < 8; h += 2) {
           const f2v dx = qx2 - f2v{X[h], X[h + 1]};
           const f2v dy = qy2 - f2v{Y[h], Y[h + 1]};
           const f2v dz = qz2 - f2v{Z[h], Z[h + 1]};
-          const f2v d = (dx * dx + dy * dy) + dz * dz;
-          if (d.x < bd) { sd = bd; bd = d.x; bh = h; } else { sd = fminf(sd, d.x); }
-          if (d.y < bd) { sd = bd; bd = d.y; bh = h + 1; } else { sd = fminf(sd, d.y); }
+          d[h / 2] = (dx * dx + dy * dy) + dz * dz;
         }
-        unsigned long long bk = dkey(bd, (int)(t >> 40) * kLeafSize + s * 8 + bh);
-        if (reuse) {
+        const bool on = ((t >> qi) & 1ull) != 0ull;
+        const int pos0 = (int)(t >> 40) * kLeafSize + s * 8;
+        if (reuse) {   // recording search: the leaf's best key and second distance (uniform branch)
+          float bd = INFINITY, sd = INFINITY;
+          int bh = 0;
+#pragma unroll
+          for (int h = 0; h < 8; ++h) {
+            const float dh = (h & 1) ? d[h / 2].y : d[h / 2].x;
+            if (dh < bd) { sd = bd; bd = dh; bh = h; } else { sd = fminf(sd, dh); }
+          }
+          unsigned long long bk = dkey(bd, pos0 + bh);
           xor_top2<16>(bk, sd);
           xor_top2<32>(bk, sd);
+          if (on) fold_top2(acc, acc2, bk, sd);
         } else {
+          float bd = INFINITY;
+          int bh = 0;
+#pragma unroll
+          for (int h = 0; h < 8; ++h) {
+            const float dh = (h & 1) ? d[h / 2].y : d[h / 2].x;
+            if (dh < bd) { bd = dh; bh = h; }
+          }
+          unsigned long long bk = dkey(bd, pos0 + bh);
           bk = xor_min64<16>(bk);
           bk = xor_min64<32>(bk);
+          if (on) acc = umin64(acc, bk);
         }
-        if (((t >> qi) & 1ull) != 0ull) {
-          fold_top2(acc, acc2, bk, sd);
-          run_bound = q.w;
-        }
+        if (on) run_bound = q.w;
       }
       __builtin_amdgcn_wave_barrier();   // reads of `cur` done before it is refilled
     }
@@ -1389,8 +1403,7 @@ __global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ j
   const auto sqd = gpw(job->sqd);
   const auto slab = gpw(job->slab);
   const double max_corr2 = job->max_corr2;
-  const int reuse = job->reuse;
-  const int rec = st->rec;
+  const int rec = st->rec;   // this iteration records reuse references
   double R[9], t[3];
   for (int e = 0; e < 9; ++e) R[e] = st->R[e];
   for (int e = 0; e < 3; ++e) t[e] = st->t[e];
@@ -1416,14 +1429,15 @@ __global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ j
       j = (kj != 0xffffffffu && (double)kd < max_corr2) ? (int)kj : -1;
       corr[i] = j;
       sqd[i] = kj != 0xffffffffu ? kd : INFINITY;
-      // reuse reference of a query searched in this iteration: its position,
-      // B^2 = min(smallest distance of an examined non-best point, walk
-      // radius) — every unexamined point lies in a leaf farther than the
-      // walk radius — and its match
-      if (reuse) {
+      // reuse reference of a query searched in a recording iteration: its
+      // position, B^2 = min(smallest distance of an examined non-best point,
+      // walk radius) — every unexamined point lies in a leaf farther than the
+      // walk radius — and its match.  A reference stays a valid proof for
+      // the rest of the align (same target), so other iterations keep it.
+      if (rec) {
         const float4 qs = ldg4(job->qstate, i);
         if (qs.w >= 0.f) {
-          job->ref[i] = make_float4(qs.x, qs.y, qs.z, rec ? fminf(__uint_as_float(job->sec[i]), qs.w) : -1.f);
+          job->ref[i] = make_float4(qs.x, qs.y, qs.z, fminf(__uint_as_float(job->sec[i]), qs.w));
           float4 pp = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
           if (kj != 0xffffffffu) {
             const float4 p = ldg4(tgt.pts, (int)kj);
@@ -1898,6 +1912,7 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
       st->lambda = tr_lambda[ntr - 1] * 2.0;  // not observable: the align ends
     }
   }
+  if (st->rec) st->any_rec = 1;   // this iteration's search recorded references
   int rec = job->reuse;
   if (accept) {
     double Rn[9], tn[3];

@@ -1,11 +1,12 @@
-"""Per-launch HBM-side traffic of the linearize (k_nn_search + k_moments) from
+"""Per-launch HBM-side traffic of the linearize (k_nn_seed + k_nn_collect +
+k_nn_scan + k_moments, or the single-kernel k_nn_search + k_moments) from
 two rocprofv3 --pmc passes over bench.py (FETCH_SIZE, WRITE_SIZE; kB units).
 
 Corrections (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports
 half of the bytes of wide coalesced reads -> doubled here; WRITE_SIZE is
 taken as reported.  Both count L2 -> fabric requests, i.e. Infinity-Cache
 hits are included (upper bound of the HBM bytes).  Active iterations only:
-a search dispatch whose kernel ran >= 20 us (no-op iterations exit at once).
+search dispatches that together ran >= 20 us (no-op iterations exit at once).
 
 usage: python tools/pmc_traffic.py fetch.csv write.csv [out.json]
 """
@@ -14,23 +15,27 @@ import json
 import sys
 
 
+SEARCH = ("k_nn_seed", "k_nn_collect", "k_nn_scan", "k_nn_search")
+
+
 def per_iteration(path, counter):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     out = []
-    pend = None
+    val_s, dur_s = 0.0, 0.0
     for r in rows:
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
         dur_us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         val = float(r["Counter_Value"]) * 1024.0  # kB -> bytes
-        if "k_nn_search" in name:
-            pend = (val, dur_us)
-        elif "k_moments" in name and pend is not None:
-            if pend[1] >= 20.0:
-                out.append((pend[0], val))
-            pend = None
+        if any(k in name for k in SEARCH):
+            val_s += val
+            dur_s += dur_us
+        elif "k_moments" in name:
+            if dur_s >= 20.0:
+                out.append((val_s, val))
+            val_s, dur_s = 0.0, 0.0
     return out
 
 
