@@ -12,15 +12,20 @@ One step = one align() (NanoGICP::computeTransformation), index build and
 covariances excluded (SURVEY.md §8(d) "ms/scan").  value = outer GICP
 iterations per second over the whole job (all ranks); ms_per_step = ms/scan.
 
-Multi-GPU (torchrun, one process per GPU): the path does not shard in this
-round (SURVEY.md §8(e) spatial sharding is future work), so every rank runs
-an independent replica on its own GPU (weak scaling, no data-path
-collective); torch.distributed is used for the barrier and max-time only.
+Multi-GPU (torchrun, one process per GPU): the headline runs an independent
+replica per GPU (weak scaling, no data-path collective); torch.distributed is
+used for the barrier and max-time / sum-work only.  Extra legs in the same
+JSON line: s2s_gn (cfg 2, 20 fixed GN iterations), sharded_s2m (cfg 4,
+spatial shards + one RCCL all-reduce per iteration), batched_s2s (cfg 5
+frame-parallel S2S) and odometry (cfg 5 S2M chain through the ddlo_odom
+driver, one independent chain per rank's frame segment).
 
-Roofline: the linearize step (k_nn_search + k_moments, launched back to back
-per outer iteration) timed with HIP events on the library's stream inside
-this process; algorithmic bytes per launch = 76 * N_s (SURVEY.md §8(d)
-B_lin), peak HBM 8 TB/s (MI355X_MICROARCH.md).  cpu_baseline = the C++/OpenMP
+Roofline: the linearize step (k_nn_seed + k_nn_collect + k_nn_scan +
+k_moments, launched back to back per outer iteration) timed with HIP events
+on the library's stream inside this process; algorithmic bytes per launch =
+76 * N_s (SURVEY.md §8(d) B_lin), peak HBM 8 TB/s (MI355X_MICROARCH.md);
+traffic = HBM-side bytes per launch from the committed rocprofv3 --pmc
+passes (profiles/r02_traffic.json).  cpu_baseline = the C++/OpenMP
 oracle (oracle/cpu_ref.cpp, a restatement of the reference algorithm, "port")
 timed on this host on the same problem.
 """
