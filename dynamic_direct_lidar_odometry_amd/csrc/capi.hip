@@ -178,7 +178,8 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   return GICP_OK;
 }
 
-int linearize_blocks(int nsrc) { return moment_blocks(nsrc); }
+int linearize_blocks(int nsrc) { return linearize_geometry(nsrc, 0).mom_blocks; }   // slab rows
+LinGeom geometry(const gicp_ctx* c) { return linearize_geometry(c->src.cloud->n, c->tgt.cloud->upper_count()); }
 
 gicp_status prepare_align(gicp_ctx* c) {
   if (!c->src.cloud) return fail(GICP_ENOSOURCE, "no source cloud");
@@ -222,7 +223,8 @@ constexpr int kMaxFirstChunk = 8;  // largest predicted first chunk (iterations)
 // RCCL: H, b, cost and the LM trial-cost moments in one collective), then
 // the LM/GN step, replicated bit-identically on every rank.
 gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks) {
-  launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
+  (void)nblocks;   // = geometry(c).mom_blocks (fill_job)
+  launch_linearize(c->stream, jd, geometry(c));
   if (c->comm) {
     launch_mom_reduce(c->stream, jd);
     NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
@@ -268,7 +270,7 @@ void drop_graphs(gicp_ctx* c) {
   c->g_first.clear();
   drop_pair(c->g_rest[0]);
   drop_pair(c->g_rest[1]);
-  c->graph_key = std::make_tuple(-1, -1, nullptr);
+  c->graph_key.fill(-1);
 }
 
 // Launch the align as a first chunk of n outer iterations (n = the previous
@@ -281,8 +283,11 @@ void drop_graphs(gicp_ctx* c) {
 // of the chunk after which the state is final.
 gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chunk) {
   const void* jd = c->job_dev.p;
-  // key: grid, job buffer and whether RCCL is in the chunk
-  auto key = std::make_tuple(c->comm ? -1 : 1, nblocks, jd);
+  // key: whether RCCL is in the chunk, the job buffer and the launch geometry
+  const LinGeom g = geometry(c);
+  (void)nblocks;   // = g.mom_blocks
+  const std::array<long long, 7> key{{c->comm ? 1 : 0, (long long)(uintptr_t)jd, g.seed_blocks, g.collect_blocks,
+                                      g.scan_blocks, g.mom_blocks, g.lds_boxes}};
   const bool use_graph = !c->comm || c->comm_graphs;
   const int first = std::max(1, std::min({c->predicted_iters, max_it, kMaxFirstChunk}));
   if (use_graph && c->graph_key != key) {
@@ -372,7 +377,7 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
   launch_align_init(c->stream, jd);
   for (int i = 0; i < max_it; ++i) {
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i], c->stream));
-    launch_linearize(c->stream, jd, c->src.cloud->n, nblocks, c->tgt.cloud->upper_count());
+    launch_linearize(c->stream, jd, geometry(c));
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i + 1], c->stream));
     if (c->comm) {
       launch_mom_reduce(c->stream, jd);

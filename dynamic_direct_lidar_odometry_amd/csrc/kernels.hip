@@ -2170,23 +2170,36 @@ bool search_uses_tasks() {
   }();
   return !old_search;
 }
-void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int job_upper_count) {
-  const int search_groups = (nsrc + kSearchQ - 1) / kSearchQ;
-  const int sb = std::max(1, (search_groups + kLinWaves - 1) / kLinWaves);
+// Bucketed launch geometry: scans of similar size (cfg 5: +-1k points per
+// frame) share one captured chunk graph, and a graph never runs with a grid
+// or LDS size smaller than the clouds need (all of it is in the graph key).
+LinGeom linearize_geometry(int nsrc, int tgt_upper) {
+  LinGeom g;
+  const int groups = cdiv(std::max(nsrc, 1), kSearchQ);
+  const int gcap = cdiv(groups, 1024) * 1024;                    // 16k-point steps
+  g.seed_blocks = gcap / kLinWaves;                               // grid-stride kernel: any grid is exact
+  g.collect_blocks = (gcap + kHardMax) / kLinWaves;               // one wave per sub-group: >= the groups
+  g.scan_blocks = scan_blocks(gcap * kSearchQ);                   // any grid is exact
+  g.mom_blocks = moment_blocks(cdiv(std::max(nsrc, 1), 4096) * 4096);   // grid-stride; = the slab rows
+  g.lds_boxes = std::min(2048, cdiv(std::max(tgt_upper, 1), 128) * 128);   // >= the target's upper boxes
+  return g;
+}
+
+void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
   if (!search_uses_tasks()) {
-    k_nn_search<kSearchQ, 3><<<sb, 64 * kLinWaves, search_lds_bytes(job_upper_count), s>>>(job);
+    k_nn_search<kSearchQ, 3><<<g.seed_blocks, 64 * kLinWaves, search_lds_bytes(g.lds_boxes), s>>>(job);
   } else {
     static const int occ_seed = env_knob("DDLO_OCC_SEED", 4), occ_col = env_knob("DDLO_OCC_COLLECT", 3),
                      occ_scan = env_knob("DDLO_OCC_SCAN", 4);
-    if (occ_seed == 6) k_nn_seed<6><<<sb, 64 * kLinWaves, 0, s>>>(job);
-    else k_nn_seed<4><<<sb, 64 * kLinWaves, 0, s>>>(job);
-    const int cb = (search_groups + kHardMax + kLinWaves - 1) / kLinWaves;
-    if (occ_col == 4) k_nn_collect<4><<<cb, 64 * kLinWaves, collect_lds_bytes(job_upper_count), s>>>(job);
-    else k_nn_collect<3><<<cb, 64 * kLinWaves, collect_lds_bytes(job_upper_count), s>>>(job);
-    if (occ_scan == 6) k_nn_scan<6><<<scan_blocks(nsrc), 64 * kScanWaves, 0, s>>>(job);
-    else k_nn_scan<4><<<scan_blocks(nsrc), 64 * kScanWaves, 0, s>>>(job);
+    if (occ_seed == 6) k_nn_seed<6><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);
+    else k_nn_seed<4><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);
+    const size_t lds = collect_lds_bytes(g.lds_boxes);
+    if (occ_col == 4) k_nn_collect<4><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
+    else k_nn_collect<3><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
+    if (occ_scan == 6) k_nn_scan<6><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
+    else k_nn_scan<4><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
   }
-  k_moments<<<nblocks, 64 * kMomWaves, 0, s>>>(job);
+  k_moments<<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
 }
 int search_queries_per_wave() { return kSearchQ; }
 int task_cap_per_region(int nsrc) {

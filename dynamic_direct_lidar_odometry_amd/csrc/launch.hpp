@@ -29,7 +29,13 @@ void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);
 void launch_align_init(hipStream_t s, const AlignJob* job);
 // tgt_upper: number of upper-level (>= 1) boxes of the target (LDS cache size)
-void launch_linearize(hipStream_t s, const AlignJob* job, int nsrc, int nblocks, int tgt_upper);
+// Launch geometry of one linearize (grids, upper-box LDS cache), bucketed by
+// cloud size; part of the chunk-graph key.
+struct LinGeom {
+  int seed_blocks, collect_blocks, scan_blocks, mom_blocks, lds_boxes;
+};
+LinGeom linearize_geometry(int nsrc, int tgt_upper);
+void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g);
 int search_queries_per_wave();
 bool search_uses_tasks();   // false under DDLO_SEARCH=collect (the single-kernel search)
 int task_cap_per_region(int nsrc);   // task-list slots per region for nsrc source points
@@ -50,11 +56,13 @@ void launch_pack4(hipStream_t s, const unsigned char* raw, size_t stride, int n,
 int crop_box(hipStream_t s, const float4* in, int n, float size, float4* out, int* keep, int* pos, void* tmp,
              size_t tmp_bytes, int* count_host);
 size_t crop_box_tmp_bytes(int n);
+// crop > 0: the crop box (points inside [-crop, crop]^3 removed) folded into the same pass
 int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, int* scratch, void* tmp, size_t tmp_bytes,
-               int* count_host);
+               int* count_host, float crop);
 size_t voxel_tmp_bytes(int n);
 constexpr size_t voxel_scratch_ints(int n) { return 7 * (size_t)n + 16 + 6 * 64; }
-float median_range(hipStream_t s, const float4* in, int n, float* d, float* d_sorted, void* tmp, size_t tmp_bytes);
+void median_range_async(hipStream_t s, const float4* in, int n, float* d, float* d_sorted, void* tmp, size_t tmp_bytes,
+                        float* out);
 size_t median_tmp_bytes(int n);
 void launch_transform4(hipStream_t s, const float4* pts, const int* perm, int n, const float* T12, float4* out);
 void launch_gather_cov6(hipStream_t s, const double* cov_sorted, const int* perm, int n, double* out);

@@ -27,6 +27,9 @@
 // past the end, :986).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+
 #include <algorithm>
 #include <array>
 #include <cfloat>
@@ -362,6 +365,11 @@ struct ddlo_odom {
   hipStream_t s = nullptr;
   // scratch (device)
   DevBuf up, a, b, keep, pos, vscratch, cubtmp, rng, rng_sorted, cat_pts, cat_cov;
+  float* median_pin = nullptr;   // pinned: the median range of the current scan
+  // DDLO_ODOM_TIMING=1: host wall time per phase, printed at destroy (development)
+  bool timing = false;
+  double t_phase[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long frames = 0;
   // state
   bool have_target = false;
   float T[16], T_s2s[16], T_s2s_prev[16];
@@ -392,6 +400,23 @@ gicp_status preprocess(ddlo_odom* o, int n, bool crop, double crop_size, bool vo
   gicp_status st = ensure_tmp(o, std::max(n, 1));
   if (st) return st;
   int m = n;
+  if (crop && vox && m > 0) {
+    // one pass: the voxel filter over the points the crop box keeps (their
+    // bbox, their input order), one count read-back instead of two
+    int c = 0;
+    if (voxel_grid(o->s, o->a.as<float4>(), m, (float)leaf, o->b.as<float4>(), o->vscratch.as<int>(), o->cubtmp.p,
+                   o->cubtmp.bytes, &c, (float)crop_size))
+      return fail(GICP_EHIP, "voxel filter scratch too small");
+    if (c >= 0) {
+      *nout = c;
+      std::swap(o->a.p, o->b.p);
+      std::swap(o->a.bytes, o->b.bytes);
+      HIP_TRY(hipGetLastError());
+      return GICP_OK;
+    }
+    // grid overflow: the reference keeps the cropped cloud unchanged -> crop alone below
+    vox = false;
+  }
   if (crop && m > 0) {
     if (crop_box(o->s, o->a.as<float4>(), m, (float)crop_size, o->b.as<float4>(), o->keep.as<int>(), o->pos.as<int>(),
                  o->cubtmp.p, o->cubtmp.bytes, &m))
@@ -402,7 +427,7 @@ gicp_status preprocess(ddlo_odom* o, int n, bool crop, double crop_size, bool vo
   if (vox && m > 0) {
     int c = 0;
     if (voxel_grid(o->s, o->a.as<float4>(), m, (float)leaf, o->b.as<float4>(), o->vscratch.as<int>(), o->cubtmp.p,
-                   o->cubtmp.bytes, &c))
+                   o->cubtmp.bytes, &c, 0.f))
       return fail(GICP_EHIP, "voxel filter scratch too small");
     if (c >= 0) {  // -1: grid overflow, the reference keeps the cloud unchanged
       m = c;
@@ -415,10 +440,12 @@ gicp_status preprocess(ddlo_odom* o, int n, bool crop, double crop_size, bool vo
   return GICP_OK;
 }
 
-// device cloud from float4 points
-gicp_status cloud_from(ddlo_odom* o, gicp_ctx* c, const float4* pts, int n, std::shared_ptr<CloudData>* out) {
+// device cloud from float4 points; `finite`: the points are known finite (a
+// voxel filter's output, keyframes, the submap), no read-back of the check
+gicp_status cloud_from(ddlo_odom* o, gicp_ctx* c, const float4* pts, int n, std::shared_ptr<CloudData>* out,
+                       bool finite) {
   (void)o;
-  return build_cloud(c, reinterpret_cast<const float*>(pts), (size_t)n, sizeof(float4), out, true);
+  return build_cloud(c, reinterpret_cast<const float*>(pts), (size_t)n, sizeof(float4), out, true, !finite);
 }
 
 // keyframe = world-frame copy of the (preprocessed) scan cloud, submap voxel
@@ -440,7 +467,7 @@ gicp_status make_keyframe(ddlo_odom* o, const std::shared_ptr<CloudData>& scan) 
   HIP_TRY(kf->pts.ensure(sizeof(float4) * (size_t)m));
   HIP_TRY(hipMemcpyAsync(kf->pts.p, o->a.p, sizeof(float4) * (size_t)m, hipMemcpyDeviceToDevice, o->s));
   Side side;
-  st = cloud_from(o, o->s2s, kf->pts.as<float4>(), m, &side.cloud);
+  st = cloud_from(o, o->s2s, kf->pts.as<float4>(), m, &side.cloud, true);
   if (st) return st;
   st = compute_cov(o->s2s, side);   // s2s->params: the S2S k (gicp_s2s_.calculateSourceCovariances)
   if (st) return st;
@@ -487,24 +514,27 @@ gicp_status submap_keyframes(ddlo_odom* o, bool* changed) {
   if (total > INT32_MAX / 2) return fail(GICP_EINVAL, "submap too large");
   HIP_TRY(o->cat_pts.ensure(sizeof(float4) * (size_t)total));
   HIP_TRY(o->cat_cov.ensure(sizeof(double) * 6 * (size_t)total));
+  // everything of the submap build runs on the S2M context's stream: the
+  // concatenation, its index (build_cloud) and the covariance import
+  hipStream_t sm = o->s2m->stream;
   int64_t off = 0;
   for (int k : cur) {
     const Keyframe& kf = *o->keyframes[k];
-    HIP_TRY(hipMemcpyAsync(o->cat_pts.as<float4>() + off, kf.pts.p, sizeof(float4) * kf.n, hipMemcpyDeviceToDevice, o->s));
+    HIP_TRY(hipMemcpyAsync(o->cat_pts.as<float4>() + off, kf.pts.p, sizeof(float4) * kf.n, hipMemcpyDeviceToDevice, sm));
     HIP_TRY(hipMemcpyAsync(o->cat_cov.as<double>() + 6 * off, kf.cov.p, sizeof(double) * 6 * kf.n,
-                           hipMemcpyDeviceToDevice, o->s));
+                           hipMemcpyDeviceToDevice, sm));
     off += kf.n;
   }
   Side tgt;
-  gicp_status st = cloud_from(o, o->s2m, o->cat_pts.as<float4>(), (int)total, &tgt.cloud);
+  gicp_status st = cloud_from(o, o->s2m, o->cat_pts.as<float4>(), (int)total, &tgt.cloud, true);
   if (st) return st;
   auto cv = std::make_shared<CovData>();
   cv->n = (int)total;
   HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * (size_t)total));
-  launch_cov_import(o->s, o->cat_cov.as<double>(), GICP_COV_SYM6, (int)total, tgt.cloud->inv_perm.as<int>(),
+  launch_cov_import(sm, o->cat_cov.as<double>(), GICP_COV_SYM6, (int)total, tgt.cloud->inv_perm.as<int>(),
                     cv->cov6.as<double>());
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(o->s));
+  HIP_TRY(hipStreamSynchronize(sm));
   tgt.cov = cv;
   o->s2m->tgt = tgt;        // setInputTarget + setTargetCovariances (odom.cc:780-783)
   invalidate_align(o->s2m);
@@ -570,6 +600,12 @@ gicp_status ddlo_odom_create(int device, const ddlo_odom_params* p, ddlo_odom** 
     return st;
   }
   o->s = o->s2s->stream;  // one stream: the driver's work is one dependent chain
+  o->timing = std::getenv("DDLO_ODOM_TIMING") != nullptr;
+  if (hipHostMalloc((void**)&o->median_pin, sizeof(float), hipHostMallocDefault) != hipSuccess) {
+    gicp_ctx_destroy(o->s2s);
+    gicp_ctx_destroy(o->s2m);
+    return fail(GICP_EHIP, "pinned allocation failed");
+  }
   mat4_identity(o->T);
   mat4_identity(o->T_s2s);
   mat4_identity(o->T_s2s_prev);
@@ -583,7 +619,14 @@ gicp_status ddlo_odom_destroy(ddlo_odom* o) {
   (void)hipSetDevice(o->device);
   (void)hipStreamSynchronize(o->s2m->stream);
   (void)hipStreamSynchronize(o->s);
+  if (o->timing && o->frames > 0) {
+    static const char* names[8] = {"upload", "preprocess", "cloud", "s2s_align", "submap", "s2m_align", "keyframe", "total"};
+    std::fprintf(stderr, "[odom timing] %ld frames, us/frame:", o->frames);
+    for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %s %.1f", names[k], 1e6 * o->t_phase[k] / o->frames);
+    std::fprintf(stderr, "\n");
+  }
   o->keyframes.clear();
+  if (o->median_pin) (void)hipHostFree(o->median_pin);
   gicp_ctx_destroy(o->s2m);
   gicp_ctx_destroy(o->s2s);
   delete o;
@@ -605,42 +648,67 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
     res->status = DDLO_ODOM_SKIPPED;
     return GICP_OK;
   }
+  using clk = std::chrono::steady_clock;
+  auto t0 = clk::now(), tl = t0;
+  auto mark = [&](int k) {
+    if (!o->timing) return;
+    (void)hipStreamSynchronize(o->s);
+    (void)hipStreamSynchronize(o->s2m->stream);
+    const auto t = clk::now();
+    o->t_phase[k] += std::chrono::duration<double>(t - tl).count();
+    tl = t;
+  };
   // upload + preprocessPoints (odom.cc:442-478)
   const int N = (int)n;
   HIP_TRY(o->up.ensure((n - 1) * stride + 12));
   HIP_TRY(hipMemcpyAsync(o->up.p, xyz, (n - 1) * stride + 12, hipMemcpyHostToDevice, o->s));
   HIP_TRY(o->a.ensure(sizeof(float4) * n));
   launch_pack4(o->s, o->up.as<unsigned char>(), stride, N, o->a.as<float4>());
+  mark(0);
   int m = N;
   st = preprocess(o, N, o->p.crop_use != 0, o->p.crop_size, o->p.vf_scan_use != 0, o->p.vf_scan_res, &m);
   if (st) return st;
   res->scan_points = m;
-  // computeSpaciousness (odom.cc:981-1001): median range, low-passed
+  mark(1);
+  // computeSpaciousness (odom.cc:981-1001): the median range is sorted on the
+  // device and copied to pinned memory; it is read after the next wait on
+  // the stream (nothing before scan matching uses it)
   HIP_TRY(o->rng.ensure(sizeof(float) * (size_t)std::max(m, 1)));
   HIP_TRY(o->rng_sorted.ensure(sizeof(float) * (size_t)std::max(m, 1)));
-  const float median_curr = median_range(o->s, o->a.as<float4>(), m, o->rng.as<float>(), o->rng_sorted.as<float>(),
-                                         o->cubtmp.p, o->cubtmp.bytes);
-  if (!o->have_median) {  // static float median_prev = median_curr (first call)
-    o->median_prev = median_curr;
-    o->have_median = true;
-  }
-  const float median_lpf = (float)(0.95 * o->median_prev + 0.05 * median_curr);
-  o->median_prev = median_lpf;
-  res->spaciousness = median_lpf;
-  // setAdaptiveParams (odom.cc:1156-1178)
-  if (o->p.adaptive) {
-    if (median_lpf > 20.0) o->thresh_dist = 10.0;
-    else if (median_lpf > 10.0 && median_lpf <= 20.0) o->thresh_dist = 5.0;
-    else if (median_lpf > 5.0 && median_lpf <= 10.0) o->thresh_dist = 1.0;
-    else if (median_lpf <= 5.0) o->thresh_dist = 0.5;
-  }
-  res->keyframe_thresh_dist = o->thresh_dist;
-  if (m < std::max(o->p.s2s.k_correspondences, o->p.s2m.k_correspondences))
+  if (m > 0)
+    median_range_async(o->s, o->a.as<float4>(), m, o->rng.as<float>(), o->rng_sorted.as<float>(), o->cubtmp.p,
+                       o->cubtmp.bytes, o->median_pin);
+  else
+    *o->median_pin = 0.f;
+  // computeMetrics + setAdaptiveParams (odom.cc:981-1001, 1156-1178), once
+  // the median has arrived
+  auto metrics = [&]() {
+    const float median_curr = *o->median_pin;
+    if (!o->have_median) {  // static float median_prev = median_curr (first call)
+      o->median_prev = median_curr;
+      o->have_median = true;
+    }
+    const float median_lpf = (float)(0.95 * o->median_prev + 0.05 * median_curr);
+    o->median_prev = median_lpf;
+    res->spaciousness = median_lpf;
+    if (o->p.adaptive) {
+      if (median_lpf > 20.0) o->thresh_dist = 10.0;
+      else if (median_lpf > 10.0 && median_lpf <= 20.0) o->thresh_dist = 5.0;
+      else if (median_lpf > 5.0 && median_lpf <= 10.0) o->thresh_dist = 1.0;
+      else if (median_lpf <= 5.0) o->thresh_dist = 0.5;
+    }
+    res->keyframe_thresh_dist = o->thresh_dist;
+  };
+  if (m < std::max(o->p.s2s.k_correspondences, o->p.s2m.k_correspondences)) {
+    HIP_TRY(hipStreamSynchronize(o->s));
+    metrics();
     return fail(GICP_ETOOFEW, "preprocessed scan has fewer points than k_correspondences");
-  // the preprocessed scan as a device cloud
+  }
+  // the preprocessed scan as a device cloud (finite after the voxel filter)
   std::shared_ptr<CloudData> scan;
-  st = cloud_from(o, o->s2s, o->a.as<float4>(), m, &scan);
+  st = cloud_from(o, o->s2s, o->a.as<float4>(), m, &scan, o->p.vf_scan_use != 0);
   if (st) return st;
+  mark(2);
 
   if (!o->have_target) {
     // initializeInputTarget (odom.cc:480-516)
@@ -649,8 +717,9 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
     invalidate_align(o->s2s);
     st = compute_cov(o->s2s, o->s2s->tgt);   // calculateTargetCovariances
     if (st) return st;
-    st = make_keyframe(o, scan);              // T_ = identity: the scan itself
+    st = make_keyframe(o, scan);              // T_ = identity: the scan itself (waits for the stream)
     if (st) return st;
+    metrics();
     o->have_target = true;
     res->status = DDLO_ODOM_FIRST;
     res->keyframe_added = 1;
@@ -667,8 +736,10 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
 
   // scanMatching (odom.cc:745-851)
   float T_S2S[16];
-  st = gicp_align(o->s2s, nullptr, T_S2S, &res->s2s);
+  st = gicp_align(o->s2s, nullptr, T_S2S, &res->s2s);   // waits for the stream: the median has arrived
   if (st) return st;
+  mark(3);
+  metrics();
   copy_pose(T_S2S, res->T_s2s_local);
   mat4_mul(o->T_s2s_prev, T_S2S, o->T_s2s);   // propagateS2S
   copy_pose(o->T_s2s, o->T_s2s_prev);
@@ -677,8 +748,10 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
   bool changed = false;
   st = submap_keyframes(o, &changed);
   if (st) return st;
+  mark(4);
   st = gicp_align(o->s2m, o->T_s2s, o->T, &res->s2m);
   if (st) return st;
+  mark(5);
   copy_pose(o->T, o->T_s2s_prev);             // T_s2s_prev_ = T_
   o->pose[0] = o->T[3];                       // propagateS2M
   o->pose[1] = o->T[7];
@@ -714,6 +787,11 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
       if (st) return st;
       res->keyframe_added = 1;
     }
+  }
+  mark(6);
+  if (o->timing) {
+    o->t_phase[7] += std::chrono::duration<double>(clk::now() - t0).count();
+    ++o->frames;
   }
   res->status = DDLO_ODOM_TRACKED;
   copy_pose(o->T, res->T);

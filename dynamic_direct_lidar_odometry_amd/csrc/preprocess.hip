@@ -60,12 +60,20 @@ __global__ __launch_bounds__(256) void k_compact(const float4* __restrict__ in, 
 }
 
 // ---- voxel grid --------------------------------------------------------------
-// bbox of the finite points: per-block partial min/max, then one block
-__global__ __launch_bounds__(256) void k_minmax_partial(const float4* __restrict__ in, int n, float* __restrict__ part) {
+// The points a voxel pass sees: finite, and — when the crop box is folded
+// into the pass (crop > 0) — outside [-crop, crop]^3 (k_crop_flags' rule).
+__device__ __forceinline__ bool voxel_input(float4 p, float crop) {
+  if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return false;
+  return !(crop > 0.f) || (p.x < -crop || p.y < -crop || p.z < -crop || p.x > crop || p.y > crop || p.z > crop);
+}
+
+// bbox of those points: per-block partial min/max, then one block
+__global__ __launch_bounds__(256) void k_minmax_partial(const float4* __restrict__ in, int n, float crop,
+                                                        float* __restrict__ part) {
   float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const float4 p = in[i];
-    if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) continue;
+    if (!voxel_input(p, crop)) continue;
     v[0] = fminf(v[0], p.x); v[1] = fminf(v[1], p.y); v[2] = fminf(v[2], p.z);
     v[3] = fmaxf(v[3], p.x); v[4] = fmaxf(v[4], p.y); v[5] = fmaxf(v[5], p.z);
   }
@@ -113,16 +121,17 @@ __global__ void k_voxel_geometry(const float* __restrict__ part, int nparts, flo
   geo[4] = divb[0] * divb[1];
 }
 
-// Voxel index of every point (non-finite points get UINT_MAX and sort last,
-// they are dropped by the caller's count).
+// Voxel index of every point (non-finite or cropped points get UINT_MAX and
+// sort last, they are dropped by the caller's count).
 __global__ __launch_bounds__(256) void k_voxel_keys(const float4* __restrict__ in, int n, float inv_x, float inv_y,
-                                                    float inv_z, const int* __restrict__ geo, unsigned* __restrict__ key,
-                                                    int* __restrict__ idx, int* __restrict__ nfinite) {
+                                                    float inv_z, float crop, const int* __restrict__ geo,
+                                                    unsigned* __restrict__ key, int* __restrict__ idx,
+                                                    int* __restrict__ nfinite) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 p = in[i];
   unsigned k = 0xffffffffu;
-  if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+  if (voxel_input(p, crop)) {
     const int i0 = (int)(floorf(p.x * inv_x) - (float)geo[0]);
     const int i1 = (int)(floorf(p.y * inv_y) - (float)geo[1]);
     const int i2 = (int)(floorf(p.z * inv_z) - (float)geo[2]);
@@ -233,7 +242,7 @@ size_t voxel_tmp_bytes(int n) {
 // part[6 * 64] floats.  Returns the output count in *count_host (-1 if the
 // grid overflows: the caller copies the input, as the reference does).
 int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, int* scratch, void* tmp, size_t tmp_bytes,
-               int* count_host) {
+               int* count_host, float crop) {
   *count_host = 0;
   if (n <= 0) return 0;
   unsigned* keys = reinterpret_cast<unsigned*>(scratch);
@@ -249,9 +258,9 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   const float inv = 1.0f / leaf;
   const int nparts = 64;
   (void)hipMemsetAsync(small, 0, 16 * sizeof(int), s);
-  k_minmax_partial<<<nparts, 256, 0, s>>>(in, n, part);
+  k_minmax_partial<<<nparts, 256, 0, s>>>(in, n, crop, part);
   k_voxel_geometry<<<1, 64, 0, s>>>(part, nparts, inv, inv, inv, small);
-  k_voxel_keys<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, inv, inv, inv, small, keys, idx, small + 9);
+  k_voxel_keys<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, inv, inv, inv, crop, small, keys, idx, small + 9);
   size_t need = voxel_tmp_bytes(n);
   if (need > tmp_bytes) return -2;
   size_t t = tmp_bytes;
@@ -263,13 +272,13 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   int h[16];
   (void)hipMemcpyAsync(h, small, sizeof(h), hipMemcpyDeviceToHost, s);
   (void)hipStreamSynchronize(s);
-  if (h[6]) return 0;            // no finite point
+  if (h[6]) return 0;            // no (finite, uncropped) point
   if (h[5]) {                    // grid overflow: the reference leaves the cloud as it is
     *count_host = -1;
     return 0;
   }
-  // runs of the finite points only (non-finite keys = UINT_MAX sort last and
-  // form the last run; a finite voxel index never reaches UINT_MAX here)
+  // runs of the voxel-pass points only (the others' keys = UINT_MAX sort last
+  // and form the last run; a real voxel index never reaches UINT_MAX here)
   int nruns = h[8];
   if (h[9] < n) nruns -= 1;
   (void)hipMemcpyAsync(small + 8, &nruns, sizeof(int), hipMemcpyHostToDevice, s);
@@ -278,17 +287,16 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   return 0;
 }
 
-float median_range(hipStream_t s, const float4* in, int n, float* d, float* d_sorted, void* tmp, size_t tmp_bytes) {
-  if (n <= 0) return 0.f;
+// median range: d[n/2] of the sorted ranges, copied to `out` (pinned host
+// memory) in stream order; the caller reads it after waiting on the stream
+void median_range_async(hipStream_t s, const float4* in, int n, float* d, float* d_sorted, void* tmp, size_t tmp_bytes,
+                        float* out) {
   k_ranges<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, d);
   size_t t = tmp_bytes;
   // non-negative floats sort like their bit patterns
   (void)hipcub::DeviceRadixSort::SortKeys(tmp, t, reinterpret_cast<const unsigned*>(d),
                                           reinterpret_cast<unsigned*>(d_sorted), n, 0, 32, s);
-  float m = 0.f;
-  (void)hipMemcpyAsync(&m, d_sorted + n / 2, sizeof(float), hipMemcpyDeviceToHost, s);
-  (void)hipStreamSynchronize(s);
-  return m;
+  (void)hipMemcpyAsync(out, d_sorted + n / 2, sizeof(float), hipMemcpyDeviceToHost, s);
 }
 size_t median_tmp_bytes(int n) {
   size_t a = 0;

@@ -8,6 +8,7 @@
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>  // types only (ncclComm_t)
 
+#include <array>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -223,7 +224,8 @@ struct gicp_ctx {
   // state copy to slot s] for s = 0, 1
   std::vector<hipExecGraphPair> g_first;
   hipExecGraphPair g_rest[2];
-  std::tuple<int, int, const void*> graph_key{-1, -1, nullptr};
+  // captured for: RCCL in the chunk, job buffer, launch geometry (LinGeom)
+  std::array<long long, 7> graph_key{{-1, -1, -1, -1, -1, -1, -1}};
   int predicted_iters = kDefaultPredictedIters;   // iterations of the previous align on this ctx
   std::vector<hipEvent_t> chunk_ev;
   hipStream_t copy_stream = nullptr;
@@ -262,10 +264,23 @@ inline gicp_status set_device(const gicp_ctx* c) {
   return GICP_OK;
 }
 
+// Grow a ctx scratch buffer; work still queued on the stream may read the
+// old block, so the stream is drained before it goes back to the pool.
+inline hipError_t grow(DevBuf& b, size_t bytes, hipStream_t s) {
+  if (bytes <= b.bytes && b.p) return hipSuccess;
+  if (b.p) {
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+  }
+  return b.ensure(bytes);
+}
+
 // xyz: host memory (copied to the device first), or device memory when
-// on_device (e.g. a preprocessed scan or a keyframe of the odometry driver)
+// on_device (e.g. a preprocessed scan or a keyframe of the odometry driver).
+// check_finite = false (device clouds known finite): no read-back, and the
+// call returns without waiting for the build.
 inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, std::shared_ptr<CloudData>* out,
-                               bool on_device = false) {
+                               bool on_device = false, bool check_finite = true) {
   if (!xyz || n == 0 || stride < 12 || (stride % 4) != 0) return fail(GICP_EINVAL, "invalid cloud (null, empty or bad stride)");
   if (n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "cloud too large");
   auto cd = std::make_shared<CloudData>();
@@ -280,21 +295,21 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   const size_t raw_sz = (n - 1) * stride + 12;
   const unsigned char* raw = reinterpret_cast<const unsigned char*>(xyz);
   if (!on_device) {
-    HIP_TRY(c->raw_bytes.ensure(raw_sz));
+    HIP_TRY(grow(c->raw_bytes, raw_sz, s));
     HIP_TRY(hipMemcpyAsync(c->raw_bytes.p, xyz, raw_sz, hipMemcpyHostToDevice, s));
     raw = c->raw_bytes.as<unsigned char>();
   }
   const int nb = (N + 255) / 256;
-  HIP_TRY(c->raw_pts.ensure(sizeof(float4) * n));
-  HIP_TRY(c->partial.ensure(sizeof(float) * 6 * nb));
-  HIP_TRY(c->nonfinite.ensure(sizeof(int)));
+  HIP_TRY(grow(c->raw_pts, sizeof(float4) * n, s));
+  HIP_TRY(grow(c->partial, sizeof(float) * 6 * nb, s));
+  HIP_TRY(grow(c->nonfinite, sizeof(int), s));
   HIP_TRY(hipMemsetAsync(c->nonfinite.p, 0, sizeof(int), s));
   HIP_TRY(cd->quant.ensure(sizeof(float) * 8));
   launch_pack_bbox(s, raw, stride, N, c->raw_pts.as<float4>(), c->partial.as<float>(),
                    c->nonfinite.as<int>(), nb);
   launch_bbox_final(s, c->partial.as<float>(), nb, cd->quant.as<float>());
-  HIP_TRY(c->keys_tmp.ensure(sizeof(unsigned long long) * n));
-  HIP_TRY(c->vals_tmp.ensure(sizeof(int) * n));
+  HIP_TRY(grow(c->keys_tmp, sizeof(unsigned long long) * n, s));
+  HIP_TRY(grow(c->vals_tmp, sizeof(int) * n, s));
   HIP_TRY(cd->keys.ensure(sizeof(unsigned long long) * n));
   HIP_TRY(cd->perm.ensure(sizeof(int) * n));
   launch_morton(s, c->raw_pts.as<float4>(), N, cd->quant.as<float>(), c->keys_tmp.as<unsigned long long>(),
@@ -303,7 +318,7 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, c->keys_tmp.as<unsigned long long>(),
                                              cd->keys.as<unsigned long long>(), c->vals_tmp.as<int>(),
                                              cd->perm.as<int>(), N, 0, 63, s));
-  HIP_TRY(c->sort_tmp.ensure(tmp_bytes));
+  HIP_TRY(grow(c->sort_tmp, tmp_bytes, s));
   tmp_bytes = c->sort_tmp.bytes;
   HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp_bytes, c->keys_tmp.as<unsigned long long>(),
                                              cd->keys.as<unsigned long long>(), c->vals_tmp.as<int>(),
@@ -324,9 +339,11 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
                        cd->lvl_cnt[l - 1], cd->lvl_cnt[l], cd->box_lo.as<float4>() + cd->lvl_off[l],
                        cd->box_hi.as<float4>() + cd->lvl_off[l]);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(c->flag_host, c->nonfinite.p, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  if (*c->flag_host) return fail(GICP_ENONFINITE, "cloud contains non-finite coordinates");
+  if (check_finite) {
+    HIP_TRY(hipMemcpyAsync(c->flag_host, c->nonfinite.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (*c->flag_host) return fail(GICP_ENONFINITE, "cloud contains non-finite coordinates");
+  }
   *out = cd;
   return GICP_OK;
 }

@@ -309,3 +309,36 @@ def test_align_sequence_on_one_ctx_matches_fresh_ctx(s2s_golden):
         seen.append(res.iterations_run)
     # the sequence really exercised rising and falling iteration counts
     assert any(b > a for a, b in zip(seen, seen[1:])) and any(b < a for a, b in zip(seen, seen[1:])), seen
+
+
+def test_context_reused_across_cloud_sizes():
+    """One context aligning a sequence whose source grows a little and whose
+    target grows (same graph-key bucket before the fix: the captured collect
+    grid and LDS box cache were sized for the first clouds) gives exactly
+    what a fresh context gives for every pair."""
+    from dynamic_direct_lidar_odometry_amd import scene
+    src, tgt, _ = scene.s2s_pair(64, 1024, 1)
+    p = P.default_params(k_correspondences=10, max_correspondence_distance=1.0)
+    c = P.Context(0)
+    c.set_params(p)
+    n0, m0 = 40000, 30000
+    # the repeats make the next align reuse the first-chunk graph captured for
+    # the previous clouds (same predicted iteration count)
+    for ds, dt in ((0, 0), (0, 0), (700, 0), (900, 0), (900, 0), (900, 9000), (300, 20000), (300, 20000)):
+        a, b = src[: n0 + ds], tgt[: m0 + dt]
+        c.set_target(b)
+        c.set_source(a)
+        T, r = c.align()
+        corr, sqd = c.correspondences()
+        f = P.Context(0)
+        f.set_params(p)
+        f.set_target(b)
+        f.set_source(a)
+        T2, r2 = f.align()
+        corr2, sqd2 = f.correspondences()
+        f.close()
+        np.testing.assert_array_equal(corr, corr2)
+        np.testing.assert_array_equal(sqd, sqd2)
+        np.testing.assert_array_equal(T, T2)
+        assert r.iterations_run == r2.iterations_run
+    c.close()
