@@ -249,6 +249,7 @@ gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks, i
 }
 
 gicp_status capture_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks, int slot, hipExecGraphPair* out) {
+  ++c->captures;
   HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
   const gicp_status s = enqueue_chunk(c, with_init, iters, nblocks, slot);
   const hipError_t e = hipStreamEndCapture(c->stream, &out->g);  // always leave capture mode
@@ -442,6 +443,7 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
 
 gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   if (!c) return GICP_OK;
+  if (std::getenv("DDLO_GRAPH_DEBUG")) std::fprintf(stderr, "[graphs] ctx %p: %ld chunk captures\n", (void*)c, c->captures);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   drop_graphs(c);

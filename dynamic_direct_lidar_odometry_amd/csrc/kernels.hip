@@ -2180,7 +2180,7 @@ LinGeom linearize_geometry(int nsrc, int tgt_upper) {
   g.seed_blocks = gcap / kLinWaves;                               // grid-stride kernel: any grid is exact
   g.collect_blocks = (gcap + kHardMax) / kLinWaves;               // one wave per sub-group: >= the groups
   g.scan_blocks = scan_blocks(gcap * kSearchQ);                   // any grid is exact
-  g.mom_blocks = moment_blocks(cdiv(std::max(nsrc, 1), 4096) * 4096);   // grid-stride; = the slab rows
+  g.mom_blocks = moment_blocks(cdiv(std::max(nsrc, 1), 32768) * 32768);   // grid-stride; = the slab rows
   g.lds_boxes = std::min(2048, cdiv(std::max(tgt_upper, 1), 128) * 128);   // >= the target's upper boxes
   return g;
 }

@@ -241,6 +241,7 @@ struct gicp_ctx {
   DevBuf search;       // correspondence search: [qstate f4 x n][key u64 x n][counters][tasks]
   bool speculate = true;    // queue a follow-on chunk before the first one's flag is seen
   bool comm_graphs = true;  // RCCL captured into the chunk graphs (else eager chunks)
+  long captures = 0;        // chunk graphs captured (diagnostics: DDLO_GRAPH_DEBUG)
 };
 
 namespace ddlo {
