@@ -234,6 +234,8 @@ struct KnnVisitor : VisitStats {
   unsigned long long K[KCAP];
   unsigned long long wk;   // worst kept key (bound)
   float wd;                // its distance
+  float tight;             // min over the tested full leaves of the farthest-corner distance (squared)
+  int nfull;               // leaves < nfull hold 32 real points (>= k: each such box bounds the k-th neighbour)
   int skip_lo, skip_hi;
 
   __device__ __forceinline__ float dist(int s) const { return __uint_as_float((unsigned)(K[s] >> 32)); }
@@ -244,6 +246,8 @@ struct KnnVisitor : VisitStats {
     for (int s = 0; s < KCAP; ++s) K[s] = dkey(INFINITY, -1);
     wk = K[0];
     wd = INFINITY;
+    tight = INFINITY;
+    nfull = 0;
     skip_lo = 1;
     skip_hi = 0;
   }
@@ -266,13 +270,18 @@ struct KnnVisitor : VisitStats {
     }
     update_worst();
   }
-  __device__ __forceinline__ float bound() const { return wd; }
-  __device__ __forceinline__ bool need(float4 lo, float4 hi) const { return box_dist2(qx, qy, qz, lo, hi) <= wd; }
+  // the k-th neighbour is no farther than the kept k-th key, nor than the
+  // farthest corner of any full leaf (32 >= k real points inside)
+  __device__ __forceinline__ float bound() const { return fminf(wd, tight); }
+  __device__ __forceinline__ bool need(float4 lo, float4 hi) const { return box_dist2(qx, qy, qz, lo, hi) <= bound(); }
+  __device__ __forceinline__ void note_leaf(f4v lo, f4v hi, int leaf) {
+    if (leaf < nfull && active) tight = fminf(tight, box_maxdist2(qx, qy, qz, lo, hi));
+  }
   __device__ __forceinline__ void process(const WaveLds* L, int start) {
     for (int j = 0; j < kLeafSize; ++j) {
       const float d = dist2(qx, qy, qz, L->px[j], L->py[j], L->pz[j]);
       const unsigned long long key = dkey(d, start + j);
-      if (active && key < wk) insert(key);
+      if (active && key < wk && d <= tight) insert(key);   // d > tight: not among the k nearest
     }
   }
   __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
@@ -326,6 +335,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
     const int i = g * 64 + lane_id();
     KnnVisitor<KCAP, EXACT> vis;
     vis.init(k);
+    vis.nfull = k <= kLeafSize ? c.n / kLeafSize : 0;   // a full leaf holds >= k points only if k <= 32
     vis.active = i < c.n;
     const float4 q = ldg4(c.pts, min(i, c.n - 1));
     vis.qx = q.x;
@@ -379,6 +389,7 @@ __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __r
     const int i = g * 64 + lane_id();
     KnnVisitor<KCAP, EXACT> vis;
     vis.init(k);
+    vis.nfull = k <= kLeafSize ? c.n / kLeafSize : 0;   // a full leaf holds >= k points only if k <= 32
     vis.active = i < nq;
     const float4 p = ldg4(q, min(i, nq - 1));
     vis.qx = p.x;

@@ -200,6 +200,16 @@ __device__ __forceinline__ float ball_radius(float bound2) {
   return bound2 < 0.f ? -1.f : sqrtf(bound2) * 1.0001f + 1e-4f;
 }
 
+// Squared distance from q to the farthest corner of a box: an upper bound on
+// the fp32 squared distance to every point inside (same operation order as
+// dist2(), each axis term at least the point's).
+__device__ __forceinline__ float box_maxdist2(float qx, float qy, float qz, f4v lo, f4v hi) {
+  const float dx = fmaxf(fabsf(qx - lo.x), fabsf(qx - hi.x));
+  const float dy = fmaxf(fabsf(qy - lo.y), fabsf(qy - hi.y));
+  const float dz = fmaxf(fabsf(qz - lo.z), fabsf(qz - hi.z));
+  return (dx * dx + dy * dy) + dz * dz;
+}
+
 __device__ __forceinline__ WaveBox make_wave_box(bool active, float qx, float qy, float qz, float bound2) {
   const float r = ball_radius(bound2);
   const bool use = active && r >= 0.f;
@@ -275,6 +285,7 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
     const int b = __builtin_ctzll(mask);
     mask &= mask - 1;
     const f4v blo = L->blo[b], bhi = L->bhi[b];
+    vis.note_leaf(blo, bhi, base + b);   // a visitor may tighten its bound from the box alone
     if (__any(vis.active && vis.need(make_float4(blo.x, blo.y, blo.z, 0.f), make_float4(bhi.x, bhi.y, bhi.z, 0.f))))
       ex |= 1ull << b;
   }
@@ -539,6 +550,7 @@ struct NNVisitor : VisitStats {
 
   __device__ __forceinline__ float bound() const { return best; }
   __device__ __forceinline__ bool need(float4 lo, float4 hi) const { return box_dist2(qx, qy, qz, lo, hi) <= best; }
+  __device__ __forceinline__ void note_leaf(f4v, f4v, int) {}
 
   __device__ __forceinline__ void merge_slices(unsigned long long& bk) const {
     if constexpr (Q <= 16) bk = xor_min64<16>(bk);
@@ -665,16 +677,6 @@ __device__ __forceinline__ void fill_upper(const CloudDev& c, f4v* U) {
     U[k] = f4v{lo.x, lo.y, lo.z, 0.f};
     U[n + k] = f4v{hi.x, hi.y, hi.z, 0.f};
   }
-}
-
-// Squared distance from q to the farthest corner of a box: an upper bound on
-// the fp32 squared distance to every point inside (same operation order as
-// dist2(), each axis term at least the point's).
-__device__ __forceinline__ float box_maxdist2(float qx, float qy, float qz, f4v lo, f4v hi) {
-  const float dx = fmaxf(fabsf(qx - lo.x), fabsf(qx - hi.x));
-  const float dy = fmaxf(fabsf(qy - lo.y), fabsf(qy - hi.y));
-  const float dz = fmaxf(fabsf(qz - lo.z), fabsf(qz - hi.z));
-  return (dx * dx + dy * dy) + dz * dz;
 }
 
 __device__ __forceinline__ bool box_overlap_v(const WaveBox& w, f4v lo, f4v hi) {
