@@ -315,7 +315,11 @@ __device__ __forceinline__ void knn_self_search(const CloudDev& c, KnnVisitor<KC
                                                 unsigned long long key, WaveLds* L) {
   s0 = max(s0, 0);
   s1 = min(s1, c.cnt0 - 1);
-  for (int l = s0; l <= s1; ++l) vis.scan_leaf(c, l, L);
+  for (int l = s0; l <= s1; ++l) {
+    vis.scan_leaf(c, l, L);
+    const float4 lo = ldg4(c.box_lo, l), hi = ldg4(c.box_hi, l);   // the seed leaves' boxes bound the k-th too
+    vis.note_leaf(f4v{lo.x, lo.y, lo.z, 0.f}, f4v{hi.x, hi.y, hi.z, 0.f}, l);
+  }
   vis.skip_lo = s0;
   vis.skip_hi = s1;
   split_search(c, vis, key, L);

@@ -281,6 +281,7 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
   vis.st_blocks += 1;
   vis.st_box += __popcll(mask);
   unsigned long long ex = 0ull;
+  const float before = vis.bound();
   while (mask) {
     const int b = __builtin_ctzll(mask);
     mask &= mask - 1;
@@ -290,8 +291,9 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
       ex |= 1ull << b;
   }
   vis.st_exact += __popcll(ex);
-  if (!ex) return;
-  if (vis.scan_leaves(c, base, ex, L)) vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
+  bool shrink = __any(vis.bound() < before);   // tightened by a box: later blocks see the smaller wave box
+  if (ex) shrink |= vis.scan_leaves(c, base, ex, L);
+  if (shrink) vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
 }
 
 // Generic LDS-staged, prefetching scan of the leaves in `ex` (bit b = leaf
