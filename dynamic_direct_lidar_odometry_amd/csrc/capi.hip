@@ -169,11 +169,13 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.hard_extent = env_float("DDLO_HARD_EXTENT", 4.0f);
   j.hard_blocks = env_int("DDLO_HARD_BLOCKS", 10);
   j.prev_window = env_int("DDLO_PREV_WINDOW", 2);
+  j.tri_mv = env_float("DDLO_TRI_MV", 0.2f);
   j.reuse = search_uses_tasks() ? env_int("DDLO_REUSE", 1) : 0;
   j.reuse_gap = env_float("DDLO_REUSE_GAP", 0.05f);
   j.reuse_gap0 = env_float("DDLO_REUSE_GAP0", 0.f);
   j.reuse_rec0 = env_int("DDLO_REUSE_REC0", 0);
   j.reuse_rec_eps = env_float("DDLO_REUSE_REC_EPS", 0.05f);
+  j.reuse_rec_conv = env_float("DDLO_REUSE_REC_CONV", 10.f);
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   return GICP_OK;
 }

@@ -132,6 +132,8 @@ struct AlignJob {
   int xcd_scan;                  // scan: one spatial eighth of the tasks per XCD (speed only)
   int prev_window;         // seed after a large pose step: 0 previous match only, 1 + Morton window around it,
                            // 2 + Morton window at the new position (default)
+  float tri_mv;            // a query that moved less than this (m) since the last linearize seeds from the
+                           // triangle bound alone (no load); else from the previous match / Morton window
   // Verified match reuse across outer iterations: per query
   // the position q_ref of its last search, its match p1 there and a lower
   // bound B^2 on the fp32 squared distance from q_ref to every OTHER target
@@ -144,6 +146,7 @@ struct AlignJob {
   int reuse_rec0;                // iteration 0 records references
   float reuse_rec_eps;           // later iterations record them only after an LM step that moved
                                  // every source point by less than this (m): the next one is smaller
+  float reuse_rec_conv;          // ... and (convergence test on) whose is_converged measure exceeds this
   float4* ref;                   // [n_src] q_ref (x, y, z) + B^2 (< 0: no reference)
   float4* ref_p;                 // [n_src] p1 (x, y, z) + its sorted target position as int bits (-1: none within the bound)
   unsigned* sec;                 // [n_src] fp32 bits: smallest squared distance of an examined non-best point

@@ -648,7 +648,11 @@ __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__
 // query's own key — then group sharing.  Writes the per-query search state
 // (qstate) and the seed key, and lists the sub-groups whose union box is
 // wider than hard_extent, so that k_nn_collect starts them first.
-template <int MINW>
+// FUSED: the same wavefront then walks its sub-group (k_nn_collect's work,
+// from the seed in registers): one launch and one query-state round trip
+// less per outer iteration; no hard list (walking hard sub-groups first
+// measured no gain).
+template <int MINW, bool FUSED>
 __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restrict__ job) {
   constexpr int Q = kTaskQ;
   AlignState* st = job->state;
@@ -661,6 +665,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   const float cap2 = job->cap2;
   const int have_prev = st->have_prev;
   const int prev_window = job->prev_window;
+  const double tri_mv = job->tri_mv;
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
   float Rf[9], tf[3];
@@ -682,6 +687,14 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   const int reuse = job->reuse;
   const bool check_ref = reuse && have_prev && st->any_rec;   // references exist only after a recording iteration
   const int rec = st->rec;   // this search records references
+  // fused walk: dynamic LDS = [kLinWaves x TaskLds][upper-level box cache]
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  TaskLds* const TL = reinterpret_cast<TaskLds*>(dsm) + wib;
+  f4v* const upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kTaskLdsBytes);
+  if constexpr (FUSED) {
+    fill_upper(tgt, upper);
+    __syncthreads();
+  }
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const int i = g * Q + qi;
@@ -733,7 +746,6 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       if (inrange && lane < Q) {
         keyout[i] = passed ? pass_key : dkey(INFINITY, -1);
         qstate[i] = make_float4(qx, qy, qz, -1.f);
-        if (reuse && !have_prev) job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);   // a new align: no reference yet
       }
       if (lane == 0) {
         job->hard_flag[g] = 2;   // nothing to search: k_nn_collect skips the sub-group
@@ -745,6 +757,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
           unsigned int* o = stats + (size_t)g * kStatFields;
           for (int f = 0; f < kStatFields; ++f) o[f] = 0;
           o[6] = npass << 8;
+          o[7] = FUSED ? 1 : 0;
         }
       }
       continue;
@@ -775,7 +788,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
         const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
         const double mv = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
-        if (mv < 0.02) {
+        if (mv < tri_mv) {
           const double r = sqrt((double)sqprev) + mv;
           const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
           if (b2 < (double)cap2) {
@@ -887,29 +900,66 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     if (inrange && lane < Q) {
       qstate[i] = make_float4(qx, qy, qz, active ? wr : -1.f);
       keyout[i] = active ? dkey(vis.best, vis.bestj) : passed ? pass_key : dkey(INFINITY, -1);
-      if (reuse && !have_prev) job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);   // a new align: no reference yet
     }
-    // hard sub-group: a wide union box (a query far from every target point
-    // drags many blocks into the walk) -> listed, walked first
-    const WaveBox whole = make_wave_box(active, qx, qy, qz, active ? wr : -1.f);
-    // hard: the previous outer iteration walked many blocks for this
-    // sub-group (same source points, a nearby pose), else -- first
-    // iteration -- a wide union box
-    const bool hard = have_prev ? job->grp_blocks[g] > job->hard_blocks : box_extent(whole) > job->hard_extent;
-    if (lane == 0) {
-      int slot = -1;
-      if (hard) {
-        slot = (int)atomicAdd(job->task_ctr + kTaskRegions * kCtrStride, 1u);
-        if (slot < kHardMax) job->hard_list[slot] = g;
+    if constexpr (FUSED) {
+      // the walk of k_nn_collect, from the seed in registers
+      const unsigned long long k0 = dkey(vis.best, vis.bestj);
+      TaskList tl;
+      tl.tasks = job->tasks;
+      tl.ctr = job->task_ctr;
+      tl.cap_r = job->task_cap_r;
+      TaskCollector col;
+      col.L = TL;
+      col.U = upper;
+      col.nup = upper_count(tgt);
+      col.qx = qx;
+      col.qy = qy;
+      col.qz = qz;
+      col.active = active;
+      col.bk = k0;
+      col.wr = active ? wr : -1.f;
+      col.sg = g;
+      const unsigned tm1 = stats ? (unsigned)__builtin_amdgcn_s_memtime() : 0u;
+      col.run(tgt, tl, gp(src.keys)[ic], job->split_extent);
+      if (inrange && lane < Q && active && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
+      if (rec && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further
+      if (stats) {
+        const unsigned npass = (unsigned)__popcll(__ballot(passed && lane < Q));
+        if (lane == 0) {
+          unsigned int* o = stats + (size_t)g * kStatFields;
+          o[0] = col.st_blocks;
+          o[1] = min((tm1 - (unsigned)tm0) >> 4, 65535u);
+          o[2] = col.st_tasks | (min(col.st_iters, 65535u) << 16);
+          o[3] = col.st_inline;
+          o[4] = (unsigned)__builtin_amdgcn_s_memtime() - (unsigned)tm0;
+          o[5] = min((col.tm_walk - (unsigned)tm0) >> 4, 65535u);
+          o[6] = npass << 8;
+          o[7] = 1;
+        }
       }
-      job->hard_flag[g] = (unsigned char)(hard && slot < kHardMax);
-    }
-    if (stats) {
-      const unsigned npass = (unsigned)__popcll(__ballot(passed && lane < Q));
+    } else {
+      // hard sub-group: a wide union box (a query far from every target point
+      // drags many blocks into the walk) -> listed, walked first
+      const WaveBox whole = make_wave_box(active, qx, qy, qz, active ? wr : -1.f);
+      // hard: the previous outer iteration walked many blocks for this
+      // sub-group (same source points, a nearby pose), else -- first
+      // iteration -- a wide union box
+      const bool hard = have_prev ? job->grp_blocks[g] > job->hard_blocks : box_extent(whole) > job->hard_extent;
       if (lane == 0) {
-        unsigned int* o = stats + (size_t)g * kStatFields;
-        o[1] = min(((unsigned)__builtin_amdgcn_s_memtime() - (unsigned)tm0) >> 4, 65535u);
-        o[6] = (unsigned)hard | (npass << 8);   // queries proven by their reuse reference
+        int slot = -1;
+        if (hard) {
+          slot = (int)atomicAdd(job->task_ctr + kTaskRegions * kCtrStride, 1u);
+          if (slot < kHardMax) job->hard_list[slot] = g;
+        }
+        job->hard_flag[g] = (unsigned char)(hard && slot < kHardMax);
+      }
+      if (stats) {
+        const unsigned npass = (unsigned)__popcll(__ballot(passed && lane < Q));
+        if (lane == 0) {
+          unsigned int* o = stats + (size_t)g * kStatFields;
+          o[1] = min(((unsigned)__builtin_amdgcn_s_memtime() - (unsigned)tm0) >> 4, 65535u);
+          o[6] = (unsigned)hard | (npass << 8);   // queries proven by their reuse reference
+        }
       }
     }
   }
@@ -1203,6 +1253,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
   const double max_corr2 = job->max_corr2;
   const int have_prev = st->have_prev;
   const int prev_window = job->prev_window;
+  const double tri_mv = job->tri_mv;
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
   float Rf[9], tf[3];
@@ -1279,7 +1330,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
         const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
         const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
         const double mv = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
-        if (mv < 0.02) {
+        if (mv < tri_mv) {
           const double r = sqrt((double)sqprev) + mv;
           const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
           if (b2 < (double)cap2) {
@@ -1419,6 +1470,7 @@ __global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ j
   const auto slab = gpw(job->slab);
   const double max_corr2 = job->max_corr2;
   const int rec = st->rec;   // this iteration records reuse references
+  const int first_rec_done = st->any_rec;   // an earlier iteration of this align recorded
   double R[9], t[3];
   for (int e = 0; e < 9; ++e) R[e] = st->R[e];
   for (int e = 0; e < 3; ++e) t[e] = st->t[e];
@@ -1459,6 +1511,10 @@ __global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ j
             pp = make_float4(p.x, p.y, p.z, __int_as_float((int)kj));
           }
           job->ref_p[i] = pp;
+        } else if (!first_rec_done) {
+          // the align's first recording iteration: a query it did not search
+          // (another shard's) must not keep a previous align's reference
+          job->ref[i] = make_float4(0.f, 0.f, 0.f, -1.f);
         }
       }
     }
@@ -1946,7 +2002,15 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
     const double* dt = tr_t[chosen];
     const double mv = sqrt(fro) * ((double)st->src_radius + sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2])) +
                       sqrt(dt[0] * dt[0] + dt[1] * dt[1] + dt[2] * dt[2]);
-    rec = rec && mv < (double)job->reuse_rec_eps;
+    // ... and, with the reference's convergence test on, only while the step
+    // is still far from converging (is_converged's measure > reuse_rec_conv):
+    // references pay off only if two more iterations follow
+    double cm = 0.0;
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        cm = fmax(cm, fabs(tr_R[chosen][3 * a + b] - (a == b ? 1.0 : 0.0)) / job->rotation_epsilon);
+    for (int a = 0; a < 3; ++a) cm = fmax(cm, fabs(dt[a]) / job->transformation_epsilon);
+    rec = rec && mv < (double)job->reuse_rec_eps && (job->fixed_iterations > 0 || cm > (double)job->reuse_rec_conv);
   }
   st->rec = rec;
   st->iter = it + 1;
@@ -2206,11 +2270,18 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
   } else {
     static const int occ_seed = env_knob("DDLO_OCC_SEED", 4), occ_col = env_knob("DDLO_OCC_COLLECT", 3),
                      occ_scan = env_knob("DDLO_OCC_SCAN", 4);
-    if (occ_seed == 6) k_nn_seed<6><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);
-    else k_nn_seed<4><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);
+    static const int fused = env_knob("DDLO_FUSED_SEED", 1);   // 0: separate seed and collect kernels (A/B)
     const size_t lds = collect_lds_bytes(g.lds_boxes);
-    if (occ_col == 4) k_nn_collect<4><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
-    else k_nn_collect<3><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
+    if (fused) {
+      static const int occ_fused = env_knob("DDLO_OCC_FUSED", 3);
+      if (occ_fused == 2) k_nn_seed<2, true><<<g.seed_blocks, 64 * kLinWaves, lds, s>>>(job);
+      else k_nn_seed<3, true><<<g.seed_blocks, 64 * kLinWaves, lds, s>>>(job);
+    } else {
+      if (occ_seed == 6) k_nn_seed<6, false><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);
+      else k_nn_seed<4, false><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);
+      if (occ_col == 4) k_nn_collect<4><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
+      else k_nn_collect<3><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
+    }
     if (occ_scan == 6) k_nn_scan<6><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
     else k_nn_scan<4><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
   }
