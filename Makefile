@@ -8,7 +8,7 @@ PKG := dynamic_direct_lidar_odometry_amd
 CSRC := $(PKG)/csrc
 LIBDIR := $(PKG)/_lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
-OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o
+OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o $(LIBDIR)/segment.o
 
 all: lib oracle facade
 
@@ -31,6 +31,10 @@ $(LIBDIR)/preprocess.o: $(CSRC)/preprocess.hip $(CSRC)/gicp_types.hpp $(CSRC)/la
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIBDIR)/odom.o: $(CSRC)/odom.hip $(CSRC)/runtime.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h include/ddlo_odom.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/segment.o: $(CSRC)/segment.hip $(CSRC)/runtime.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h include/ddlo_segment.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

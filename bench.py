@@ -255,6 +255,35 @@ def s2s_gn_leg(local_rank, args):
             "ms_per_align": round(1e3 * el / args.gn_steps, 4), "iterations_per_align": iters // args.gn_steps}
 
 
+def segmentation_leg(local_rank, args):
+    """range-image segmentation (include/ddlo_segment.h)
+    of one 512x512 organized scan with cfg/ddlo.yaml's detection parameters:
+    H2D, the fused per-pixel device pass (projection, ground, label init), the
+    read-back and the host labelling.  One step = one ddlo_seg_process."""
+    import math
+    from dynamic_direct_lidar_odometry_amd import scene
+    from dynamic_direct_lidar_odometry_amd import segmentation as SG
+    sc = scene.make_scene(1005, moving=True)
+    pose = scene.make_pose([0.0, 0.0, scene.SENSOR_Z], (0.0, 0.0, math.radians(20.0)))
+    pts = scene.raycast(sc, pose, 512, 512, 1005, organized=True)
+    bad = ~np.isfinite(pts).all(axis=1)
+    xyz = scene.transform(np.nan_to_num(pts, nan=0.0), pose).astype(np.float32)
+    xyz[bad] = np.nan
+    T = pose.astype(np.float32)
+    resid = np.abs(np.random.default_rng(0).normal(0, 0.2, (512, 512))).astype(np.float32)
+    seg = SG.Segmentation(local_rank, SG.yaml_seg_params())
+    for _ in range(3):
+        r = seg.process(xyz, T, resid)
+    t0 = time.perf_counter()
+    for _ in range(args.seg_steps):
+        r = seg.process(xyz, T, resid)
+    el = time.perf_counter() - t0
+    seg.close()
+    return {"workload": "range-image segmentation, 512x512 organized scan, ddlo.yaml detection parameters "
+                        "(window rows/cols 156..356)", "ms_per_frame": round(1e3 * el / args.seg_steps, 4),
+            "frames_per_s": round(args.seg_steps / el, 2), "segments": r.segments, "ground_pixels": r.ground_pixels}
+
+
 def odometry_leg(dist, rank, world, local_rank, args, frames=None):
     """BASELINE.json configs[4], the S2M half (SURVEY.md §8(e) cfg 5): the
     odometry driver (include/ddlo_odom.h, cfg/ddlo.yaml parameters) over the
@@ -322,6 +351,8 @@ def main():
     ap.add_argument("--no-gn", action="store_true", help="skip the cfg2 S2S 20-GN-iteration leg")
     ap.add_argument("--gn-steps", type=int, default=10)
     ap.add_argument("--no-odom", action="store_true", help="skip the cfg5 odometry-driver (S2M chain) leg")
+    ap.add_argument("--no-seg", action="store_true", help="skip the range-image segmentation leg")
+    ap.add_argument("--seg-steps", type=int, default=50)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -449,6 +480,8 @@ def main():
         result["batched_s2s"] = batched_leg(dist, rank, world, local_rank, args)
     if not args.no_odom:
         result["odometry"] = odometry_leg(dist, rank, world, local_rank, args)
+    if not args.no_seg:
+        result["segmentation"] = segmentation_leg(local_rank, args)
     if rank == 0:
         print(json.dumps(result), file=json_out, flush=True)
     if dist:

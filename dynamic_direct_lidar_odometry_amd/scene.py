@@ -147,11 +147,13 @@ def lidar_dirs(rows: int, cols: int) -> np.ndarray:
     return np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], axis=-1).reshape(-1, 3)
 
 
-def raycast(scene: Scene, pose: np.ndarray, rows: int, cols: int, seed: int, t: float = 0.0) -> np.ndarray:
+def raycast(scene: Scene, pose: np.ndarray, rows: int, cols: int, seed: int, t: float = 0.0,
+            organized: bool = False) -> np.ndarray:
     """Ray-cast one scan from world pose ``pose`` (4x4, world <- sensor).
 
     Returns float32 points (N,3) in the SENSOR frame, organized row-major with
-    no-return pixels dropped.
+    no-return pixels dropped; with ``organized`` all rows*cols pixels, NaN for
+    no return, top beam first.
     """
     rng = np.random.default_rng(seed)
     dirs_s = lidar_dirs(rows, cols)
@@ -183,6 +185,10 @@ def raycast(scene: Scene, pose: np.ndarray, rows: int, cols: int, seed: int, t: 
     rng_noise = rng.normal(0.0, 0.01, size=tbest.shape)
     r = tbest + rng_noise
     valid = np.isfinite(tbest) & (r >= 0.5) & (r <= 80.0)
+    if organized:
+        pts = np.where(valid[:, None], dirs_s * np.where(valid, r, 0.0)[:, None], np.nan).astype(np.float32)
+        # row 0 = the top beam, the last row = the lowest (the range-image convention of detection.cpp:463)
+        return pts.reshape(rows, cols, 3)[::-1].reshape(-1, 3).copy()
     pts = dirs_s[valid] * r[valid, None]
     return pts.astype(np.float32)
 
