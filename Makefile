@@ -54,3 +54,11 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all lib oracle facade clean
+
+# developer variant: k_lm_step prints per-phase cycle counts (load with DDLO_GICP_LIB)
+lmprof: $(OBJS)
+	@mkdir -p $(LIBDIR)/lmprof
+	$(HIPCC) $(HIPFLAGS) -DDDLO_LM_PROF -c $(CSRC)/kernels.hip -o $(LIBDIR)/lmprof/kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/lmprof/libddlo_gicp.so $(LIBDIR)/lmprof/kernels.o $(filter-out $(LIBDIR)/kernels.o,$(OBJS))
+
+.PHONY: lmprof

@@ -1455,9 +1455,12 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
 // K3b: Mahalanobis + normal-equation moments of the matched pairs
 // (update_correspondences :265-273 + linearize :292-328), 64 points per
 // wavefront, in-register transpose reduction, one slab row per block.
-constexpr int kMomWaves = 16;   // waves per moment block (1024 threads)
+constexpr int kMomWaves = 8;    // waves per moment block (512 threads: 256 blocks fill the chip at 131k points)
 
-__global__ __launch_bounds__(1024) void k_moments(const AlignJob* __restrict__ job) {
+// (A last-block-done fusion of k_lm_step into this kernel measured slower:
+// 27.3 us against 9 + 13.5 us — every block's agent-scope release writes
+// back its XCD's L2 before the completion counter.)
+__global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
   const CloudDev src = job->src;
@@ -1770,6 +1773,15 @@ __device__ double normal_eq_entry(const Moments& mo, int e) {
   return -s;
 }
 
+// The quadratic form of cost_decrease as a 12 x 12 matrix over d = vec(D)
+// (d[3k + a] = D[a][k]): W12[3k + a][3l + b] = W(k,l)[a][b], g12[3k + r] =
+// G(r, k); built once per LM step by 156 threads, so that the trials' cost
+// decreases are 12-term row products spread over 12 threads per trial (the
+// same products as cost_decrease, summed row by row).
+__device__ __forceinline__ double w12_entry(const Moments& mo, int e) {
+  const int r = e / 12, c = e % 12;
+  return mo.W(r / 3, c / 3, r % 3, c % 3);
+}
 // y0 - y(delta) for the frozen correspondences/M of the last linearize:
 // e' = e - D qt, D = [Rd - I | td]  =>  y0 - y = 2 <D, G> - sum_kl D_k^T W(k,l) D_l
 __device__ double cost_decrease(const Moments& mo, const double Rd[9], const double td[3]) {
@@ -1812,33 +1824,40 @@ __device__ void compose(const double Rd[9], const double td[3], const double R[9
 
 constexpr int kLmThreads = 512;
 constexpr int kMaxTrials = 64;
-constexpr int kMomBlocksMax = 128;                      // moment-kernel blocks (slab rows)
-constexpr int kLmRowsPerPart = (kMomBlocksMax + 5) / 6;  // slab rows per reducer thread
+constexpr int kMomBlocksMax = 256;                      // moment-kernel blocks (slab rows)
+constexpr int kLmParts = 12;                                          // slab row partitions
+constexpr int kLmRowsPerPart = (kMomBlocksMax + kLmParts - 1) / kLmParts;  // slab rows per reducer thread
 
 // Fixed-order reduction of the linearize slab (nblocks x kSlabStride) into
-// mom[kSlabStride] by one workgroup of >= 6 * kSlabStride threads.
+// mom[kSlabStride] by one workgroup: thread (p, v2) sums column pair v2 of
+// rows p, p + 12, ... with 16-byte loads (kLmParts x 40 threads), then 80
+// threads add the 12 partials in order (fixed order => deterministic).
 __device__ __forceinline__ void reduce_slab(const AlignJob* job, double (*part)[kSlabStride], double* mom) {
   const int tid = threadIdx.x;
   const int nb = job->nblocks;
-  const auto slab = gp(job->slab);
-  if (tid < 6 * kSlabStride) {
-    // issue every load before summing (fixed order => deterministic)
-    const int v = tid % kSlabStride, p = tid / kSlabStride;
-    double vals[kLmRowsPerPart];
+  const auto slab = (const __attribute__((address_space(1))) d2v*)gp(job->slab);
+  constexpr int kPairs = kSlabStride / 2;
+  if (tid < kLmParts * kPairs) {
+    // unconditional (clamped) loads, summed in row order; fully unrolled, so
+    // the loads are all issued before the in-order adds consume them (no
+    // private array: it would go to scratch)
+    const int v2 = tid % kPairs, p = tid / kPairs;
+    double s0 = 0.0, s1 = 0.0;
 #pragma unroll
     for (int r = 0; r < kLmRowsPerPart; ++r) {
-      const int b = p + 6 * r;
-      vals[r] = b < nb ? slab[(size_t)b * kSlabStride + v] : 0.0;
+      const int b = p + kLmParts * r;
+      const d2v x = slab[(size_t)min(b, nb - 1) * kPairs + v2];
+      s0 += b < nb ? x.x : 0.0;
+      s1 += b < nb ? x.y : 0.0;
     }
-    double s = 0.0;
-#pragma unroll
-    for (int r = 0; r < kLmRowsPerPart; ++r) s += vals[r];
-    part[p][v] = s;
+    part[p][2 * v2] = s0;
+    part[p][2 * v2 + 1] = s1;
   }
   __syncthreads();
   if (tid < kSlabStride) {
     double s = 0.0;
-    for (int p = 0; p < 6; ++p) s += part[p][tid];
+#pragma unroll
+    for (int p = 0; p < kLmParts; ++p) s += part[p][tid];
     mom[tid] = s;
   }
   __syncthreads();
@@ -1849,7 +1868,7 @@ __device__ __forceinline__ void reduce_slab(const AlignJob* job, double (*part)[
 __global__ __launch_bounds__(kLmThreads) void k_mom_reduce(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
-  __shared__ double part[6][kSlabStride];
+  __shared__ double part[kLmParts][kSlabStride];
   __shared__ double mom[kSlabStride];
   reduce_slab(job, part, mom);
   if (threadIdx.x < kSlabStride) gpw(job->mom)[threadIdx.x] = mom[threadIdx.x];
@@ -1860,27 +1879,54 @@ __global__ __launch_bounds__(kLmThreads) void k_mom_reduce(const AlignJob* __res
 // the reference's trial sequence is fully determined up front (lambda_i =
 // nu_{i-1} lambda_{i-1}, nu doubling: lsq_registration_impl.hpp:187-223), so
 // trial i is evaluated with exactly the lambda the sequential loop would use,
-// (4) thread 0 replays the sequential accept/reject decisions.
+// (4) thread 0 replays the sequential accept/reject decisions, (5) the new
+// state is stored by many threads.  Every state word is loaded at the start
+// (its latency hides behind the slab loads).
+#ifdef DDLO_LM_PROF   // developer build (make lmprof): per-phase cycle counts of one LM step, printed by thread 0
+#define LM_PROF(i) if (threadIdx.x == 0) lm_t[i] = __builtin_amdgcn_s_memtime()
+#else
+#define LM_PROF(i)
+#endif
 __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
-  __shared__ double part[6][kSlabStride];
+#ifdef DDLO_LM_PROF
+  unsigned long long lm_t[6];
+#endif
+  LM_PROF(0);
+  __shared__ double part[kLmParts][kSlabStride];
   __shared__ double mom[kSlabStride];
   __shared__ double Hs[36], bs[6];
-  __shared__ double tr_rho[kMaxTrials], tr_lambda[kMaxTrials];
+  __shared__ double W12[144], g12[12];
+  __shared__ double tr_rho[kMaxTrials], tr_lambda[kMaxTrials], tr_cm[kMaxTrials], tr_fro[kMaxTrials];
   __shared__ double tr_R[kMaxTrials][9], tr_t[kMaxTrials][3];
+  __shared__ double tr_d[kMaxTrials][12], tr_row[kMaxTrials][12], tr_den[kMaxTrials];
+  __shared__ double Rt_s[12];
   __shared__ int tr_conv[kMaxTrials];
+  __shared__ int dec_s[2];   // chosen trial, accept
   __shared__ double lambda0_s;
   const int tid = threadIdx.x;
-  // state words thread 0 needs at the end, loaded now (overlaps the slab loads)
+  // state words, loaded before the slab (their latency overlaps it)
   const int it_pre = st->iter;
   const int trials_pre = st->lm_trials;
+  const int rec_pre = st->rec;
+  const float src_radius = st->src_radius;
+  const double lambda_pre = st->lambda;
+  if (tid < 12) Rt_s[tid] = tid < 9 ? st->R[tid] : st->t[tid - 9];
+  // job words too (scalar-cache misses at their first use would each stall a phase)
+  const int optimizer = job->optimizer, lm_max_iterations = job->lm_max_iterations;
+  const int fixed_iterations = job->fixed_iterations, max_iterations = job->max_iterations;
+  const double lm_init_lambda_factor = job->lm_init_lambda_factor;
+  const double rotation_epsilon = job->rotation_epsilon, transformation_epsilon = job->transformation_epsilon;
+  const int reuse = job->reuse;
+  const float reuse_rec_eps = job->reuse_rec_eps, reuse_rec_conv = job->reuse_rec_conv;
   if (job->premom) {  // moments already reduced (and summed across shards)
     if (tid < kSlabStride) mom[tid] = gp((const double*)job->mom)[tid];
     __syncthreads();
   } else {
-    reduce_slab(job, part, mom);
+    reduce_slab(job, part, mom);   // ends with a barrier: Rt_s is visible too
   }
+  LM_PROF(1);
   const Moments mo{mom};
   if (tid < 42) {
     const double v = normal_eq_entry(mo, tid);
@@ -1888,23 +1934,26 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
       Hs[tid] = v;
     else
       bs[tid - 36] = v;
+  } else if (tid >= 64 && tid < 64 + 144) {
+    W12[tid - 64] = w12_entry(mo, tid - 64);
+  } else if (tid >= 256 && tid < 256 + 12) {
+    const int e = tid - 256;
+    g12[e] = mo.G(e % 3, e / 3);
   }
   __syncthreads();
-  double R[9], t[3];
-  for (int e = 0; e < 9; ++e) R[e] = st->R[e];
-  for (int e = 0; e < 3; ++e) t[e] = st->t[e];
-  const bool lm = job->optimizer != 0;
+  const bool lm = optimizer != 0;
   if (lm && tid == 0) {
-    double lambda = st->lambda;
+    double lambda = lambda_pre;
     if (lambda < 0.0) {
       double mx = 0.0;
       for (int e = 0; e < 6; ++e) mx = fmax(mx, fabs(Hs[7 * e]));
-      lambda = job->lm_init_lambda_factor * mx;
+      lambda = lm_init_lambda_factor * mx;
     }
     lambda0_s = lambda;
   }
   __syncthreads();
-  const int ntr = lm ? min(job->lm_max_iterations, kMaxTrials) : 1;
+  LM_PROF(2);
+  const int ntr = lm ? min(lm_max_iterations, kMaxTrials) : 1;
   if (tid < ntr) {
     double lambda = 0.0;
     if (lm) {
@@ -1924,105 +1973,163 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
     double Rd[9], td[3];
     so3_exp_d(d, Rd);
     td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
-    double rho = 1.0;
-    if (lm) {
-      const double dec = cost_decrease(mo, Rd, td);  // y0 - yi
-      double den = 0.0;
-      for (int e = 0; e < 6; ++e) den += d[e] * (lambda * d[e] - bs[e]);
-      rho = dec / den;
-    }
-    tr_rho[tid] = rho;
+    double den = 0.0;
+    for (int e = 0; e < 6; ++e) den += d[e] * (lambda * d[e] - bs[e]);
+    tr_den[tid] = den;
     tr_lambda[tid] = lambda;
-    tr_conv[tid] = is_converged_d(job, Rd, td) ? 1 : 0;
+    // is_converged's measure max(|Rd - I| / rot_eps, |td| / trans_eps) (lsq_registration_impl.hpp:128-139)
+    double cm = 0.0;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) cm = fmax(cm, fabs(Rd[3 * i + j] - (i == j ? 1.0 : 0.0)) / rotation_epsilon);
+    for (int i = 0; i < 3; ++i) cm = fmax(cm, fabs(td[i]) / transformation_epsilon);
+    tr_cm[tid] = cm;
+    tr_conv[tid] = fixed_iterations <= 0 && cm < 1;
+    double fro = 0.0;
+    for (int e = 0; e < 9; ++e) {
+      const double dd = Rd[e] - ((e % 4 == 0) ? 1.0 : 0.0);
+      fro += dd * dd;
+    }
+    tr_fro[tid] = fro;
     for (int e = 0; e < 9; ++e) tr_R[tid][e] = Rd[e];
     for (int e = 0; e < 3; ++e) tr_t[tid][e] = td[e];
+    // d = vec([Rd - I | td]), d[3k + a] = D[a][k] (cost_decrease)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) tr_d[tid][3 * k + a] = k < 3 ? Rd[3 * a + k] - (a == k ? 1.0 : 0.0) : td[a];
+  }
+  __syncthreads();
+  LM_PROF(3);
+  // trial cost decrease y0 - y(delta) = 2 <g, d> - d^T W d (cost_decrease),
+  // one row of the quadratic form per thread: (trial, row) = (x / 12, x % 12)
+  for (int x = tid; lm && x < 12 * ntr; x += kLmThreads) {
+    const int tr = x / 12, i = x % 12;
+    double srow = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) srow += W12[12 * i + j] * tr_d[tr][j];
+    tr_row[tr][i] = tr_d[tr][i] * srow;
+  }
+  __syncthreads();
+  if (tid < ntr) {
+    double rho = 1.0;
+    if (lm) {
+      double lin = 0.0, quad = 0.0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lin += tr_d[tid][3 * k + r] * g12[3 * k + r];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) quad += tr_row[tid][i];
+      rho = (2.0 * lin - quad) / tr_den[tid];
+    }
+    tr_rho[tid] = rho;
   }
   __syncthreads();
   // the per-linearize record, stored by many threads at once
   if (tid < kSlabStride) st->last_mom[tid] = mom[tid];
-  else if (tid < kSlabStride + 9) st->last_lin_R[tid - kSlabStride] = R[tid - kSlabStride];
-  else if (tid < kSlabStride + 12) st->last_lin_t[tid - kSlabStride - 9] = t[tid - kSlabStride - 9];
+  else if (tid < kSlabStride + 9) st->last_lin_R[tid - kSlabStride] = Rt_s[tid - kSlabStride];
+  else if (tid < kSlabStride + 12) st->last_lin_t[tid - kSlabStride - 9] = Rt_s[tid - kSlabStride];
   else if (tid < kSlabStride + 18) st->last_b[tid - kSlabStride - 12] = bs[tid - kSlabStride - 12];
-  if (tid != 0) return;
-
-  const int it = it_pre;
-  st->nr_iterations = it;
-  st->final_cost = mo.y0();
-  st->num_corr = (int)mo.count();
-
-  bool ok = false;
-  int chosen = -1;
-  bool accept = false;
-  if (!lm) {  // step_gn: always take the step (lsq_registration_impl.hpp:155-173)
-    ok = true;
-    chosen = 0;
-    accept = true;
-  } else {    // step_lm decisions (:188-231)
-    int i = 0;
-    for (; i < ntr; ++i) {
-      if (tr_rho[i] < 0) {
-        if (tr_conv[i]) {
-          ok = true;
-          chosen = i;
-          break;
-        }
-        continue;
-      }
+  LM_PROF(4);
+  // the sequential decisions (thread 0)
+  if (tid == 0) {
+    const int it = it_pre;
+    st->nr_iterations = it;
+    st->final_cost = mo.y0();
+    st->num_corr = (int)mo.count();
+    bool ok = false;
+    int chosen = -1;
+    bool accept = false;
+    if (!lm) {  // step_gn: always take the step (lsq_registration_impl.hpp:155-173)
       ok = true;
+      chosen = 0;
       accept = true;
-      chosen = i;
-      break;
+    } else {    // step_lm decisions (:188-231)
+      for (int i = 0; i < ntr; ++i) {
+        if (tr_rho[i] < 0) {
+          if (tr_conv[i]) {
+            ok = true;
+            chosen = i;
+            break;
+          }
+          continue;
+        }
+        ok = true;
+        accept = true;
+        chosen = i;
+        break;
+      }
+      st->lm_trials = trials_pre + (ok ? chosen + 1 : ntr);
+      if (accept) {
+        const double c = 2 * tr_rho[chosen] - 1;
+        st->lambda = tr_lambda[chosen] * fmax(1.0 / 3.0, 1 - c * c * c);
+      } else if (ok) {
+        st->lambda = tr_lambda[chosen];
+      } else {
+        st->lambda = tr_lambda[ntr - 1] * 2.0;  // not observable: the align ends
+      }
     }
-    st->lm_trials = trials_pre + (ok ? chosen + 1 : ntr);
-    if (accept) {
-      const double c = 2 * tr_rho[chosen] - 1;
-      st->lambda = tr_lambda[chosen] * fmax(1.0 / 3.0, 1 - c * c * c);
-    } else if (ok) {
-      st->lambda = tr_lambda[chosen];
-    } else {
-      st->lambda = tr_lambda[ntr - 1] * 2.0;  // not observable: the align ends
+    if (rec_pre) st->any_rec = 1;   // this iteration's search recorded references
+    st->iter = it + 1;
+    st->have_prev = 1;
+    int done = 0;
+    if (!ok) {
+      st->lm_failed = 1;
+      done = 1;
+    } else if (tr_conv[chosen]) {
+      st->converged = 1;
+      done = 1;
+    }
+    if (it + 1 >= max_iterations) done = 1;
+    if (done) st->done = 1;
+    dec_s[0] = chosen;
+    dec_s[1] = accept ? 1 : 0;
+  }
+  __syncthreads();
+  const int chosen = dec_s[0];
+  if (dec_s[1]) {   // accepted: x0 = delta * x0 (compose, lsq_registration_impl.hpp:193-197,225-228)
+    if (tid < 12) {   // one entry of (Rn | tn) per thread, compose()'s arithmetic
+      const double* Rd = tr_R[chosen];
+      const int i = tid < 9 ? tid / 3 : tid - 9;
+      double v;
+      if (tid < 9) {
+        const int j = tid % 3;
+        v = Rd[3 * i + 0] * Rt_s[0 + j] + Rd[3 * i + 1] * Rt_s[3 + j] + Rd[3 * i + 2] * Rt_s[6 + j];
+        st->R[tid] = v;
+      } else {
+        v = (Rd[3 * i + 0] * Rt_s[9] + Rd[3 * i + 1] * Rt_s[10] + Rd[3 * i + 2] * Rt_s[11]) + tr_t[chosen][i];
+        st->t[i] = v;
+        part[0][i] = v;   // tn for the reuse-recording test below
+      }
+    } else if (tid >= 64 && tid < 64 + 36) {
+      st->final_hessian[tid - 64] = Hs[tid - 64];
     }
   }
-  if (st->rec) st->any_rec = 1;   // this iteration's search recorded references
-  int rec = job->reuse;
-  if (accept) {
-    double Rn[9], tn[3];
-    compose(tr_R[chosen], tr_t[chosen], R, t, Rn, tn);
-    for (int e = 0; e < 9; ++e) st->R[e] = Rn[e];
-    for (int e = 0; e < 3; ++e) st->t[e] = tn[e];
-    for (int e = 0; e < 36; ++e) st->final_hessian[e] = Hs[e];
-    // how far the step moved a source point: |dR q + dt - q| <= |dR - I|_F |q| + |dt|,
-    // |q| <= src_radius + |t|; the next search records references only
-    // after a small step (the one after it is expected to be smaller)
-    double fro = 0.0;
-    for (int e = 0; e < 9; ++e) {
-      const double d = tr_R[chosen][e] - ((e % 4 == 0) ? 1.0 : 0.0);
-      fro += d * d;
+  __syncthreads();
+  if (tid == 0) {
+    int rec = reuse;
+    if (dec_s[1]) {
+      // how far the step moved a source point: |dR q + dt - q| <= |dR - I|_F |q| + |dt|,
+      // |q| <= src_radius + |t|; the next search records references only
+      // after a small step (the one after it is expected to be smaller) ...
+      const double* tn = part[0];
+      const double* dt = tr_t[chosen];
+      const double mv = sqrt(tr_fro[chosen]) * ((double)src_radius + sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2])) +
+                        sqrt(dt[0] * dt[0] + dt[1] * dt[1] + dt[2] * dt[2]);
+      // ... and, with the reference's convergence test on, only while the step
+      // is still far from converging (is_converged's measure > reuse_rec_conv):
+      // references pay off only if two more iterations follow
+      rec = rec && mv < (double)reuse_rec_eps &&
+            (fixed_iterations > 0 || tr_cm[chosen] > (double)reuse_rec_conv);
     }
-    const double* dt = tr_t[chosen];
-    const double mv = sqrt(fro) * ((double)st->src_radius + sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2])) +
-                      sqrt(dt[0] * dt[0] + dt[1] * dt[1] + dt[2] * dt[2]);
-    // ... and, with the reference's convergence test on, only while the step
-    // is still far from converging (is_converged's measure > reuse_rec_conv):
-    // references pay off only if two more iterations follow
-    double cm = 0.0;
-    for (int a = 0; a < 3; ++a)
-      for (int b = 0; b < 3; ++b)
-        cm = fmax(cm, fabs(tr_R[chosen][3 * a + b] - (a == b ? 1.0 : 0.0)) / job->rotation_epsilon);
-    for (int a = 0; a < 3; ++a) cm = fmax(cm, fabs(dt[a]) / job->transformation_epsilon);
-    rec = rec && mv < (double)job->reuse_rec_eps && (job->fixed_iterations > 0 || cm > (double)job->reuse_rec_conv);
+    st->rec = rec;
   }
-  st->rec = rec;
-  st->iter = it + 1;
-  st->have_prev = 1;
-  if (!ok) {
-    st->lm_failed = 1;
-    st->done = 1;
-  } else if (tr_conv[chosen]) {
-    st->converged = 1;
-    st->done = 1;
-  }
-  if (st->iter >= job->max_iterations) st->done = 1;
+  LM_PROF(5);
+#ifdef DDLO_LM_PROF
+  if (tid == 0)
+    printf("lm_prof %d %llu %llu %llu %llu %llu\n", it_pre, lm_t[1] - lm_t[0], lm_t[2] - lm_t[1], lm_t[3] - lm_t[2],
+           lm_t[4] - lm_t[3], lm_t[5] - lm_t[4]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
