@@ -166,6 +166,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   }
   j.list_flush = (int)env_float("DDLO_LIST_FLUSH", 16.f);
   j.xcd_scan = env_int("DDLO_XCD_SCAN", 1);
+  j.pf_ratio = env_int("DDLO_PF_RATIO", 2);
   j.hard_extent = env_float("DDLO_HARD_EXTENT", 4.0f);
   j.hard_blocks = env_int("DDLO_HARD_BLOCKS", 10);
   j.prev_window = env_int("DDLO_PREV_WINDOW", 2);

@@ -130,6 +130,7 @@ struct AlignJob {
   unsigned short* grp_blocks;    // [n_src / 16] blocks the last collect walked per sub-group
   int hard_blocks;               // later iterations: hard if the last walk took more blocks
   int xcd_scan;                  // scan: one spatial eighth of the tasks per XCD (speed only)
+  int pf_ratio;                  // collect: lane-per-leaf pair tests below this queries / leaf-rounds ratio (speed only)
   int prev_window;         // seed after a large pose step: 0 previous match only, 1 + Morton window around it,
                            // 2 + Morton window at the new position (default)
   float tri_mv;            // a query that moved less than this (m) since the last linearize seeds from the

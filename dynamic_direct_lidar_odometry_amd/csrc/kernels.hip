@@ -919,6 +919,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       col.bk = k0;
       col.wr = active ? wr : -1.f;
       col.sg = g;
+      col.pf_ratio = job->pf_ratio;
       const unsigned tm1 = stats ? (unsigned)__builtin_amdgcn_s_memtime() : 0u;
       col.run(tgt, tl, gp(src.keys)[ic], job->split_extent);
       if (inrange && lane < Q && active && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
@@ -1031,6 +1032,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __rest
   col.bk = k0;
   col.wr = q.w;
   col.sg = g;
+  col.pf_ratio = job->pf_ratio;
   col.run(tgt, tl, skey, job->split_extent);
   if (inrange && lane < Q && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
   if (st->rec && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further

@@ -125,6 +125,7 @@ struct TaskCollector {
   bool ovf = false;
   int nfull = 0;           // kNN mode: leaves < nfull hold 32 real points
   float tight = INFINITY;  // kNN mode: min over tested full leaves of the farthest-corner distance (squared)
+  int pf_ratio = 0;        // 1-NN mode: lane-per-leaf pair tests while queries < pf_ratio * ceil(leaves / 4)
 
   __device__ __forceinline__ float bound() const { return __uint_as_float((unsigned)(bk >> 32)); }
 
@@ -161,12 +162,15 @@ struct TaskCollector {
   }
 
   // (leaf, query) pair tests of the cm staged leaves against the queries
-  // of qmask; a leaf any of them needs becomes one task.  Few queries: lane =
-  // leaf, one test per query (64 leaves per round); else 4 leaves x 16
-  // queries per round.
+  // of qmask; a leaf any of them needs becomes one task.  Few queries or
+  // many leaves: lane = leaf, one test per query (a broadcast LDS read and a
+  // box distance each); else 4 leaves x 16 queries per round (each round an
+  // append).  A block whose 64 leaves all pass the union box takes 16 cheap
+  // query steps instead of 16 rounds.
   __device__ __forceinline__ void pair_filter(int cm, unsigned qmask) {
     const int lane = lane_id();
-    if (__popc(qmask) <= 2) {
+    const int nq = __popc(qmask);
+    if (nq <= 2 || (!knn && nq < pf_ratio * ((cm + 3) >> 2))) {
       unsigned m16 = 0u;
       if (lane < cm) {
         const f4v blo = L->sb_lo[lane], bhi = L->sb_hi[lane];
