@@ -93,6 +93,34 @@ int env_int(const char* name, int dflt) {
   return (v && *v) ? std::atoi(v) : dflt;
 }
 
+// The search's development knobs, read from the environment once per
+// process, not on every align (host time between aligns).
+struct SearchKnobs {
+  float split_extent, hard_extent, tri_mv, reuse_gap, reuse_gap0, reuse_rec_eps, reuse_rec_conv;
+  int list_flush, xcd_scan, pf_ratio, hard_blocks, prev_window, reuse, reuse_rec0;
+};
+const SearchKnobs& search_knobs() {
+  static const SearchKnobs k = [] {
+    SearchKnobs v;
+    v.split_extent = env_float("DDLO_SPLIT_EXTENT", kSplitExtentDefault);
+    v.list_flush = (int)env_float("DDLO_LIST_FLUSH", 16.f);
+    v.xcd_scan = env_int("DDLO_XCD_SCAN", 1);
+    v.pf_ratio = env_int("DDLO_PF_RATIO", 2);
+    v.hard_extent = env_float("DDLO_HARD_EXTENT", 4.0f);
+    v.hard_blocks = env_int("DDLO_HARD_BLOCKS", 10);
+    v.prev_window = env_int("DDLO_PREV_WINDOW", 2);
+    v.tri_mv = env_float("DDLO_TRI_MV", 0.2f);
+    v.reuse = search_uses_tasks() ? env_int("DDLO_REUSE", 1) : 0;
+    v.reuse_gap = env_float("DDLO_REUSE_GAP", 0.05f);
+    v.reuse_gap0 = env_float("DDLO_REUSE_GAP0", 0.f);
+    v.reuse_rec0 = env_int("DDLO_REUSE_REC0", 0);
+    v.reuse_rec_eps = env_float("DDLO_REUSE_REC_EPS", 0.05f);
+    v.reuse_rec_conv = env_float("DDLO_REUSE_REC_CONV", 10.f);
+    return v;
+  }();
+  return k;
+}
+
 // byte layout of ctx->search for ns source points
 struct SearchLayout {
   size_t qstate, key, ctr, hard_list, hard_flag, grp_blocks, ref, ref_p, sec, tasks, total;
@@ -115,6 +143,7 @@ struct SearchLayout {
 };
 
 gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
+  const SearchKnobs& kn = search_knobs();
   AlignJob& j = *c->job_host;
   std::memset(&j, 0, sizeof(j));
   j.src = c->src.cloud->dev();
@@ -146,7 +175,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.own_axis = c->own_axis;
   j.own_lo = c->own_lo;
   j.own_hi = c->own_hi;
-  j.split_extent = env_float("DDLO_SPLIT_EXTENT", kSplitExtentDefault);
+  j.split_extent = kn.split_extent;
   j.premom = c->comm ? 1 : 0;
   j.mom = c->mom.as<double>();
   {
@@ -164,19 +193,19 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
     j.ref_p = reinterpret_cast<float4*>(u + sl.ref_p);
     j.sec = reinterpret_cast<unsigned*>(u + sl.sec);
   }
-  j.list_flush = (int)env_float("DDLO_LIST_FLUSH", 16.f);
-  j.xcd_scan = env_int("DDLO_XCD_SCAN", 1);
-  j.pf_ratio = env_int("DDLO_PF_RATIO", 2);
-  j.hard_extent = env_float("DDLO_HARD_EXTENT", 4.0f);
-  j.hard_blocks = env_int("DDLO_HARD_BLOCKS", 10);
-  j.prev_window = env_int("DDLO_PREV_WINDOW", 2);
-  j.tri_mv = env_float("DDLO_TRI_MV", 0.2f);
-  j.reuse = search_uses_tasks() ? env_int("DDLO_REUSE", 1) : 0;
-  j.reuse_gap = env_float("DDLO_REUSE_GAP", 0.05f);
-  j.reuse_gap0 = env_float("DDLO_REUSE_GAP0", 0.f);
-  j.reuse_rec0 = env_int("DDLO_REUSE_REC0", 0);
-  j.reuse_rec_eps = env_float("DDLO_REUSE_REC_EPS", 0.05f);
-  j.reuse_rec_conv = env_float("DDLO_REUSE_REC_CONV", 10.f);
+  j.list_flush = kn.list_flush;
+  j.xcd_scan = kn.xcd_scan;
+  j.pf_ratio = kn.pf_ratio;
+  j.hard_extent = kn.hard_extent;
+  j.hard_blocks = kn.hard_blocks;
+  j.prev_window = kn.prev_window;
+  j.tri_mv = kn.tri_mv;
+  j.reuse = kn.reuse;
+  j.reuse_gap = kn.reuse_gap;
+  j.reuse_gap0 = kn.reuse_gap0;
+  j.reuse_rec0 = kn.reuse_rec0;
+  j.reuse_rec_eps = kn.reuse_rec_eps;
+  j.reuse_rec_conv = kn.reuse_rec_conv;
   HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
   return GICP_OK;
 }
