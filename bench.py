@@ -446,7 +446,7 @@ def main():
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_unit": "bytes per linearize launch (L2->fabric, Infinity-Cache hits included)",
                      "traffic_source": traffic_src,
-                     "kernel": "linearize = k_nn_seed + k_nn_collect + k_nn_scan + k_moments (per outer iteration)",
+                     "kernel": "linearize = k_nn_seed (seed + tree walk) + k_nn_scan + k_moments (per outer iteration)",
                      "avg_launch_us": round(avg_launch_s * 1e6, 2),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch)},
     }
