@@ -62,3 +62,12 @@ lmprof: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/lmprof/libddlo_gicp.so $(LIBDIR)/lmprof/kernels.o $(filter-out $(LIBDIR)/kernels.o,$(OBJS))
 
 .PHONY: lmprof
+
+# developer variant: the search kernels fill the per-sub-group counters of
+# gicp_debug_stats (tools/probe_tasks.py; load with DDLO_GICP_LIB)
+statsprof: $(OBJS)
+	@mkdir -p $(LIBDIR)/statsprof
+	$(HIPCC) $(HIPFLAGS) -DDDLO_SEARCH_STATS -c $(CSRC)/kernels.hip -o $(LIBDIR)/statsprof/kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/statsprof/libddlo_gicp.so $(LIBDIR)/statsprof/kernels.o $(filter-out $(LIBDIR)/kernels.o,$(OBJS))
+
+.PHONY: statsprof

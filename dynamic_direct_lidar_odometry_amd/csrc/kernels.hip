@@ -661,17 +661,19 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   const CloudDev tgt = job->tgt;
   const auto corr = gpw(job->corr);
   const auto sqd = gpw(job->sqd);
+#ifdef DDLO_SEARCH_STATS
   unsigned int* const stats = job->stats;
+#else
+  // per-sub-group counters only in the developer build (make statsprof): the
+  // production kernel then fits 128 VGPRs (4 waves/SIMD, no hot-loop spills)
+  unsigned int* const stats = nullptr;
+#endif
   const float cap2 = job->cap2;
   const int have_prev = st->have_prev;
   const int prev_window = job->prev_window;
   const double tri_mv = job->tri_mv;
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
-  float Rf[9], tf[3];
-  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
-  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
-
   const int lane = lane_id();
   const int qi = lane % Q;
   const int wib = threadIdx.x >> 6;
@@ -680,10 +682,6 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   const int wave = (int)blockIdx.x * kLinWaves + wib;
   const int nwaves_total = gridDim.x * kLinWaves;
   const int ngroups = (src.n + Q - 1) / Q;
-  // previous linearization pose (for the triangle-inequality bound)
-  float Rp[9], tp[3];
-  for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
-  for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
   const int reuse = job->reuse;
   const bool check_ref = reuse && have_prev && st->any_rec;   // references exist only after a recording iteration
   const int rec = st->rec;   // this search records references
@@ -706,6 +704,11 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     const float sqprev = have_prev ? sqd[ic] : 0.f;
     const float4 rf = check_ref ? ldg4(job->ref, ic) : make_float4(0.f, 0.f, 0.f, -1.f);
     const float4 rp = check_ref ? ldg4(job->ref_p, ic) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // the pose is read per sub-group, so that it is not held in 12 VGPRs
+    // (the fp64 -> fp32 conversions are vector ops) across the walk
+    float Rf[9], tf[3];
+    for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
+    for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
     // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
@@ -783,6 +786,10 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         // NN(q) <= |q - p_prev| <= sqrt(sqd_prev) + |q - q_prev| (triangle
         // inequality; fp64 with an upward margin covers fp32 rounding), so
         // the bound needs no load of the previous match.
+        // previous linearization pose (for the triangle-inequality bound)
+        float Rp[9], tp[3];
+        for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
+        for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
         const float qpx = (Rp[0] * a.x + Rp[1] * a.y) + (Rp[2] * a.z + tp[0]);
         const float qpy = (Rp[3] * a.x + Rp[4] * a.y) + (Rp[5] * a.z + tp[1]);
         const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
@@ -897,7 +904,10 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       const double r = sqrt((double)vis.best) + (double)gap;
       wr = __uint_as_float(__float_as_uint((float)(r * r)) + 1);   // rounded up
     }
-    if (inrange && lane < Q) {
+    // FUSED: the query state and key are stored after the walk -- a store
+    // ahead of the walk's first box loads would be waited for with them
+    // (vmcnt counts loads and stores in issue order)
+    if (!FUSED && inrange && lane < Q) {
       qstate[i] = make_float4(qx, qy, qz, active ? wr : -1.f);
       keyout[i] = active ? dkey(vis.best, vis.bestj) : passed ? pass_key : dkey(INFINITY, -1);
     }
@@ -922,7 +932,10 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       col.pf_ratio = job->pf_ratio;
       const unsigned tm1 = stats ? (unsigned)__builtin_amdgcn_s_memtime() : 0u;
       col.run(tgt, tl, gp(src.keys)[ic], job->split_extent);
-      if (inrange && lane < Q && active && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
+      if (inrange && lane < Q) {
+        qstate[i] = make_float4(qx, qy, qz, active ? wr : -1.f);
+        keyout[i] = active ? col.bk : passed ? pass_key : dkey(INFINITY, -1);   // col.bk: the seed, lowered by inline scans
+      }
       if (rec && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further
       if (stats) {
         const unsigned npass = (unsigned)__popcll(__ballot(passed && lane < Q));
@@ -2382,8 +2395,9 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
     static const int fused = env_knob("DDLO_FUSED_SEED", 1);   // 0: separate seed and collect kernels (A/B)
     const size_t lds = collect_lds_bytes(g.lds_boxes);
     if (fused) {
-      static const int occ_fused = env_knob("DDLO_OCC_FUSED", 3);
+      static const int occ_fused = env_knob("DDLO_OCC_FUSED", 4);
       if (occ_fused == 2) k_nn_seed<2, true><<<g.seed_blocks, 64 * kLinWaves, lds, s>>>(job);
+      else if (occ_fused == 4) k_nn_seed<4, true><<<g.seed_blocks, 64 * kLinWaves, lds, s>>>(job);
       else k_nn_seed<3, true><<<g.seed_blocks, 64 * kLinWaves, lds, s>>>(job);
     } else {
       if (occ_seed == 6) k_nn_seed<6, false><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);

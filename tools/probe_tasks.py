@@ -1,5 +1,6 @@
 """Developer probe: task-search statistics of the cfg3 S2M search, per outer iteration
-(per sub-group: seed cycles, hard flag, collect blocks / tasks / cycles)."""
+(per sub-group: seed cycles, hard flag, collect blocks / tasks / cycles).
+Needs `make statsprof`: the production kernels carry no per-sub-group counters."""
 import os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
