@@ -1081,7 +1081,7 @@ constexpr int kScanBatch = 8;                         // tasks per LDS batch (tw
 constexpr int kScanTaskBytes = 3 * kLeafSize * 4 + kTaskQ * 16;   // 384 B points + 256 B queries
 constexpr int kScanWaves = 4;                         // waves per block
 
-template <int MINW>
+template <int MINW, int BATCH = kScanBatch>
 __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJob* __restrict__ job) {
   const AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
@@ -1091,7 +1091,9 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   const int cap_r = job->task_cap_r;
   const int lane = lane_id();
   const int qi = lane & 15, s = lane >> 4;
-  constexpr int kBatchBytes = kScanBatch * kScanTaskBytes;   // 5 KB = 5 LDS-DMA wave-instructions
+  constexpr int kBatchBytes = BATCH * kScanTaskBytes;   // 8 tasks: 5 KB = 5 LDS-DMA wave-instructions
+  constexpr int kDma = (kBatchBytes + 1023) / 1024;     // LDS-DMA wave-instructions per batch
+  static_assert(kDma <= 15, "vmcnt immediate");
   __shared__ __attribute__((aligned(16))) unsigned char lds_all[kScanWaves][2][kBatchBytes];
   unsigned char* const L0 = lds_all[threadIdx.x >> 6][0];
   unsigned char* const L1 = lds_all[threadIdx.x >> 6][1];
@@ -1167,28 +1169,29 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
     // again, never read)
     auto issue = [&](int b0, unsigned char* buf) {
 #pragma unroll
-      for (int i = 0; i < kBatchBytes / 1024; ++i) {
+      for (int i = 0; i < kDma; ++i) {
         const int o = i * 1024 + lane * 16;
         const int k = min(b0 + o / kScanTaskBytes, wcnt - 1), w = o % kScanTaskBytes;
-        const unsigned long long tk = __shfl(tl, k);
+        const unsigned long long tk = __shfl(tl, k);   // every lane takes part in the permute
         const char* src = w < 3 * kLeafSize * 4
                               ? (const char*)(tgt.soa + (size_t)(tk >> 40) * (3 * kLeafSize)) + w
                               : (const char*)(qstate + (size_t)((tk >> 16) & 0xffffffull) * kTaskQ) + (w - 3 * kLeafSize * 4);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+        if (kBatchBytes % 1024 == 0 || o < kBatchBytes)   // a partial last instruction: lanes past the batch idle
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
       }
     };
     issue(0, L0);
-    for (int b0 = 0; b0 < wcnt; b0 += kScanBatch) {
-      unsigned char* const cur = ((b0 / kScanBatch) & 1) ? L1 : L0;
-      if (b0 + kScanBatch < wcnt) {
-        issue(b0 + kScanBatch, ((b0 / kScanBatch) & 1) ? L0 : L1);
-        __builtin_amdgcn_s_waitcnt(0x0F75);  // vmcnt(5): all but the 5 just issued -> the current batch landed
+    for (int b0 = 0; b0 < wcnt; b0 += BATCH) {
+      unsigned char* const cur = ((b0 / BATCH) & 1) ? L1 : L0;
+      if (b0 + BATCH < wcnt) {
+        issue(b0 + BATCH, ((b0 / BATCH) & 1) ? L0 : L1);
+        __builtin_amdgcn_s_waitcnt(0x0F70 | kDma);  // vmcnt(kDma): all but the batch just issued -> the current batch landed
       } else {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       }
       __builtin_amdgcn_wave_barrier();
-      const int nb = min(kScanBatch, wcnt - b0);
+      const int nb = min(BATCH, wcnt - b0);
       for (int k = 0; k < nb; ++k) {
         const unsigned long long t = readlane_u64(tl, b0 + k);
         const int sg = (int)((t >> 16) & 0xffffffull);
@@ -2391,7 +2394,7 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
     k_nn_search<kSearchQ, 3><<<g.seed_blocks, 64 * kLinWaves, search_lds_bytes(g.lds_boxes), s>>>(job);
   } else {
     static const int occ_seed = env_knob("DDLO_OCC_SEED", 4), occ_col = env_knob("DDLO_OCC_COLLECT", 3),
-                     occ_scan = env_knob("DDLO_OCC_SCAN", 4);
+                     occ_scan = env_knob("DDLO_OCC_SCAN", 5);
     static const int fused = env_knob("DDLO_FUSED_SEED", 1);   // 0: separate seed and collect kernels (A/B)
     const size_t lds = collect_lds_bytes(g.lds_boxes);
     if (fused) {
@@ -2406,6 +2409,7 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
       else k_nn_collect<3><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
     }
     if (occ_scan == 6) k_nn_scan<6><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
+    else if (occ_scan == 5) k_nn_scan<5, 6><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);   // 6-task batches: 7.5 KB LDS per wave
     else k_nn_scan<4><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
   }
   k_moments<<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
