@@ -380,6 +380,139 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
   }
 }
 
+// Two lanes per query (lanes l and l + 32, 32 queries per wave): twice the
+// wavefronts of k_covariances for the same cloud, and half the serial scan
+// per lane.  Each half keeps the exact top-k of its half of every leaf's
+// points (positions 0-15 / 16-31); the k-th key of either half bounds the
+// k-th of the union (k real points lie within it), so a point is inserted
+// only below BOTH halves' k-th keys and a leaf is tested against the smaller
+// bound.  At the end the two lists are merged: the union's exact top-k.
+// The partner lane's word from a permlane32 swap of (v, v): one of the two
+// results is the lane's own word, the other the partner's (equal words make
+// the choice immaterial), whatever order the builtin returns them in.
+template <class R>
+__device__ __forceinline__ unsigned swap_partner(const R& r, unsigned own) { return r[0] == own ? r[1] : r[0]; }
+
+template <int KCAP, bool EXACT>
+struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
+  using Base = KnnVisitor<KCAP, EXACT>;
+  unsigned long long wk_other = ~0ull;   // the other half's k-th key
+  __device__ __forceinline__ unsigned long long wk_both() const { return umin64(this->wk, wk_other); }
+  __device__ __forceinline__ float bound() const {
+    return fminf(__uint_as_float((unsigned)(wk_both() >> 32)), this->tight);
+  }
+  __device__ __forceinline__ bool need(float4 lo, float4 hi) const {
+    return box_dist2(this->qx, this->qy, this->qz, lo, hi) <= bound();
+  }
+  __device__ __forceinline__ void exchange() {   // whole wave: wk of lane l ^ 32
+    const unsigned lo = (unsigned)this->wk, hi = (unsigned)(this->wk >> 32);
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    wk_other = ((unsigned long long)swap_partner(rh, hi) << 32) | swap_partner(rl, lo);
+  }
+  __device__ __forceinline__ void process(const WaveLds* L, int start) {
+    const int h0 = (lane_id() >> 5) * (kLeafSize / 2);
+    for (int j = 0; j < kLeafSize / 2; ++j) {
+      const float d = dist2(this->qx, this->qy, this->qz, L->px[h0 + j], L->py[h0 + j], L->pz[h0 + j]);
+      const unsigned long long key = dkey(d, start + h0 + j);
+      if (this->active && key < wk_both() && d <= this->tight) this->insert(key);
+    }
+    exchange();
+  }
+  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane_id() < kLeafSize) p = ldg4(c.pts, leaf * kLeafSize + lane_id());
+    stage_points<KnnVisitor2>(L, p);
+    process(L, leaf * kLeafSize);
+  }
+  __device__ __forceinline__ bool scan_leaves(const CloudDev& c, int base, unsigned long long ex, WaveLds* L) {
+    return scan_leaves_lds(c, base, ex, *this, L);
+  }
+  // whole wave: merge the partner's list into this lane's (both end equal)
+  __device__ __forceinline__ void merge_halves() {
+    unsigned long long own[KCAP];   // the lists as they were: inserts below reorder K
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) own[s] = this->K[s];
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      const unsigned lo = (unsigned)own[s], hi = (unsigned)(own[s] >> 32);
+      const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+      const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+      const unsigned long long other = ((unsigned long long)swap_partner(rh, hi) << 32) | swap_partner(rl, lo);
+      if (other < this->wk) this->insert(other);
+    }
+  }
+};
+
+// covariances with two lanes per query: wave w handles sorted points
+// [32w, 32w+32) (leaf w); seeds leaves w-1 .. w+1
+template <int KCAP, bool EXACT, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, int method, double* __restrict__ cov6) {
+  __shared__ WaveLds lds[4];
+  WaveLds* L = &lds[threadIdx.x >> 6];
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
+  const int ngroups = (c.n + 31) >> 5;
+  for (int g = wave; g < ngroups; g += nwaves_total) {
+    const int i = g * 32 + (lane_id() & 31);
+    KnnVisitor2<KCAP, EXACT> vis;
+    vis.init(k);
+    vis.wk_other = ~0ull;
+    vis.nfull = k <= kLeafSize ? c.n / kLeafSize : 0;
+    vis.active = i < c.n;
+    const float4 q = ldg4(c.pts, min(i, c.n - 1));
+    vis.qx = q.x;
+    vis.qy = q.y;
+    vis.qz = q.z;
+    {
+      const int s0 = max(g - 1, 0), s1 = min(g + 1, c.cnt0 - 1);
+      for (int l = s0; l <= s1; ++l) {
+        vis.scan_leaf(c, l, L);
+        const float4 lo = ldg4(c.box_lo, l), hi = ldg4(c.box_hi, l);
+        vis.note_leaf(f4v{lo.x, lo.y, lo.z, 0.f}, f4v{hi.x, hi.y, hi.z, 0.f}, l);
+      }
+      vis.skip_lo = s0;
+      vis.skip_hi = s1;
+      split_search<KnnVisitor2<KCAP, EXACT>, 32>(c, vis, gp(c.keys)[min(i, c.n - 1)], L);
+    }
+    vis.merge_halves();
+    if (!vis.active || lane_id() >= 32) continue;
+    // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
+    double mx = 0, my = 0, mz = 0;
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      if (s < k) {
+        const float4 p = ldg4(c.pts, vis.idx(s));
+        mx += (double)p.x;
+        my += (double)p.y;
+        mz += (double)p.z;
+      }
+    }
+    mx /= k;
+    my /= k;
+    mz /= k;
+    double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      if (s < k) {
+        const float4 p = ldg4(c.pts, vis.idx(s));
+        const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
+        C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
+        C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
+        C[6] += d2 * d0; C[7] += d2 * d1; C[8] += d2 * d2;
+      }
+    }
+    for (int e = 0; e < 9; ++e) C[e] /= k;
+    double out[6];
+    regularize(C, method, out);
+    double* o = cov6 + 6 * (size_t)i;
+    for (int e = 0; e < 6; ++e) o[e] = out[e];
+  }
+}
+template __global__ void k_covariances2<10, true, 3>(CloudDev, int, int, double*);
+template __global__ void k_covariances2<10, true, 4>(CloudDev, int, int, double*);
+template __global__ void k_covariances2<20, true, 3>(CloudDev, int, int, double*);
+
 // kNN of external queries (any order) against a cloud; outputs original indices.
 template <int KCAP, bool EXACT>
 __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __restrict__ q, int nq, int k,
@@ -2324,6 +2457,15 @@ static int env_knob(const char* name, int dflt) {   // development knobs (A/B of
 }
 bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo) {
   const int nb = group_blocks(c.n);
+  static const int two_lanes = env_knob("DDLO_COV_2LANE", 1);   // two lanes per query (A/B)
+  if (two_lanes && !redo && (k == 10 || k == 20)) {
+    const int nb2 = std::max(1, std::min(cdiv(cdiv(c.n, 32), 4), 8192));
+    static const int occ = env_knob("DDLO_COV_OCC", 3);
+    if (k == 10 && occ == 4) k_covariances2<10, true, 4><<<nb2, 256, 0, s>>>(c, k, method, cov6);
+    else if (k == 10) k_covariances2<10, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6);
+    else k_covariances2<20, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6);
+    return true;
+  }
   if (k == 10) k_covariances<10, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
   else if (k == 20) k_covariances<20, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
   else if (k <= 16) k_covariances<16, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
