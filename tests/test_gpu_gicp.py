@@ -57,6 +57,19 @@ def test_covariances_other_k_vs_oracle(s2s_golden, k):
     assert_cov_parity(src, k, c.get_covariances(TARGET), O.covariances(src, k))
 
 
+@pytest.mark.parametrize("n,k", [(n, k) for n in [10, 20, 31, 32, 33, 63, 65, 1000, 2049] for k in [10, 20] if k <= n])
+def test_covariances_ragged_sizes_vs_oracle(n, k):
+    """k = 10 / 20 covariances (two lanes per query, 32 queries per wavefront:
+    partial leaves, single and partial wavefronts) against the oracle."""
+    rng = np.random.default_rng(n * 7 + k)
+    pts = (rng.standard_normal((n, 3)) * [8, 8, 1]).astype(np.float32)
+    c = P.Context(0)
+    c.set_params(P.default_params(k_correspondences=k))
+    c.set_target(pts)
+    c.compute_covariances(TARGET)
+    assert_cov_parity(pts, k, c.get_covariances(TARGET), O.covariances(pts, k))
+
+
 @pytest.mark.parametrize("k", [10, 20, 7, 32])
 def test_covariances_task_knn_matches(s2s_golden, k, monkeypatch):
     """The opt-in task-based kNN (knn_tasks.hip, DDLO_COV_TASKS=1) is exact:
