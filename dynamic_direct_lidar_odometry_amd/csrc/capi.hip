@@ -96,7 +96,7 @@ int env_int(const char* name, int dflt) {
 // The search's development knobs, read from the environment once per
 // process, not on every align (host time between aligns).
 struct SearchKnobs {
-  float split_extent, hard_extent, tri_mv, reuse_gap, reuse_gap0, reuse_rec_eps, reuse_rec_conv;
+  float split_extent, hard_extent, probe, probe_d, tri_mv, reuse_gap, reuse_gap0, reuse_rec_eps, reuse_rec_conv;
   int list_flush, xcd_scan, pf_ratio, hard_blocks, prev_window, reuse, reuse_rec0;
 };
 const SearchKnobs& search_knobs() {
@@ -110,6 +110,8 @@ const SearchKnobs& search_knobs() {
     v.hard_blocks = env_int("DDLO_HARD_BLOCKS", 10);
     v.prev_window = env_int("DDLO_PREV_WINDOW", 2);
     v.tri_mv = env_float("DDLO_TRI_MV", 0.2f);
+    v.probe = env_float("DDLO_PROBE", 1.0f);
+    v.probe_d = env_float("DDLO_PROBE_D", 0.5f);
     v.reuse = search_uses_tasks() ? env_int("DDLO_REUSE", 1) : 0;
     v.reuse_gap = env_float("DDLO_REUSE_GAP", 0.05f);
     v.reuse_gap0 = env_float("DDLO_REUSE_GAP0", 0.f);
@@ -200,6 +202,8 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.hard_blocks = kn.hard_blocks;
   j.prev_window = kn.prev_window;
   j.tri_mv = kn.tri_mv;
+  j.probe2 = kn.probe * kn.probe;
+  j.probe_d = kn.probe_d;
   j.reuse = kn.reuse;
   j.reuse_gap = kn.reuse_gap;
   j.reuse_gap0 = kn.reuse_gap0;

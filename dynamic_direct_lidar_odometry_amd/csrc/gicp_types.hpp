@@ -133,6 +133,9 @@ struct AlignJob {
   int pf_ratio;                  // collect: lane-per-leaf pair tests below this queries / leaf-rounds ratio (speed only)
   int prev_window;         // seed after a large pose step: 0 previous match only, 1 + Morton window around it,
                            // 2 + Morton window at the new position (default)
+  float probe2;            // fused seed: a sub-group with a windowed query still above this (squared m) probes the
+                           // Morton windows of 8 points around its centre (0 = off)
+  float probe_d;           // their offset from the centre (m)
   float tri_mv;            // a query that moved less than this (m) since the last linearize seeds from the
                            // triangle bound alone (no load); else from the previous match / Morton window
   // Verified match reuse across outer iterations: per query

@@ -1003,6 +1003,51 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         }
       }
     }
+    // Probe seeds: a sub-group whose Morton windows found nothing near (its
+    // queries sit off every surface near their own Morton positions, e.g.
+    // 0.4-0.5 m off a wall under the guess pose, and keep a bound near the
+    // cap) takes the Morton windows of 8 points around its centre, offset by
+    // probe_d along +-x, +-y, +-z and the two xy diagonals: 8 points each,
+    // staged in LDS, every query their exact distances (real candidates, so
+    // exactness is kept; group sharing below spreads them).
+    if constexpr (FUSED) {
+      const float pt2 = job->probe2;
+      if (pt2 > 0.f && pt2 < 0.5f * cap2 && __any(need_seed && vis.best > pt2)) {   // radius < 0.71 x the cap
+        // centre: the first active query (the sub-group is Morton-compact)
+        const unsigned long long am = __ballot(active);
+        const int c0 = am ? __builtin_ctzll(am) : 0;
+        const float cx = readlane_f(qx, c0), cy = readlane_f(qy, c0), cz = readlane_f(qz, c0);
+        const float d = job->probe_d, dd = d * 0.70710678f;
+        const int pr = lane & 7;
+        const float ox = pr == 0 ? d : pr == 1 ? -d : pr == 6 ? dd : pr == 7 ? -dd : 0.f;
+        const float oy = pr == 2 ? d : pr == 3 ? -d : pr == 6 ? dd : pr == 7 ? -dd : 0.f;
+        const float oz = pr == 4 ? d : pr == 5 ? -d : 0.f;
+        const unsigned long long pk = morton_key(cx + ox, cy + oy, cz + oz, tgt.quant);
+        int plo, phi;
+        dir_range(tgt.dir, pk, plo, phi);
+        const int plb = group_lower_bound<8>(tgt.keys, tgt.n, pk, plo, phi);
+        const int cand = min(max(plb - 4 + (lane >> 3), 0), tgt.n - 1);
+        const float4 p = ldg4(tgt.pts, cand);
+        f4v* const CP = TL->sb_lo;   // 64 staged candidates (the walk's box stage, free until the walk)
+        CP[lane] = f4v{p.x, p.y, p.z, __int_as_float(cand)};
+        __builtin_amdgcn_wave_barrier();
+        unsigned long long bk = dkey(vis.best, vis.bestj);
+        const int s4 = lane / Q;
+#pragma unroll 4
+        for (int k = 0; k < 64 / (64 / Q); ++k) {
+          const f4v c = CP[s4 * (64 / (64 / Q)) + k];
+          bk = umin64(bk, dkey(dist2(qx, qy, qz, c.x, c.y, c.z), __float_as_int(c.w)));
+        }
+        vis.merge_slices(bk);
+        __builtin_amdgcn_wave_barrier();
+        if (active && bk < dkey(vis.best, vis.bestj)) {
+          vis.best = __uint_as_float((unsigned)(bk >> 32));
+          vis.bestj = (int)(unsigned)bk;
+          have_bp = false;
+          seeded = true;
+        }
+      }
+    }
     // Group sharing: every query also takes the exact distance to the other
     // queries' candidate points (Morton-adjacent queries are spatially
     // adjacent, so a neighbour's candidate is often far closer than the
