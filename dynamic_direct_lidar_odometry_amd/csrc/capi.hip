@@ -133,7 +133,7 @@ struct SearchLayout {
     qstate = 0;
     key = al(sizeof(float4) * (size_t)ns);
     ctr = key + al(sizeof(unsigned long long) * (size_t)ns);
-    hard_list = ctr + al(sizeof(unsigned) * kTaskCounters * kCtrStride);
+    hard_list = ctr + al(sizeof(unsigned) * (kTaskCounters + 1) * kCtrStride);   // + the moment kernel's arrival counter
     hard_flag = hard_list + al(sizeof(int) * kHardMax);
     grp_blocks = hard_flag + al((size_t)ns / 16 + 16);
     ref = grp_blocks + al(sizeof(unsigned short) * ((size_t)ns / 16 + 16));
@@ -215,7 +215,11 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
 }
 
 int linearize_blocks(int nsrc) { return linearize_geometry(nsrc, 0).mom_blocks; }   // slab rows
-LinGeom geometry(const gicp_ctx* c) { return linearize_geometry(c->src.cloud->n, c->tgt.cloud->upper_count()); }
+LinGeom geometry(const gicp_ctx* c) {
+  LinGeom g = linearize_geometry(c->src.cloud->n, c->tgt.cloud->upper_count());
+  g.fuse_lm = !c->comm && lm_fusion_enabled();   // a sharded align all-reduces between the moments and the LM step
+  return g;
+}
 
 gicp_status prepare_align(gicp_ctx* c) {
   if (!c->src.cloud) return fail(GICP_ENOSOURCE, "no source cloud");
@@ -260,12 +264,13 @@ constexpr int kMaxFirstChunk = 8;  // largest predicted first chunk (iterations)
 // the LM/GN step, replicated bit-identically on every rank.
 gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks) {
   (void)nblocks;   // = geometry(c).mom_blocks (fill_job)
-  launch_linearize(c->stream, jd, geometry(c));
+  const LinGeom g = geometry(c);
+  launch_linearize(c->stream, jd, g);
   if (c->comm) {
     launch_mom_reduce(c->stream, jd);
     NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
   }
-  launch_lm_step(c->stream, jd);
+  if (!g.fuse_lm) launch_lm_step(c->stream, jd);
   return GICP_OK;
 }
 
@@ -414,7 +419,9 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
   launch_align_init(c->stream, jd);
   for (int i = 0; i < max_it; ++i) {
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i], c->stream));
-    launch_linearize(c->stream, jd, geometry(c));
+    LinGeom g = geometry(c);
+    g.fuse_lm = false;   // profiled aligns time the linearize on its own
+    launch_linearize(c->stream, jd, g);
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i + 1], c->stream));
     if (c->comm) {
       launch_mom_reduce(c->stream, jd);
@@ -427,6 +434,16 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
 }
 
 }  // namespace
+
+namespace ddlo {
+bool lm_fusion_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("DDLO_FUSE_LM");
+    return v && *v && std::atoi(v) != 0;
+  }();
+  return on;
+}
+}  // namespace ddlo
 
 extern "C" {
 

@@ -731,7 +731,7 @@ constexpr int kSeedW = 8;           // Morton-window seed points per slice lane
 
 __global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
-  if (threadIdx.x < kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;
+  if (threadIdx.x <= kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;   // + the moment kernel's arrival counter
   if (threadIdx.x < 64) {   // source radius from the top-level boxes (<= 64 of them)
     const CloudDev& c = job->src;
     const int top = c.nlevels - 1;
@@ -1656,6 +1656,15 @@ constexpr int kMomWaves = 8;    // waves per moment block (512 threads: 256 bloc
 // (A last-block-done fusion of k_lm_step into this kernel measured slower:
 // 27.3 us against 9 + 13.5 us — every block's agent-scope release writes
 // back its XCD's L2 before the completion counter.)
+__device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job);
+
+// FUSE_LM: the LM step runs in the last block to finish (one block per CU:
+// 256 blocks), handed off without a release fence -- each block stores its
+// slab row write-through (sc1), drains it (vmcnt(0)), and one lane adds to
+// an arrival counter (memory-side atomic); the block that arrives last takes
+// one agent-scope acquire and reads the slab with plain loads
+// (MI355X_MICROARCH.md "visibility", the split-K form of Guideline 16).
+template <bool FUSE_LM>
 __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
@@ -1777,9 +1786,32 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     double sum = 0.0;
     if (threadIdx.x < kMoments)
       for (int w = 0; w < kMomWaves; ++w) sum += red[w][threadIdx.x];
-    slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = sum;
+    if constexpr (FUSE_LM)
+      __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)(slab + (size_t)blockIdx.x * kSlabStride +
+                                                                                 threadIdx.x),
+                         (unsigned long long)__double_as_longlong(sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = sum;
+  }
+  if constexpr (FUSE_LM) {
+    __shared__ int last_s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its sc1 slab stores are done
+    __syncthreads();
+    unsigned* const arrive = job->task_ctr + kTaskCounters * kCtrStride;
+    if (threadIdx.x == 0) last_s = atomicAdd(arrive, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last_s) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      atomicExch(arrive, 0u);   // re-armed for the next iteration (k_align_init zeroes it per align)
+    }
+    __syncthreads();
+    lm_step_body(job);
   }
 }
+template __global__ void k_moments<false>(const AlignJob*);
+template __global__ void k_moments<true>(const AlignJob*);
 
 // ---------------------------------------------------------------------------
 // K5: slab reduction + LM/GN step on one workgroup.
@@ -2083,9 +2115,8 @@ __global__ __launch_bounds__(kLmThreads) void k_mom_reduce(const AlignJob* __res
 #else
 #define LM_PROF(i)
 #endif
-__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job) {
+__device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
-  if (__builtin_amdgcn_readfirstlane(st->done)) return;
 #ifdef DDLO_LM_PROF
   unsigned long long lm_t[6];
 #endif
@@ -2326,6 +2357,11 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
     printf("lm_prof %d %llu %llu %llu %llu %llu\n", it_pre, lm_t[1] - lm_t[0], lm_t[2] - lm_t[1], lm_t[3] - lm_t[2],
            lm_t[4] - lm_t[3], lm_t[5] - lm_t[4]);
 #endif
+}
+
+__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job) {
+  if (__builtin_amdgcn_readfirstlane(job->state->done)) return;
+  lm_step_body(job);
 }
 
 // ---------------------------------------------------------------------------
@@ -2599,7 +2635,8 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
     else if (occ_scan == 5) k_nn_scan<5, 6><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);   // 6-task batches: 7.5 KB LDS per wave
     else k_nn_scan<4><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
   }
-  k_moments<<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
+  if (g.fuse_lm) k_moments<true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
+  else k_moments<false><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
 }
 int search_queries_per_wave() { return kSearchQ; }
 int task_cap_per_region(int nsrc) {

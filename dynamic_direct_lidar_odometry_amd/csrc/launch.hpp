@@ -33,7 +33,9 @@ void launch_align_init(hipStream_t s, const AlignJob* job);
 // cloud size; part of the chunk-graph key.
 struct LinGeom {
   int seed_blocks, collect_blocks, scan_blocks, mom_blocks, lds_boxes;
+  bool fuse_lm = false;   // the LM step runs in the moment kernel's last block (no k_lm_step launch)
 };
+bool lm_fusion_enabled();   // DDLO_FUSE_LM (unsharded graph aligns)
 LinGeom linearize_geometry(int nsrc, int tgt_upper);
 void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g);
 int search_queries_per_wave();
