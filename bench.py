@@ -347,7 +347,7 @@ def main():
     ap.add_argument("--no-batch", action="store_true", help="skip the frame-parallel S2S cfg5 leg")
     ap.add_argument("--batch-frames", type=int, default=1000)
     ap.add_argument("--batch-unique", type=int, default=20)
-    ap.add_argument("--batch-streams", type=int, default=2)
+    ap.add_argument("--batch-streams", type=int, default=3)
     ap.add_argument("--no-gn", action="store_true", help="skip the cfg2 S2S 20-GN-iteration leg")
     ap.add_argument("--gn-steps", type=int, default=10)
     ap.add_argument("--no-odom", action="store_true", help="skip the cfg5 odometry-driver (S2M chain) leg")
