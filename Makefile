@@ -8,7 +8,7 @@ PKG := dynamic_direct_lidar_odometry_amd
 CSRC := $(PKG)/csrc
 LIBDIR := $(PKG)/_lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
-OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o $(LIBDIR)/segment.o
+OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/nftree.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o $(LIBDIR)/segment.o
 
 all: lib oracle facade
 
@@ -19,6 +19,10 @@ $(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(CSRC)/search.hpp $(CSRC)/nn_tasks.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIBDIR)/knn_tasks.o: $(CSRC)/knn_tasks.hip $(CSRC)/search.hpp $(CSRC)/nn_tasks.hpp $(CSRC)/cov_math.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/nftree.o: $(CSRC)/nftree.hip $(CSRC)/nftree.hpp $(CSRC)/cov_math.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -39,7 +43,7 @@ $(LIBDIR)/segment.o: $(CSRC)/segment.hip $(CSRC)/runtime.hpp $(CSRC)/gicp_types.
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIBDIR)/libddlo_gicp.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,--no-undefined -o $@ $(OBJS)
 
 oracle:
 	$(MAKE) -C oracle

@@ -128,6 +128,8 @@ def load():
         "gicp_get_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
         "gicp_s2s_batch": (I, [I, C.POINTER(GicpParams), P, P, S, I, I, P, P]),
         "gicp_residual_image": (I, [P, D, D, I, I, P, P]),
+        "gicp_set_tie_order": (I, [P, I]),
+        "gicp_debug_nftree": (I, [P, I, P, P, P, S, C.POINTER(S)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -330,6 +332,22 @@ class Context:
         d = np.zeros((len(q), k), np.float32)
         self._check(self.L.gicp_knn_target(self.h, _ptr(q), len(q), stride, k, _ptr(idx), _ptr(d)))
         return idx, d
+
+    def set_tie_order(self, nanoflann_order=True):
+        """Exact distance ties in nanoflann's traversal order (default) or by Morton position."""
+        self._check(self.L.gicp_set_tie_order(self.h, 1 if nanoflann_order else 0))
+
+    def nftree(self, side):
+        """nanoflann's kd-tree of a side's cloud as built on the device: (vind, nodes (c1, c2, feat, parent),
+        div (divlow, divhigh))."""
+        nn = C.c_size_t(0)
+        self._check(self.L.gicp_debug_nftree(self.h, side, None, None, None, 0, C.byref(nn)))
+        n = self.size(side)
+        vind = np.empty(n, np.int32)
+        nodes = np.empty((nn.value, 4), np.int32)
+        div = np.empty((nn.value, 2), np.float32)
+        self._check(self.L.gicp_debug_nftree(self.h, side, _ptr(vind), _ptr(nodes), _ptr(div), nn.value, C.byref(nn)))
+        return vind, nodes, div
 
     def debug_stats(self, enable=True, read=False):
         """Per 64-query group search counters of the last linearize (development)."""

@@ -490,6 +490,10 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
+  {
+    const char* v = std::getenv("DDLO_TIE_EXACT");   // A/B of the tie resolution (default: nanoflann's order)
+    c->tie_exact = !(v && *v == '0');
+  }
   *out = c.release();
   return GICP_OK;
 }
@@ -508,6 +512,7 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   if (c->job_host) (void)hipHostFree(c->job_host);
   if (c->state_host) (void)hipHostFree(c->state_host);
   if (c->flag_host) (void)hipHostFree(c->flag_host);
+  if (c->nf_err_host) (void)hipHostFree(c->nf_err_host);
   c->src = Side();
   c->tgt = Side();
   (void)hipStreamDestroy(c->stream);
@@ -540,15 +545,28 @@ gicp_status gicp_get_params(const gicp_ctx* c, gicp_params* out) {
 }
 
 gicp_status gicp_set_source(gicp_ctx* c, const float* xyz, size_t n, size_t stride, int build_index) {
-  (void)build_index;  // the device cloud is always sorted + indexed (cheap)
   if (!c) return fail(GICP_EINVAL, "null ctx");
   gicp_status s = set_device(c);
   if (s) return s;
   std::shared_ptr<CloudData> cd;
-  s = build_cloud(c, xyz, n, stride, &cd);
+  s = build_cloud(c, xyz, n, stride, &cd);   // the device cloud is always sorted + indexed (cheap)
   if (s) return s;
+  const Side old = c->src;
   c->src.cloud = cd;
   c->src.cov.reset();  // setInputSource clears source covariances (:142)
+  if (!build_index && old.has_cov() && old.cloud->n == (int)n) {
+    // registerInputSource (:122-130) keeps source_covs_: covariance i stays
+    // with point i of the new cloud (a size mismatch is recomputed at align,
+    // :186-189, so it is dropped here)
+    auto cv = std::make_shared<CovData>();
+    cv->n = (int)n;
+    HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * n));
+    launch_cov_remap(c->stream, old.cov->cov6.as<double>(), old.cloud->inv_perm.as<int>(), cd->perm.as<int>(), (int)n,
+                     cv->cov6.as<double>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->src.cov = cv;
+  }
   invalidate_align(c);
   return GICP_OK;
 }
@@ -593,7 +611,7 @@ gicp_status gicp_compute_covariances(gicp_ctx* c, int side) {
   s = compute_cov(c, side == GICP_SIDE_SOURCE ? c->src : c->tgt);
   if (s) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
-  return GICP_OK;
+  return check_ties(c);
 }
 
 gicp_status gicp_set_covariances(gicp_ctx* c, int side, const double* cov, size_t n, int layout) {
@@ -720,6 +738,8 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
       res->linearize_ms = tot;
     }
   }
+  s = check_ties(c);
+  if (s) return s;
   if (st.lm_failed) g_last_error = "lm not converged!!";
   return GICP_OK;
 }
@@ -883,11 +903,60 @@ gicp_status gicp_knn_target(gicp_ctx* c, const float* q, size_t nq, size_t strid
   HIP_TRY(c->tmp_out.ensure((sizeof(int) + sizeof(float)) * nq * k + 64));
   int* didx = c->tmp_out.as<int>();
   float* dd = reinterpret_cast<float*>(c->tmp_out.as<char>() + ((sizeof(int) * nq * k + 63) / 64) * 64);
-  if (!launch_knn_query(c->stream, c->tgt.cloud->dev(), c->raw_pts.as<float4>(), (int)nq, k, didx, dd))
+  TieList tl{nullptr, nullptr};
+  if (c->tie_exact) {   // tied answers are re-run in nanoflann's order (nftree.hip)
+    s = ensure_nftree(c, *c->tgt.cloud, c->stream);
+    if (!s) s = tie_scratch(c, (int)nq, c->stream, &tl);
+    if (s) return s;
+  }
+  if (!launch_knn_query(c->stream, c->tgt.cloud->dev(), c->raw_pts.as<float4>(), (int)nq, k, didx, dd, tl))
     return fail(GICP_EINVAL, "unsupported k");
+  if (c->tie_exact) {
+    launch_nf_resolve_knn(c->stream, c->tgt.cloud->nf->dev(), c->raw_pts.as<float4>(), tl.list, tl.count, k, didx, dd,
+                          c->tgt.cloud->nf->status.as<int>(), c->nf_err.as<int>());
+    s = publish_ties(c, c->stream);
+    if (s) return s;
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(idx, didx, sizeof(int) * nq * k, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(sqd, dd, sizeof(float) * nq * k, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return check_ties(c);
+}
+
+gicp_status gicp_set_tie_order(gicp_ctx* c, int nanoflann_order) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  c->tie_exact = nanoflann_order != 0;
+  return GICP_OK;
+}
+
+gicp_status gicp_debug_nftree(gicp_ctx* c, int side, int32_t* vind, int32_t* nodes4, float* div2, size_t cap,
+                              size_t* nnodes) {
+  if (!c || (side != 0 && side != 1) || !nnodes) return fail(GICP_EINVAL, "invalid argument");
+  Side& sd = side == GICP_SIDE_SOURCE ? c->src : c->tgt;
+  if (!sd.cloud) return fail(GICP_ESTATE, "no cloud on this side");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  s = ensure_nftree(c, *sd.cloud, c->stream);
+  if (s) return s;
+  const NfTreeData& t = *sd.cloud->nf;
+  int st[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(st, t.status.p, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (st[0]) return fail(GICP_EHIP, "nanoflann tree build failed (error bits " + std::to_string(st[0]) + ")");
+  *nnodes = (size_t)st[1];
+  if (!vind && !nodes4 && !div2) return GICP_OK;
+  if (cap < (size_t)st[1]) return fail(GICP_EINVAL, "node capacity too small");
+  const int n = t.n;
+  DevBuf dv, dn, df;
+  HIP_TRY(dv.ensure(sizeof(int) * (size_t)n));
+  HIP_TRY(dn.ensure(sizeof(int) * 4 * (size_t)st[1]));
+  HIP_TRY(df.ensure(sizeof(float) * 2 * (size_t)st[1]));
+  launch_nf_export(c->stream, t.dev(), t.status.as<int>(), st[1], dv.as<int>(), dn.as<int>(), df.as<float>());
+  HIP_TRY(hipGetLastError());
+  if (vind) HIP_TRY(hipMemcpyAsync(vind, dv.p, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  if (nodes4) HIP_TRY(hipMemcpyAsync(nodes4, dn.p, sizeof(int) * 4 * (size_t)st[1], hipMemcpyDeviceToHost, c->stream));
+  if (div2) HIP_TRY(hipMemcpyAsync(div2, df.p, sizeof(float) * 2 * (size_t)st[1], hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return GICP_OK;
 }

@@ -156,6 +156,66 @@ struct AlignJob {
   unsigned* sec;                 // [n_src] fp32 bits: smallest squared distance of an examined non-best point
 };
 
+// ---------------------------------------------------------------------------
+// nanoflann's kd-tree on the device (nftree.hpp / nftree.hip): only used to
+// resolve exact distance ties in nanoflann's traversal order.
+// nanoflann Node (reference impl/nanoflann_impl.hpp:876-894): a leaf holds the
+// vind range [c1, c2); an inner node its children and divfeat / divlow / divhigh.
+struct NfNode {
+  int c1, c2;
+  int feat;            // divfeat; -1 = leaf
+  float divlow, divhigh;
+  int parent;          // -1 at the root (build bookkeeping)
+  int pad0, pad1;
+};
+
+struct NfTreeDev {
+  const float4* vpts;  // [n] points in vind order: x, y, z, original index (int bits)
+  const NfNode* nodes; // node 0 = root
+  const float4* box;   // [2 * node + 0/1] the node's bounding box (lo / hi); node 0's = root_bbox
+  int n;
+};
+
+constexpr int kNfMaxLevels = 40;   // big levels of the device build (deeper: the build reports a failure)
+
+struct NfCtl {
+  int nnodes, nsmall, err;   // err bits: 1 node capacity, 2 node left too large, 4 depth, 8 list capacity
+  int nchunks[2];
+  int ntask[kNfMaxLevels + 1];
+};
+
+// A node to split: its vind range, the box divideTree passes down (the
+// middleSplit_ bbox argument) and its points' min / max (ordered uints).
+struct NfTask {
+  int node, begin, count, chunk0;
+  float lo[3], hi[3];
+  unsigned mm[6];
+  int feat;
+  float cut;
+  int nch, pad;
+};
+
+struct NfBuild {
+  float4* vpts;            // [n] in: original order (x, y, z, index); out: vind order
+  NfNode* nodes;
+  float4* box;             // [2 * cap]
+  int cap;                 // node capacity
+  NfCtl* ctl;
+  NfTask* tasks;           // [(Lmax + 1) * max_task]
+  NfTask* pend;            // [(Lmax + 1) * max_pend] children produced by the level above
+  NfTask* small;           // [max_small]
+  int* chunk_task;         // [2 * max_chunks]
+  int *cA, *cAE, *cE2;     // [max_chunks] per-chunk counts
+  float4 *tblL, *tblR;     // [n] rank tables of the Hoare pairing
+  int* arrive;             // [cap] refit arrival counters (zeroed)
+  const float* quant;      // the cloud's bbox: min [0..2], max [4..6]
+  int n, Lmax, max_task, max_pend, max_small, max_chunks;
+};
+
+struct NfSizes {
+  int Lmax, max_task, max_pend, max_small, max_chunks;
+};
+
 // Task-based kNN-k of a cloud's own points (covariances, knn_tasks.hip).
 struct KnnJob {
   CloudDev c;

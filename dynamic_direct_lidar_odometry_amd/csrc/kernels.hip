@@ -235,6 +235,8 @@ struct KnnVisitor : VisitStats {
   unsigned long long wk;   // worst kept key (bound)
   float wd;                // its distance
   float tight;             // min over the tested full leaves of the farthest-corner distance (squared)
+  float td;                // smallest distance of an examined point that is not kept (tie detection:
+                           // the k-th distance is tied iff it equals td at the end)
   int nfull;               // leaves < nfull hold 32 real points (>= k: each such box bounds the k-th neighbour)
   int skip_lo, skip_hi;
 
@@ -247,9 +249,37 @@ struct KnnVisitor : VisitStats {
     wk = K[0];
     wd = INFINITY;
     tight = INFINITY;
+    td = INFINITY;
     nfull = 0;
     skip_lo = 1;
     skip_hi = 0;
+  }
+  // k-th distance (slot k - 1) and whether an examined point outside the
+  // kept k lies at exactly that distance (nanoflann then keeps the one its
+  // walk met first)
+  __device__ __forceinline__ float kth_dist() const {
+    float d = INFINITY;
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s)
+      if (s == k - 1) d = dist(s);
+    return d;
+  }
+  __device__ __forceinline__ float outside_min() const {   // td, plus slot k of an oversized list
+    float t = td;
+    if constexpr (!EXACT) {
+#pragma unroll
+      for (int s = 0; s < KCAP; ++s)
+        if (s == k) t = fminf(t, dist(s));
+    }
+    return t;
+  }
+  // any two of the kept k at the same distance (their order is nanoflann's walk order)
+  __device__ __forceinline__ bool inner_tie() const {
+    bool t = false;
+#pragma unroll
+    for (int s = 1; s < KCAP; ++s)
+      if (s < k) t |= dist(s) == dist(s - 1);
+    return t;
   }
   __device__ __forceinline__ void update_worst() {
     if constexpr (EXACT) {
@@ -268,6 +298,7 @@ struct KnnVisitor : VisitStats {
       key = key < K[s] ? K[s] : key;
       K[s] = lo;
     }
+    td = fminf(td, key_dist(key));   // the key pushed out of the list
     update_worst();
   }
   // the k-th neighbour is no farther than the kept k-th key, nor than the
@@ -282,6 +313,7 @@ struct KnnVisitor : VisitStats {
       const float d = dist2(qx, qy, qz, L->px[j], L->py[j], L->pz[j]);
       const unsigned long long key = dkey(d, start + j);
       if (active && key < wk && d <= tight) insert(key);   // d > tight: not among the k nearest
+      else td = fminf(td, d);
     }
   }
   __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
@@ -294,6 +326,45 @@ struct KnnVisitor : VisitStats {
     return scan_leaves_lds(c, base, ex, *this, L);
   }
 };
+
+// Mean and biased covariance of the kept neighbours in their order
+// (nano_gicp_impl.hpp:392-399), regularised, stored as sym6.  The neighbour
+// points are loaded four at a time (compiler barriers between the groups):
+// with all KCAP loads hoisted, k = 20 held 20 float4s live and spilled.
+template <int KCAP>
+__device__ __forceinline__ void cov_from_keys(const CloudDev& c, const unsigned long long (&K)[KCAP], int k, int method,
+                                              double* o) {
+  double mx = 0, my = 0, mz = 0;
+#pragma unroll
+  for (int s = 0; s < KCAP; ++s) {
+    if (s < k) {
+      const float4 p = ldg4(c.pts, (int)(unsigned)K[s]);
+      mx += (double)p.x;
+      my += (double)p.y;
+      mz += (double)p.z;
+    }
+    if ((s & 3) == 3) asm volatile("" ::: "memory");
+  }
+  mx /= k;
+  my /= k;
+  mz /= k;
+  double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < KCAP; ++s) {
+    if (s < k) {
+      const float4 p = ldg4(c.pts, (int)(unsigned)K[s]);
+      const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
+      C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
+      C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
+      C[6] += d2 * d0; C[7] += d2 * d1; C[8] += d2 * d2;
+    }
+    if ((s & 3) == 3) asm volatile("" ::: "memory");
+  }
+  for (int e = 0; e < 9; ++e) C[e] /= k;
+  double out[6];
+  regularize(C, method, out);
+  for (int e = 0; e < 6; ++e) o[e] = out[e];
+}
 
 // Seed a kNN visitor with the leaves [s0, s1] and then run the full traversal.
 template <int KCAP, bool EXACT>
@@ -328,7 +399,7 @@ __device__ __forceinline__ void knn_self_search(const CloudDev& c, KnnVisitor<KC
 // covariances of a cloud: wave w handles sorted points [64w, 64w+64) (leaves 2w, 2w+1)
 template <int KCAP, bool EXACT>
 __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int method, double* __restrict__ cov6,
-                                                     const unsigned char* __restrict__ redo) {
+                                                     const unsigned char* __restrict__ redo, TieList ties) {
   __shared__ WaveLds lds[4];
   WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -347,36 +418,8 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
     vis.qz = q.z;
     knn_self_search(c, vis, 2 * g - 1, 2 * g + 2, gp(c.keys)[min(i, c.n - 1)], L);
     if (!vis.active) continue;
-    // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
-    double mx = 0, my = 0, mz = 0;
-#pragma unroll
-    for (int s = 0; s < KCAP; ++s) {
-      if (s < k) {
-        const float4 p = ldg4(c.pts, vis.idx(s));
-        mx += (double)p.x;
-        my += (double)p.y;
-        mz += (double)p.z;
-      }
-    }
-    mx /= k;
-    my /= k;
-    mz /= k;
-    double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < KCAP; ++s) {
-      if (s < k) {
-        const float4 p = ldg4(c.pts, vis.idx(s));
-        const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
-        C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
-        C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
-        C[6] += d2 * d0; C[7] += d2 * d1; C[8] += d2 * d2;
-      }
-    }
-    for (int e = 0; e < 9; ++e) C[e] /= k;
-    double out[6];
-    regularize(C, method, out);
-    double* o = cov6 + 6 * (size_t)i;
-    for (int e = 0; e < 6; ++e) o[e] = out[e];
+    if (ties.list && vis.outside_min() == vis.kth_dist()) ties.list[atomicAdd(ties.count, 1)] = i;
+    cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
   }
 }
 
@@ -416,6 +459,7 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
       const float d = dist2(this->qx, this->qy, this->qz, L->px[h0 + j], L->py[h0 + j], L->pz[h0 + j]);
       const unsigned long long key = dkey(d, start + h0 + j);
       if (this->active && key < wk_both() && d <= this->tight) this->insert(key);
+      else this->td = fminf(this->td, d);
     }
     exchange();
   }
@@ -428,26 +472,34 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
   __device__ __forceinline__ bool scan_leaves(const CloudDev& c, int base, unsigned long long ex, WaveLds* L) {
     return scan_leaves_lds(c, base, ex, *this, L);
   }
-  // whole wave: merge the partner's list into this lane's (both end equal)
+  // whole wave: lanes 0-31 merge their partner's list (lane + 32) into their
+  // own; lanes 32-63 keep theirs unchanged, so the partner word each swap
+  // returns is still the partner's original list entry (no copy of the list)
   __device__ __forceinline__ void merge_halves() {
-    unsigned long long own[KCAP];   // the lists as they were: inserts below reorder K
-#pragma unroll
-    for (int s = 0; s < KCAP; ++s) own[s] = this->K[s];
+    const bool low = lane_id() < 32;
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
-      const unsigned lo = (unsigned)own[s], hi = (unsigned)(own[s] >> 32);
+      const unsigned lo = (unsigned)this->K[s], hi = (unsigned)(this->K[s] >> 32);
       const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
       const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
       const unsigned long long other = ((unsigned long long)swap_partner(rh, hi) << 32) | swap_partner(rl, lo);
-      if (other < this->wk) this->insert(other);
+      if (low) {
+        if (other < this->wk) this->insert(other);
+        else this->td = fminf(this->td, key_dist(other));
+      }
     }
+    // both halves' discarded points: the union's
+    const unsigned tb = __float_as_uint(this->td);
+    const auto rt = __builtin_amdgcn_permlane32_swap(tb, tb, false, false);
+    this->td = fminf(__uint_as_float(rt[0]), __uint_as_float(rt[1]));
   }
 };
 
 // covariances with two lanes per query: wave w handles sorted points
 // [32w, 32w+32) (leaf w); seeds leaves w-1 .. w+1
 template <int KCAP, bool EXACT, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, int method, double* __restrict__ cov6) {
+__global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, int method, double* __restrict__ cov6,
+                                                            TieList ties) {
   __shared__ WaveLds lds[4];
   WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -477,46 +529,19 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
     }
     vis.merge_halves();
     if (!vis.active || lane_id() >= 32) continue;
-    // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
-    double mx = 0, my = 0, mz = 0;
-#pragma unroll
-    for (int s = 0; s < KCAP; ++s) {
-      if (s < k) {
-        const float4 p = ldg4(c.pts, vis.idx(s));
-        mx += (double)p.x;
-        my += (double)p.y;
-        mz += (double)p.z;
-      }
-    }
-    mx /= k;
-    my /= k;
-    mz /= k;
-    double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < KCAP; ++s) {
-      if (s < k) {
-        const float4 p = ldg4(c.pts, vis.idx(s));
-        const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
-        C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
-        C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
-        C[6] += d2 * d0; C[7] += d2 * d1; C[8] += d2 * d2;
-      }
-    }
-    for (int e = 0; e < 9; ++e) C[e] /= k;
-    double out[6];
-    regularize(C, method, out);
-    double* o = cov6 + 6 * (size_t)i;
-    for (int e = 0; e < 6; ++e) o[e] = out[e];
+    if (ties.list && vis.td == vis.kth_dist()) ties.list[atomicAdd(ties.count, 1)] = i;
+    cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
   }
 }
-template __global__ void k_covariances2<10, true, 3>(CloudDev, int, int, double*);
-template __global__ void k_covariances2<10, true, 4>(CloudDev, int, int, double*);
-template __global__ void k_covariances2<20, true, 3>(CloudDev, int, int, double*);
+template __global__ void k_covariances2<10, true, 3>(CloudDev, int, int, double*, TieList);
+template __global__ void k_covariances2<10, true, 4>(CloudDev, int, int, double*, TieList);
+template __global__ void k_covariances2<20, true, 3>(CloudDev, int, int, double*, TieList);
+template __global__ void k_covariances2<20, true, 2>(CloudDev, int, int, double*, TieList);
 
 // kNN of external queries (any order) against a cloud; outputs original indices.
 template <int KCAP, bool EXACT>
 __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __restrict__ q, int nq, int k,
-                                                   int* __restrict__ out_idx, float* __restrict__ out_d) {
+                                                   int* __restrict__ out_idx, float* __restrict__ out_d, TieList ties) {
   __shared__ WaveLds lds[4];
   WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -538,6 +563,7 @@ __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __r
     const int leaf = min(pos, c.n - 1) / kLeafSize;
     knn_search(c, vis, leaf - 1, leaf + 1, L);
     if (!vis.active) continue;
+    if (ties.list && (vis.outside_min() == vis.kth_dist() || vis.inner_tie())) ties.list[atomicAdd(ties.count, 1)] = i;
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
       if (s < k) {
@@ -550,17 +576,17 @@ __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __r
 }
 
 
-template __global__ void k_covariances<10, true>(CloudDev, int, int, double*, const unsigned char*);
-template __global__ void k_covariances<20, true>(CloudDev, int, int, double*, const unsigned char*);
-template __global__ void k_covariances<16, false>(CloudDev, int, int, double*, const unsigned char*);
-template __global__ void k_covariances<32, false>(CloudDev, int, int, double*, const unsigned char*);
-template __global__ void k_covariances<64, false>(CloudDev, int, int, double*, const unsigned char*);
-template __global__ void k_knn_query<1, true>(CloudDev, const float4*, int, int, int*, float*);
-template __global__ void k_knn_query<10, true>(CloudDev, const float4*, int, int, int*, float*);
-template __global__ void k_knn_query<20, true>(CloudDev, const float4*, int, int, int*, float*);
-template __global__ void k_knn_query<16, false>(CloudDev, const float4*, int, int, int*, float*);
-template __global__ void k_knn_query<32, false>(CloudDev, const float4*, int, int, int*, float*);
-template __global__ void k_knn_query<64, false>(CloudDev, const float4*, int, int, int*, float*);
+template __global__ void k_covariances<10, true>(CloudDev, int, int, double*, const unsigned char*, TieList);
+template __global__ void k_covariances<20, true>(CloudDev, int, int, double*, const unsigned char*, TieList);
+template __global__ void k_covariances<16, false>(CloudDev, int, int, double*, const unsigned char*, TieList);
+template __global__ void k_covariances<32, false>(CloudDev, int, int, double*, const unsigned char*, TieList);
+template __global__ void k_covariances<64, false>(CloudDev, int, int, double*, const unsigned char*, TieList);
+template __global__ void k_knn_query<1, true>(CloudDev, const float4*, int, int, int*, float*, TieList);
+template __global__ void k_knn_query<10, true>(CloudDev, const float4*, int, int, int*, float*, TieList);
+template __global__ void k_knn_query<20, true>(CloudDev, const float4*, int, int, int*, float*, TieList);
+template __global__ void k_knn_query<16, false>(CloudDev, const float4*, int, int, int*, float*, TieList);
+template __global__ void k_knn_query<32, false>(CloudDev, const float4*, int, int, int*, float*, TieList);
+template __global__ void k_knn_query<64, false>(CloudDev, const float4*, int, int, int*, float*, TieList);
 
 // covariance import/export between original order (host layout) and sorted sym6
 __global__ __launch_bounds__(256) void k_cov_import(const double* __restrict__ in, int layout, int n,
@@ -592,6 +618,19 @@ __global__ __launch_bounds__(256) void k_cov_export(const double* __restrict__ c
     double* m = out + 6 * (size_t)i;
     for (int e = 0; e < 6; ++e) m[e] = c[e];
   }
+}
+
+// registerInputSource keeps source_covs_ (nano_gicp_impl.hpp:122-130): the
+// covariance of original index o moves from the old cloud's sorted position
+// to the new one's
+__global__ __launch_bounds__(256) void k_cov_remap(const double* __restrict__ old_cov6,
+                                                   const int* __restrict__ old_inv_perm,
+                                                   const int* __restrict__ new_perm, int n, double* __restrict__ cov6) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;   // new sorted index
+  if (s >= n) return;
+  const double* src = old_cov6 + 6 * (size_t)old_inv_perm[new_perm[s]];
+  double* o = cov6 + 6 * (size_t)s;
+  for (int e = 0; e < 6; ++e) o[e] = src[e];
 }
 
 // ============================================================================
@@ -2536,33 +2575,38 @@ static int env_knob(const char* name, int dflt) {   // development knobs (A/B of
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : dflt;
 }
-bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo) {
+bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo,
+                        TieList ties) {
   const int nb = group_blocks(c.n);
   static const int two_lanes = env_knob("DDLO_COV_2LANE", 1);   // two lanes per query (A/B)
   if (two_lanes && !redo && (k == 10 || k == 20)) {
     const int nb2 = std::max(1, std::min(cdiv(cdiv(c.n, 32), 4), 8192));
     static const int occ = env_knob("DDLO_COV_OCC", 3);
-    if (k == 10 && occ == 4) k_covariances2<10, true, 4><<<nb2, 256, 0, s>>>(c, k, method, cov6);
-    else if (k == 10) k_covariances2<10, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6);
-    else k_covariances2<20, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6);
+    // k = 20 at 2 waves / SIMD: 191 VGPRs, no spills (3 waves: 168 VGPRs + 16 spilled; DDLO_COV_OCC20=3)
+    static const int occ20 = env_knob("DDLO_COV_OCC20", 2);
+    if (k == 10 && occ == 4) k_covariances2<10, true, 4><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties);
+    else if (k == 10) k_covariances2<10, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties);
+    else if (occ20 == 3) k_covariances2<20, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties);
+    else k_covariances2<20, true, 2><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties);
     return true;
   }
-  if (k == 10) k_covariances<10, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
-  else if (k == 20) k_covariances<20, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
-  else if (k <= 16) k_covariances<16, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
-  else if (k <= 32) k_covariances<32, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
-  else if (k <= 64) k_covariances<64, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo);
+  if (k == 10) k_covariances<10, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo, ties);
+  else if (k == 20) k_covariances<20, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo, ties);
+  else if (k <= 16) k_covariances<16, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo, ties);
+  else if (k <= 32) k_covariances<32, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo, ties);
+  else if (k <= 64) k_covariances<64, false><<<nb, 256, 0, s>>>(c, k, method, cov6, redo, ties);
   else return false;
   return true;
 }
-bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq, int k, int* out_idx, float* out_d) {
+bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq, int k, int* out_idx, float* out_d,
+                      TieList ties) {
   const int nb = group_blocks(nq);
-  if (k == 1) k_knn_query<1, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
-  else if (k == 10) k_knn_query<10, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
-  else if (k == 20) k_knn_query<20, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
-  else if (k <= 16) k_knn_query<16, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
-  else if (k <= 32) k_knn_query<32, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
-  else if (k <= 64) k_knn_query<64, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d);
+  if (k == 1) k_knn_query<1, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d, ties);
+  else if (k == 10) k_knn_query<10, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d, ties);
+  else if (k == 20) k_knn_query<20, true><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d, ties);
+  else if (k <= 16) k_knn_query<16, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d, ties);
+  else if (k <= 32) k_knn_query<32, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d, ties);
+  else if (k <= 64) k_knn_query<64, false><<<nb, 256, 0, s>>>(c, q, nq, k, out_idx, out_d, ties);
   else return false;
   return true;
 }
@@ -2571,6 +2615,10 @@ void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const
 }
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out) {
   k_cov_export<<<cdiv(n, 256), 256, 0, s>>>(cov6, layout, n, perm, out);
+}
+void launch_cov_remap(hipStream_t s, const double* old_cov6, const int* old_inv_perm, const int* new_perm, int n,
+                      double* cov6) {
+  k_cov_remap<<<cdiv(n, 256), 256, 0, s>>>(old_cov6, old_inv_perm, new_perm, n, cov6);
 }
 void launch_align_init(hipStream_t s, const AlignJob* job) { k_align_init<<<1, 128, 0, s>>>(job); }
 size_t search_lds_bytes(int upper_count) {

@@ -19,12 +19,23 @@ void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int
                         float4* phi);
 // returns false if k is unsupported (> 64)
 // redo: nullptr = every point, else only the 64-point groups flagged 1
-bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo);
+// ties (optional): sorted positions whose k-neighbourhood has an exact
+// distance tie at its boundary are appended to ties->list (nftree.hip
+// resolves them in nanoflann's order)
+struct TieList {
+  int* list;
+  int* count;
+};
+bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo,
+                        TieList ties = TieList{nullptr, nullptr});
 // task-based kNN-k covariances (knn_tasks.hip), k <= 32; groups it flags in
 // j.redo must then be recomputed with launch_covariances(..., j.redo)
 bool launch_knn_covariances(hipStream_t s, const KnnJob& j, int tgt_upper);
 int knn_task_cap_per_region(int n);
-bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq, int k, int* out_idx, float* out_d);
+// ties: query rows whose answer holds an exact distance tie (inside the k or
+// at its boundary) are listed for the nanoflann-order resolver
+bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq, int k, int* out_idx, float* out_d,
+                      TieList ties = TieList{nullptr, nullptr});
 void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6);
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);
 void launch_align_init(hipStream_t s, const AlignJob* job);
@@ -51,6 +62,22 @@ void launch_residual_image(hipStream_t s, const float4* pts, const int* perm, co
 void launch_transform(hipStream_t s, const float4* pts, int n, const int* perm, const float* T16, float* out,
                       size_t stride_floats);
 void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr, float* sqd);
+
+// nftree.hip: nanoflann's kd-tree on the device (tie order) and the tie resolvers
+NfSizes nf_sizes(int n);
+// sorted_pts: the cloud's Morton-sorted points (w = original index)
+void launch_nf_build(hipStream_t s, const NfBuild& b, const float4* sorted_pts);
+// status = {build error bits, node count}; nodes: 4 ints per node (c1, c2, feat, parent), f: divlow, divhigh
+void launch_nf_export(hipStream_t s, const NfTreeDev& t, const int* status, int cap, int* vind, int* nodes, float* f);
+// re-run the listed (tied) queries with nanoflann's search; status: the
+// tree build's error bits (nonzero: nothing resolved, *err |= 2); *err |= 1
+// on a failed search
+bool launch_nf_resolve_cov(hipStream_t s, const NfTreeDev& t, const CloudDev& c, const int* list, const int* count,
+                           int k, int method, double* cov6, const int* status, int* err);
+bool launch_nf_resolve_knn(hipStream_t s, const NfTreeDev& t, const float4* q, const int* list, const int* count, int k,
+                           int* out_idx, float* out_d, const int* status, int* err);
+void launch_cov_remap(hipStream_t s, const double* old_cov6, const int* old_inv_perm, const int* new_perm, int n,
+                      double* cov6);
 
 // preprocess.hip (odometry driver): see the kernels there for the reference
 // filters they restate.  Scratch sizes: *_tmp_bytes (hipcub temporaries).

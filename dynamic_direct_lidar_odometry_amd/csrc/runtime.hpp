@@ -129,10 +129,26 @@ struct DevBuf {
   }
 };
 
+// nanoflann's own kd-tree of a cloud (nftree.hip), built on first need: the
+// order in which the reference's search meets equidistant points.
+struct NfTreeData {
+  int n = 0, cap = 0;
+  DevBuf vpts, nodes, box, status;   // status: {the build's error bits, node count} (device ints)
+  NfTreeDev dev() const {
+    NfTreeDev t;
+    t.vpts = vpts.as<float4>();
+    t.nodes = nodes.as<NfNode>();
+    t.box = box.as<float4>();
+    t.n = n;
+    return t;
+  }
+};
+
 // Immutable device cloud + search hierarchy (shared between ctxs/sides).
 struct CloudData {
   int n = 0;
   DevBuf pts, keys, perm, inv_perm, box_lo, box_hi, quant, soa, dir;
+  std::shared_ptr<NfTreeData> nf;   // nanoflann's tree (tie order), built on first need
   int nlevels = 0;
   int lvl_off[kMaxLevels] = {0};
   int lvl_cnt[kMaxLevels] = {0};
@@ -242,6 +258,13 @@ struct gicp_ctx {
   bool speculate = true;    // queue a follow-on chunk before the first one's flag is seen
   bool comm_graphs = true;  // RCCL captured into the chunk graphs (else eager chunks)
   long captures = 0;        // chunk graphs captured (diagnostics: DDLO_GRAPH_DEBUG)
+  // exact distance ties in nanoflann's order (gicp_set_tie_order): the tree
+  // build scratch, the tied-query list and the resolvers' error word
+  bool tie_exact = true;
+  DevBuf nf_scratch, tie_buf, nf_err;
+  int* nf_err_host = nullptr;   // pinned copy of nf_err, read after the entry point's final wait
+  bool nf_err_pending = false;
+  long ties_resolved = 0;       // diagnostics
 };
 
 namespace ddlo {
@@ -349,6 +372,94 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   return GICP_OK;
 }
 
+// nanoflann's tree of a cloud (once per cloud, on the given stream)
+inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s) {
+  if (cd.nf) return GICP_OK;
+  auto t = std::make_shared<NfTreeData>();
+  const int n = cd.n;
+  t->n = n;
+  t->cap = 2 * n + 2;   // a tree of n points has at most 2n - 1 nodes
+  HIP_TRY(t->vpts.ensure(sizeof(float4) * (size_t)n));
+  HIP_TRY(t->nodes.ensure(sizeof(NfNode) * (size_t)t->cap));
+  HIP_TRY(t->box.ensure(2 * sizeof(float4) * (size_t)t->cap));
+  HIP_TRY(t->status.ensure(2 * sizeof(int)));
+  const NfSizes z = nf_sizes(n);
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t o_ctl = 0, o_tasks = o_ctl + al(sizeof(NfCtl)),
+               o_pend = o_tasks + al(sizeof(NfTask) * (size_t)(z.Lmax + 1) * z.max_task),
+               o_small = o_pend + al(sizeof(NfTask) * (size_t)(z.Lmax + 1) * z.max_pend),
+               o_cmap = o_small + al(sizeof(NfTask) * (size_t)z.max_small),
+               o_cA = o_cmap + al(sizeof(int) * 2 * (size_t)z.max_chunks),
+               o_cAE = o_cA + al(sizeof(int) * (size_t)z.max_chunks),
+               o_cE2 = o_cAE + al(sizeof(int) * (size_t)z.max_chunks),
+               o_tblL = o_cE2 + al(sizeof(int) * (size_t)z.max_chunks),
+               o_tblR = o_tblL + al(sizeof(float4) * (size_t)n), o_arrive = o_tblR + al(sizeof(float4) * (size_t)n),
+               total = o_arrive + al(sizeof(int) * (size_t)t->cap);
+  HIP_TRY(grow(c->nf_scratch, total, s));
+  char* u = c->nf_scratch.as<char>();
+  NfBuild b;
+  b.vpts = t->vpts.as<float4>();
+  b.nodes = t->nodes.as<NfNode>();
+  b.box = t->box.as<float4>();
+  b.cap = t->cap;
+  b.ctl = reinterpret_cast<NfCtl*>(u + o_ctl);
+  b.tasks = reinterpret_cast<NfTask*>(u + o_tasks);
+  b.pend = reinterpret_cast<NfTask*>(u + o_pend);
+  b.small = reinterpret_cast<NfTask*>(u + o_small);
+  b.chunk_task = reinterpret_cast<int*>(u + o_cmap);
+  b.cA = reinterpret_cast<int*>(u + o_cA);
+  b.cAE = reinterpret_cast<int*>(u + o_cAE);
+  b.cE2 = reinterpret_cast<int*>(u + o_cE2);
+  b.tblL = reinterpret_cast<float4*>(u + o_tblL);
+  b.tblR = reinterpret_cast<float4*>(u + o_tblR);
+  b.arrive = reinterpret_cast<int*>(u + o_arrive);
+  b.quant = cd.quant.as<float>();
+  b.n = n;
+  b.Lmax = z.Lmax;
+  b.max_task = z.max_task;
+  b.max_pend = z.max_pend;
+  b.max_small = z.max_small;
+  b.max_chunks = z.max_chunks;
+  HIP_TRY(hipMemsetAsync(b.arrive, 0, sizeof(int) * (size_t)t->cap, s));
+  launch_nf_build(s, b, cd.pts.as<float4>());
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(t->status.p, &b.ctl->err, sizeof(int), hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipMemcpyAsync(t->status.as<int>() + 1, &b.ctl->nnodes, sizeof(int), hipMemcpyDeviceToDevice, s));
+  cd.nf = t;
+  return GICP_OK;
+}
+
+// the tied-query list ([count][list n]) and the resolvers' error word, reset on the stream
+inline gicp_status tie_scratch(gicp_ctx* c, int n, hipStream_t s, TieList* tl) {
+  HIP_TRY(grow(c->tie_buf, sizeof(int) * ((size_t)n + 64), s));
+  HIP_TRY(c->nf_err.ensure(sizeof(int)));
+  if (!c->nf_err_host) HIP_TRY(hipHostMalloc((void**)&c->nf_err_host, sizeof(int), hipHostMallocDefault));
+  if (!c->nf_err_pending) {
+    HIP_TRY(hipMemsetAsync(c->nf_err.p, 0, sizeof(int), s));
+    c->nf_err_pending = true;
+  }
+  HIP_TRY(hipMemsetAsync(c->tie_buf.p, 0, sizeof(int), s));
+  tl->count = c->tie_buf.as<int>();
+  tl->list = c->tie_buf.as<int>() + 64;
+  return GICP_OK;
+}
+
+// after the entry point's final wait: a failed tie resolution is an error
+// (the answers would silently carry the Morton tie order instead of nanoflann's)
+inline gicp_status check_ties(gicp_ctx* c) {
+  if (!c->nf_err_pending) return GICP_OK;
+  c->nf_err_pending = false;
+  if (*(volatile int*)c->nf_err_host)
+    return fail(GICP_EHIP, "nanoflann tie order: the device kd-tree build or search failed (tree deeper than supported)");
+  return GICP_OK;
+}
+
+// enqueue the copy of the resolvers' error word that check_ties reads
+inline gicp_status publish_ties(gicp_ctx* c, hipStream_t s) {
+  if (c->nf_err_pending) HIP_TRY(hipMemcpyAsync(c->nf_err_host, c->nf_err.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  return GICP_OK;
+}
+
 inline gicp_status compute_cov(gicp_ctx* c, Side& side) {
   if (!side.cloud) return fail(GICP_ESTATE, "no cloud on this side");
   const int k = c->params.k_correspondences;
@@ -419,8 +530,23 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side) {
       std::fprintf(stderr, "[cov] n %d k %d redo groups %zu / %zu, points over cap %zu, mean cand %.1f max %zu\n", n, k,
                    nr, r.size(), over, (double)sum / n, mx);
     }
-  } else if (!launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), nullptr)) {
-    return fail(GICP_EINVAL, "unsupported k");
+  } else {
+    // exact ties: the points whose k-th neighbour distance is tied get their
+    // neighbourhood from nanoflann's own search (nftree.hip)
+    TieList tl{nullptr, nullptr};
+    if (c->tie_exact) {
+      gicp_status st = ensure_nftree(c, *side.cloud, c->stream);
+      if (!st) st = tie_scratch(c, side.cloud->n, c->stream, &tl);
+      if (st) return st;
+    }
+    if (!launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), nullptr, tl))
+      return fail(GICP_EINVAL, "unsupported k");
+    if (c->tie_exact) {
+      launch_nf_resolve_cov(c->stream, side.cloud->nf->dev(), cd, tl.list, tl.count, k, c->params.regularization,
+                            cv->cov6.as<double>(), side.cloud->nf->status.as<int>(), c->nf_err.as<int>());
+      gicp_status st = publish_ties(c, c->stream);
+      if (st) return st;
+    }
   }
   HIP_TRY(hipGetLastError());
   side.cov = cv;

@@ -123,9 +123,11 @@ gicp_status gicp_get_params(const struct gicp_ctx* ctx, gicp_params* out);
  * gicp_set_source(build_index=1) replaces NanoGICP::setInputSource
  *   (nano_gicp_impl.hpp:132-143: sets input_, builds the source kd-tree,
  *   clears source covariances);
- * gicp_set_source(build_index=0) replaces registerInputSource (:122-130).
- *   The device path always sorts the cloud spatially, so both forms produce
- *   the same device object; build_index=0 only skips the search hierarchy.
+ * gicp_set_source(build_index=0) replaces registerInputSource (:122-130):
+ *   no covariance reset — existing source covariances stay attached to the
+ *   same point indices (dropped only if the point count changes: the
+ *   reference then recomputes them at align, :186-189).  The device index is
+ *   built either way (it is cheap and the sorted cloud is the storage).
  * gicp_set_target replaces setInputTarget (:145-155). */
 gicp_status gicp_set_source(struct gicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes, int build_index);
 gicp_status gicp_set_target(struct gicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
@@ -192,9 +194,25 @@ gicp_status gicp_linearize(struct gicp_ctx* ctx, const double* pose16, double* H
                            int32_t* num_correspondences);
 /* Exact k-NN of query points against the TARGET index (nanoflann
  * nearestKSearch, nanoflann.hpp:145-156).  Indices are original target
- * indices, sorted ascending by (squared distance, index). */
+ * indices, ascending by squared distance; equal distances in the order
+ * nanoflann's own tree meets them (see gicp_set_tie_order). */
 gicp_status gicp_knn_target(struct gicp_ctx* ctx, const float* q, size_t nq, size_t stride_bytes, int k,
                             int32_t* idx, float* sq_dist);
+/* Exact distance ties (equidistant points at the k-th neighbour, or inside
+ * the k of gicp_knn_target): 1 (default) = nanoflann's answer, the point its
+ * depth-first walk of its own kd-tree meets first (KNNResultSet::addPoint
+ * keeps the earlier of equal distances, nanoflann_impl.hpp:205-237,1509);
+ * the device builds that tree (nftree.hip) and re-runs only the tied queries
+ * through it.  0 = the lower position in the device's Morton order (no tree
+ * is built).  Distances are identical either way.  Applies to covariances
+ * and gicp_knn_target. */
+gicp_status gicp_set_tie_order(struct gicp_ctx* ctx, int nanoflann_order);
+/* nanoflann's kd-tree of a side's cloud as the device built it (tests):
+ * vind[n]; per node (c1, c2, divfeat, parent) with divfeat -1 for a leaf
+ * whose vind range is [c1, c2), and (divlow, divhigh).  With all three
+ * outputs NULL only *nnodes is returned. */
+gicp_status gicp_debug_nftree(struct gicp_ctx* ctx, int side, int32_t* vind, int32_t* nodes4, float* div2, size_t cap,
+                              size_t* nnodes);
 /* The 74 reduced normal-equation moments of the last linearize (80 doubles,
  * layout in DESIGN.md "Normal-equation moments"); test/debug entry. */
 gicp_status gicp_get_moments(const struct gicp_ctx* ctx, double* out80);

@@ -84,6 +84,25 @@ class KdTree {
 
   int size() const { return n_; }
 
+  // tests: vind and the nodes in preorder (= this restatement's allocation
+  // order): (child1, child2, divfeat, -1) or (left, right, -1, -1) for a
+  // leaf, and (divlow, divhigh); returns the node count (-1: cap too small)
+  int export_tree(int* vind, int* nodes4, float* div2, int cap) const {
+    for (int i = 0; i < n_; ++i) vind[i] = vind_[i];
+    if ((int)nodes_.size() > cap) return -1;
+    for (size_t i = 0; i < nodes_.size(); ++i) {
+      const Node& nd = nodes_[i];
+      const bool leaf = nd.child1 < 0 && nd.child2 < 0;
+      nodes4[4 * i] = leaf ? nd.left : nd.child1;
+      nodes4[4 * i + 1] = leaf ? nd.right : nd.child2;
+      nodes4[4 * i + 2] = leaf ? -1 : nd.divfeat;
+      nodes4[4 * i + 3] = -1;
+      div2[2 * i] = leaf ? 0.f : nd.divlow;
+      div2[2 * i + 1] = leaf ? 0.f : nd.divhigh;
+    }
+    return (int)nodes_.size();
+  }
+
   // nearestKSearch: returns count found (== k when n >= k)
   int knn(const float* q, int k, int* idx, float* dist) const {
     // KNNResultSet::init (nanoflann_impl.hpp:180-187)
@@ -880,6 +899,9 @@ void* oref_tree_build(const float* xyz, int n) {
   return t;
 }
 void oref_tree_free(void* t) { delete static_cast<oref::KdTree*>(t); }
+int oref_tree_export(void* t, int* vind, int* nodes4, float* div2, int cap) {
+  return static_cast<oref::KdTree*>(t)->export_tree(vind, nodes4, div2, cap);
+}
 
 // k-NN of nq queries; outputs idx[nq*k], d[nq*k]; returns 0
 int oref_tree_knn(void* th, const float* q, int nq, int k, int* idx, float* d, int nthreads) {

@@ -84,6 +84,7 @@ def lib():
         L.oref_tree_build.argtypes = [C.c_void_p, C.c_int]
         L.oref_tree_free.argtypes = [C.c_void_p]
         L.oref_tree_knn.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        L.oref_tree_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.oref_covariances.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]
         L.oref_gicp_create.restype = C.c_void_p
         L.oref_gicp_create.argtypes = [C.POINTER(GicpParams), C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
@@ -119,6 +120,7 @@ def ref_lib():
         L.ref_tree_build.argtypes = [C.c_void_p, C.c_int]
         L.ref_tree_free.argtypes = [C.c_void_p]
         L.ref_tree_knn.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.ref_tree_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         _REF = L
     return _REF
 
@@ -151,6 +153,63 @@ def ref_knn(points, queries, k):
     L.ref_tree_knn(h, _fp(q), len(q), k, _fp(idx), _fp(d))
     L.ref_tree_free(h)
     return idx, d
+
+
+def _export(L, build, free, export, points):
+    pts = _xyz(points)
+    h = build(_fp(pts), len(pts))
+    cap = 2 * len(pts) + 2
+    vind = np.zeros(len(pts), np.int32)
+    nodes = np.zeros((cap, 4), np.int32)
+    div = np.zeros((cap, 2), np.float32)
+    nn = export(h, _fp(vind), _fp(nodes), _fp(div), cap)
+    free(h)
+    assert nn > 0, "tree export failed"
+    return vind, nodes[:nn], div[:nn]
+
+
+def tree(points):
+    """The oracle's nanoflann tree: vind, preorder nodes (c1, c2, divfeat, -1; divfeat -1 = leaf with vind
+    range [c1, c2)), (divlow, divhigh)."""
+    L = lib()
+    return _export(L, L.oref_tree_build, L.oref_tree_free, L.oref_tree_export, points)
+
+
+def ref_tree(points):
+    """The REFERENCE nanoflann's tree in the same layout (oracle/_ref), or None."""
+    L = ref_lib()
+    if L is None:
+        return None
+    return _export(L, L.ref_tree_build, L.ref_tree_free, L.ref_tree_export, points)
+
+
+def same_tree(a, b):
+    """Two exported trees (any node numbering) describe the same nanoflann tree: identical vind and, walked from
+    the roots, identical leaves, divfeat, divlow and divhigh.  Returns a mismatch description or None."""
+    va, na, da = a
+    vb, nb, db = b
+    if not np.array_equal(va, vb):
+        i = int(np.argmax(va != vb))
+        return f"vind differs first at {i}: {va[i]} vs {vb[i]}"
+    st = [(0, 0)]
+    seen = 0
+    while st:
+        x, y = st.pop()
+        seen += 1
+        if na[x, 2] != nb[y, 2]:
+            return f"node kind/divfeat differs ({x} vs {y}): {na[x, 2]} vs {nb[y, 2]}"
+        if na[x, 2] < 0:
+            if na[x, 0] != nb[y, 0] or na[x, 1] != nb[y, 1]:
+                return f"leaf range differs: {na[x, :2]} vs {nb[y, :2]}"
+            continue
+        if da[x, 0].view(np.int32) != db[y, 0].view(np.int32) or da[x, 1].view(np.int32) != db[y, 1].view(np.int32):
+            if not (da[x, 0] == db[y, 0] and da[x, 1] == db[y, 1]):   # +-0 are the same split
+                return f"divlow/divhigh differ at ({x}, {y}): {da[x]} vs {db[y]}"
+        st.append((na[x, 1], nb[y, 1]))
+        st.append((na[x, 0], nb[y, 0]))
+    if seen != len(na) or seen != len(nb):
+        return f"node counts differ: walked {seen}, sizes {len(na)} / {len(nb)}"
+    return None
 
 
 def covariances(points, k, reg="PLANE", threads=0):

@@ -14,6 +14,7 @@
  * oracle's kd-tree restatement and to generate tests/golden fixtures.
  */
 #include <cstddef>
+#include <functional>
 #include <vector>
 
 #include "nano_gicp/impl/nanoflann_impl.hpp"
@@ -49,5 +50,42 @@ int ref_tree_knn(void* h, const float* q, int nq, int k, int* idx, float* d) {
     t->tree.findNeighbors(rs, &q[3 * i], nanoflann::SearchParams());
   }
   return 0;
+}
+// the built tree (tests): vind, and the nodes in preorder (the order
+// divideTree allocates them): (child1, child2, divfeat, -1) with preorder
+// child indices, or (left, right, -1, -1) for a leaf; (divlow, divhigh).
+// Returns the node count (-1: cap too small).
+int ref_tree_export(void* h, int* vind, int* nodes4, float* div2, int cap) {
+  auto* t = static_cast<Handle*>(h);
+  for (size_t i = 0; i < t->tree.vind.size(); ++i) vind[i] = t->tree.vind[i];
+  int next = 0;
+  bool ok = true;
+  std::function<int(Tree::NodePtr)> walk = [&](Tree::NodePtr nd) -> int {
+    const int id = next++;
+    if (id >= cap) {
+      ok = false;
+      return id;
+    }
+    nodes4[4 * id + 3] = -1;
+    if (!nd->child1 && !nd->child2) {
+      nodes4[4 * id] = (int)nd->node_type.lr.left;
+      nodes4[4 * id + 1] = (int)nd->node_type.lr.right;
+      nodes4[4 * id + 2] = -1;
+      div2[2 * id] = div2[2 * id + 1] = 0.f;
+      return id;
+    }
+    nodes4[4 * id + 2] = nd->node_type.sub.divfeat;
+    div2[2 * id] = nd->node_type.sub.divlow;
+    div2[2 * id + 1] = nd->node_type.sub.divhigh;
+    const int c1 = walk(nd->child1);
+    const int c2 = walk(nd->child2);
+    if (ok) {
+      nodes4[4 * id] = c1;
+      nodes4[4 * id + 1] = c2;
+    }
+    return id;
+  };
+  walk(t->tree.root_node);
+  return ok ? next : -1;
 }
 }

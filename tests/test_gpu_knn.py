@@ -1,11 +1,12 @@
 """GPU parity of the exact nearest-neighbour search (HIP, through the C-ABI)
 against the reference nanoflann's golden vectors and the oracle.
 
-Bar: bit-exact indices and squared distances.  Exact distance ties (duplicate
-or equidistant points) are the one documented divergence: nanoflann keeps the
-first point its traversal meets, the GPU keeps the lowest Morton position; the
-returned squared distances stay bit-identical and each returned index is a
-point at exactly that distance (DESIGN.md "Tie rule")."""
+Bar: bit-exact indices and squared distances, exact distance ties
+(duplicate or equidistant points) included: nanoflann keeps the first point
+its traversal meets, and the device re-runs every tied query through
+nanoflann's own kd-tree, built on the device (nftree.hip, DESIGN.md "Tie
+order").  With gicp_set_tie_order(0) ties fall back to the lowest Morton
+position (same distances; checked tie-aware)."""
 import numpy as np
 import pytest
 
@@ -63,9 +64,22 @@ def test_knn_self_and_far_golden(knn_golden):
 
 @pytest.mark.parametrize("case,k", [("dup", 10), ("lat", 1), ("lat", 10)])
 def test_knn_ties_golden(knn_golden, case, k):
+    """The reference nanoflann's own answers on duplicate points and an integer lattice, bit for bit."""
     g = knn_golden
     pts, q = g[f"{case}_pts"], g[f"{case}_q"]
     c = _ctx_with_target(pts)
+    idx, sqd = c.knn_target(q, k)
+    np.testing.assert_array_equal(sqd, g[f"{case}_k{k}_sqd"])
+    np.testing.assert_array_equal(idx, g[f"{case}_k{k}_idx"])
+
+
+@pytest.mark.parametrize("case,k", [("dup", 10), ("lat", 10)])
+def test_knn_ties_morton_order_mode(knn_golden, case, k):
+    """gicp_set_tie_order(0): no tree; same distances, ties by Morton position."""
+    g = knn_golden
+    pts, q = g[f"{case}_pts"], g[f"{case}_q"]
+    c = _ctx_with_target(pts)
+    c.set_tie_order(False)
     idx, sqd = c.knn_target(q, k)
     _assert_tie_aware(pts, q, idx, sqd, g[f"{case}_k{k}_idx"], g[f"{case}_k{k}_sqd"])
 
