@@ -35,6 +35,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <queue>
 #include <vector>
@@ -122,209 +123,301 @@ Quatf quat_inverse(const Quatf& q) {  // Eigen: conjugate / squaredNorm
 }
 
 // ---- hulls over the keyframe positions (computeConvexHull / computeConcaveHull) ----
-// pcl::ConvexHull / ConcaveHull pick the dimension from the covariance of the
-// input (calculateInputDimension): planar (2) when the smallest eigenvalue is
-// ~0 or below 1e-3 of the largest, else 3.
-void sym_eig3(const double* A, double* lam, double* V) {  // Jacobi; V columns = eigenvectors
-  double a[9];
-  std::memcpy(a, A, sizeof(a));
-  for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
-  for (int sweep = 0; sweep < 60; ++sweep) {
-    const double off = a[1] * a[1] + a[2] * a[2] + a[5] * a[5];
-    if (off < 1e-300) break;
-    for (int p = 0; p < 2; ++p)
-      for (int q = p + 1; q < 3; ++q) {
-        const double apq = a[3 * p + q];
-        if (std::fabs(apq) < 1e-300) continue;
-        const double theta = (a[3 * q + q] - a[3 * p + p]) / (2.0 * apq);
-        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
-        const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
-        for (int k = 0; k < 3; ++k) {  // A <- J^T A J
-          const double akp = a[3 * k + p], akq = a[3 * k + q];
-          a[3 * k + p] = c * akp - s * akq;
-          a[3 * k + q] = s * akp + c * akq;
-        }
-        for (int k = 0; k < 3; ++k) {
-          const double apk = a[3 * p + k], aqk = a[3 * q + k];
-          a[3 * p + k] = c * apk - s * aqk;
-          a[3 * q + k] = s * apk + c * aqk;
-        }
-        for (int k = 0; k < 3; ++k) {
-          const double vkp = V[3 * k + p], vkq = V[3 * k + q];
-          V[3 * k + p] = c * vkp - s * vkq;
-          V[3 * k + q] = s * vkp + c * vkq;
-        }
-      }
-  }
-  for (int i = 0; i < 3; ++i) lam[i] = a[4 * i];
-}
+// OdomNode sets both hulls to dimension 3 (odom.cc:87-88), so PCL never
+// projects to a plane: pcl::ConvexHull runs qhull in 3-D ("qhull ", no
+// joggle; a flat keyframe set is a qhull precision error and an EMPTY hull),
+// pcl::ConcaveHull runs qhull's 3-D Delaunay ("qhull d QJ") and keeps the
+// alpha shape's boundary triangles.  Both are restated here on the host (a
+// few hundred keyframes at most), as the reference runs qhull on its host.
+using P3 = std::array<double, 3>;
 
-// returns the dimension; u, v: the in-plane orthonormal basis (2D case)
-int hull_frame(const float* xyz, int n, double* c, double* u, double* v) {
-  c[0] = c[1] = c[2] = 0.0;
-  for (int i = 0; i < n; ++i)
-    for (int a = 0; a < 3; ++a) c[a] += xyz[3 * i + a];
-  for (int a = 0; a < 3; ++a) c[a] /= n;
-  double C[9] = {0};
-  for (int i = 0; i < n; ++i) {
-    const double d[3] = {xyz[3 * i] - c[0], xyz[3 * i + 1] - c[1], xyz[3 * i + 2] - c[2]};
-    for (int r = 0; r < 3; ++r)
-      for (int q = 0; q < 3; ++q) C[3 * r + q] += d[r] * d[q];
-  }
-  for (int e = 0; e < 9; ++e) C[e] /= n;
-  double lam[3], V[9];
-  sym_eig3(C, lam, V);
-  int ord[3] = {0, 1, 2};
-  std::sort(ord, ord + 3, [&](int a, int b) { return lam[a] < lam[b]; });
-  for (int a = 0; a < 3; ++a) {
-    u[a] = V[3 * a + ord[2]];
-    v[a] = V[3 * a + ord[1]];
-  }
-  const double l0 = lam[ord[0]], l2 = lam[ord[2]];
-  return (std::fabs(l0) < DBL_EPSILON || std::fabs(l0 / l2) < 1.0e-3) ? 2 : 3;
-}
-
-double cross2(const double* o, const double* a, const double* b) {
-  return (a[0] - o[0]) * (b[1] - o[1]) - (a[1] - o[1]) * (b[0] - o[0]);
-}
-
-// vertex set of the convex hull (collinear / coplanar boundary points are not
-// vertices, as qhull reports them)
+// vertex set of the 3-D convex hull; empty when the points are coplanar or
+// fewer than 4 (qhull: "initial simplex is flat")
 std::vector<int> convex_hull(const float* xyz, int n) {
   std::vector<int> out;
-  if (n <= 0) return out;
-  if (n <= 2) {
-    for (int i = 0; i < n; ++i) out.push_back(i);
-    return out;
+  if (n < 4) return out;
+  struct F {
+    int a, b, c;
+    double n[3], d;
+    bool alive;
+  };
+  auto P = [&](int i) { return P3{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]}; };
+  auto make = [&](int a, int b, int cc) {
+    const P3 A = P(a), B = P(b), Cc = P(cc);
+    const double e1[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, e2[3] = {Cc[0] - A[0], Cc[1] - A[1], Cc[2] - A[2]};
+    F f{a, b, cc, {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]}, 0, true};
+    const double nn = std::sqrt(f.n[0] * f.n[0] + f.n[1] * f.n[1] + f.n[2] * f.n[2]);
+    if (nn > 0)
+      for (int k = 0; k < 3; ++k) f.n[k] /= nn;   // unit normal: the visibility test below is a distance
+    f.d = f.n[0] * A[0] + f.n[1] * A[1] + f.n[2] * A[2];
+    return f;
+  };
+  double scale = 0;
+  for (int i = 0; i < 3 * n; ++i) scale = std::max(scale, (double)std::fabs(xyz[i]));
+  scale = std::max(scale, 1e-30);
+  const double eps = 1e-12 * scale;   // a point this close to a facet's plane does not see it (qhull: round-off)
+  // initial tetrahedron: farthest-apart picks
+  int i0 = 0, i1 = -1, i2 = -1, i3 = -1;
+  double best = -1;
+  for (int i = 1; i < n; ++i) {
+    const P3 a = P(i0), b = P(i);
+    const double d = (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+    if (d > best) { best = d; i1 = i; }
   }
-  double c[3], u[3], v[3];
-  const int dim = hull_frame(xyz, n, c, u, v);
-  if (dim == 2) {
-    std::vector<std::array<double, 3>> p(n);  // (s, t, index)
-    for (int i = 0; i < n; ++i) {
-      const double d[3] = {xyz[3 * i] - c[0], xyz[3 * i + 1] - c[1], xyz[3 * i + 2] - c[2]};
-      p[i] = {d[0] * u[0] + d[1] * u[1] + d[2] * u[2], d[0] * v[0] + d[1] * v[1] + d[2] * v[2], (double)i};
-    }
-    std::sort(p.begin(), p.end());
-    std::vector<std::array<double, 3>> h(2 * n);
-    int k = 0;
-    for (int i = 0; i < n; ++i) {  // Andrew's monotone chain, strict turns
-      while (k >= 2 && cross2(h[k - 2].data(), h[k - 1].data(), p[i].data()) <= 0) --k;
-      h[k++] = p[i];
-    }
-    for (int i = n - 2, t = k + 1; i >= 0; --i) {
-      while (k >= t && cross2(h[k - 2].data(), h[k - 1].data(), p[i].data()) <= 0) --k;
-      h[k++] = p[i];
-    }
-    for (int i = 0; i < k - 1; ++i) out.push_back((int)h[i][2]);
-  } else {
-    // 3D: incremental hull; a point is a vertex of the final hull if it
-    // remains on a facet
-    struct F {
-      int a, b, c;
-      double n[3], d;
-      bool alive;
-    };
-    auto P = [&](int i) { return std::array<double, 3>{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]}; };
-    auto make = [&](int a, int b, int cc) {
-      const auto A = P(a), B = P(b), Cc = P(cc);
-      const double e1[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, e2[3] = {Cc[0] - A[0], Cc[1] - A[1], Cc[2] - A[2]};
-      F f{a, b, cc, {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]}, 0, true};
-      f.d = f.n[0] * A[0] + f.n[1] * A[1] + f.n[2] * A[2];
-      return f;
-    };
-    double scale = 0;
-    for (int i = 0; i < 3 * n; ++i) scale = std::max(scale, (double)std::fabs(xyz[i]));
-    const double eps = 1e-9 * std::max(1.0, scale * scale);
-    // initial tetrahedron: farthest-apart picks
-    int i0 = 0, i1 = -1, i2 = -1, i3 = -1;
-    double best = -1;
-    for (int i = 1; i < n; ++i) {
-      const auto a = P(i0), b = P(i);
-      const double d = (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
-      if (d > best) { best = d; i1 = i; }
-    }
-    best = -1;
-    for (int i = 0; i < n; ++i) {
-      if (i == i0 || i == i1) continue;
-      const F f = make(i0, i1, i);
-      const double a2 = f.n[0] * f.n[0] + f.n[1] * f.n[1] + f.n[2] * f.n[2];
-      if (a2 > best) { best = a2; i2 = i; }
-    }
-    best = -1;
-    const F base = make(i0, i1, i2);
-    for (int i = 0; i < n; ++i) {
-      if (i == i0 || i == i1 || i == i2) continue;
-      const auto p = P(i);
-      const double s = std::fabs(base.n[0] * p[0] + base.n[1] * p[1] + base.n[2] * p[2] - base.d);
-      if (s > best) { best = s; i3 = i; }
-    }
-    std::vector<F> fs;
-    auto add_oriented = [&](int a, int b, int cc, int inside) {
-      F f = make(a, b, cc);
-      const auto q = P(inside);
-      if (f.n[0] * q[0] + f.n[1] * q[1] + f.n[2] * q[2] - f.d > 0) f = make(a, cc, b);
-      fs.push_back(f);
-    };
-    add_oriented(i0, i1, i2, i3);
-    add_oriented(i0, i1, i3, i2);
-    add_oriented(i0, i2, i3, i1);
-    add_oriented(i1, i2, i3, i0);
-    for (int i = 0; i < n; ++i) {
-      if (i == i0 || i == i1 || i == i2 || i == i3) continue;
-      const auto p = P(i);
-      std::vector<std::pair<int, int>> edges;
-      bool any = false;
-      for (auto& f : fs) {
-        if (!f.alive) continue;
-        if (f.n[0] * p[0] + f.n[1] * p[1] + f.n[2] * p[2] - f.d > eps) {
-          f.alive = false;
-          any = true;
-          edges.push_back({f.a, f.b});
-          edges.push_back({f.b, f.c});
-          edges.push_back({f.c, f.a});
-        }
-      }
-      if (!any) continue;
-      // horizon: directed edges whose reverse was not removed
-      for (const auto& e : edges) {
-        bool twin = false;
-        for (const auto& g : edges)
-          if (g.first == e.second && g.second == e.first) { twin = true; break; }
-        if (!twin) fs.push_back(make(e.first, e.second, i));
+  best = -1;
+  for (int i = 0; i < n; ++i) {
+    if (i == i0 || i == i1) continue;
+    const P3 A = P(i0), B = P(i1), Cc = P(i);
+    const double e1[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, e2[3] = {Cc[0] - A[0], Cc[1] - A[1], Cc[2] - A[2]};
+    const double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2], cz = e1[0] * e2[1] - e1[1] * e2[0];
+    const double a2 = cx * cx + cy * cy + cz * cz;
+    if (a2 > best) { best = a2; i2 = i; }
+  }
+  if (i2 < 0 || !(best > 0)) return out;   // collinear
+  best = -1;
+  const F base = make(i0, i1, i2);
+  const double bn = 1.0;
+  for (int i = 0; i < n; ++i) {
+    if (i == i0 || i == i1 || i == i2) continue;
+    const P3 p = P(i);
+    const double sd = std::fabs(base.n[0] * p[0] + base.n[1] * p[1] + base.n[2] * p[2] - base.d);
+    if (sd > best) { best = sd; i3 = i; }
+  }
+  // qhull's flat-simplex test is at round-off level: coplanar within ~1e-13 of the extent
+  if (!(bn > 0) || i3 < 0 || best / bn <= 1e-13 * scale) return out;
+  std::vector<F> fs;
+  auto add_oriented = [&](int a, int b, int cc, int inside) {
+    F f = make(a, b, cc);
+    const P3 q = P(inside);
+    if (f.n[0] * q[0] + f.n[1] * q[1] + f.n[2] * q[2] - f.d > 0) f = make(a, cc, b);
+    fs.push_back(f);
+  };
+  add_oriented(i0, i1, i2, i3);
+  add_oriented(i0, i1, i3, i2);
+  add_oriented(i0, i2, i3, i1);
+  add_oriented(i1, i2, i3, i0);
+  for (int i = 0; i < n; ++i) {
+    if (i == i0 || i == i1 || i == i2 || i == i3) continue;
+    const P3 p = P(i);
+    std::vector<std::pair<int, int>> edges;
+    bool any = false;
+    for (auto& f : fs) {
+      if (!f.alive) continue;
+      if (f.n[0] * p[0] + f.n[1] * p[1] + f.n[2] * p[2] - f.d > eps) {
+        f.alive = false;
+        any = true;
+        edges.push_back({f.a, f.b});
+        edges.push_back({f.b, f.c});
+        edges.push_back({f.c, f.a});
       }
     }
-    std::vector<char> on(n, 0);
-    for (const auto& f : fs)
-      if (f.alive) on[f.a] = on[f.b] = on[f.c] = 1;
-    for (int i = 0; i < n; ++i)
-      if (on[i]) out.push_back(i);
+    if (!any) continue;
+    // horizon: directed edges whose reverse was not removed
+    for (const auto& e : edges) {
+      bool twin = false;
+      for (const auto& g : edges)
+        if (g.first == e.second && g.second == e.first) { twin = true; break; }
+      if (!twin) fs.push_back(make(e.first, e.second, i));
+    }
   }
-  std::sort(out.begin(), out.end());
-  out.erase(std::unique(out.begin(), out.end()), out.end());
+  std::vector<char> on(n, 0);
+  for (const auto& f : fs)
+    if (f.alive) on[f.a] = on[f.b] = on[f.c] = 1;
+  for (int i = 0; i < n; ++i)
+    if (on[i]) out.push_back(i);
   return out;
 }
 
-// Vertex set of the concave hull (pcl::ConcaveHull, alpha).  Its planar
-// branch keeps every edge of a Delaunay triangle whose circumradius is
-// <= alpha and every other Delaunay edge of half-length <= alpha; an edge of
-// a triangle is never longer than the circumcircle's diameter, so the kept
-// edges are exactly the Delaunay edges of length <= 2 alpha, and a point is
-// a vertex iff its shortest Delaunay edge — the one to its nearest neighbour
-// — is that short.  (Parity unpinned: PCL is not in this image; the 3D
-// branch, for non-planar keyframe sets, is restated with the same criterion.)
+// ---- 3-D Delaunay (Bowyer-Watson, long double predicates) ----
+using LD = long double;
+struct Tet {
+  int v[4];
+  bool alive;
+};
+
+LD det3(LD a, LD b, LD c, LD d, LD e, LD f, LD g, LD h, LD i) { return a * (e * i - f * h) - b * (d * i - f * g) + c * (d * h - e * g); }
+
+// det[b - a; c - a; d - a]
+LD orient(const std::vector<std::array<LD, 3>>& p, int a, int b, int c, int d) {
+  const auto& A = p[a];
+  const auto& B = p[b];
+  const auto& C = p[c];
+  const auto& D = p[d];
+  return det3(B[0] - A[0], B[1] - A[1], B[2] - A[2], C[0] - A[0], C[1] - A[1], C[2] - A[2], D[0] - A[0], D[1] - A[1],
+              D[2] - A[2]);
+}
+
+// 4x4 lifted determinant; for a positively oriented tetrahedron its sign
+// tells whether e lies inside the circumsphere (kInside below)
+LD insphere(const std::vector<std::array<LD, 3>>& p, const int* t, int e) {
+  LD m[4][4];
+  for (int r = 0; r < 4; ++r) {
+    const auto& A = p[t[r]];
+    const LD x = A[0] - p[e][0], y = A[1] - p[e][1], z = A[2] - p[e][2];
+    m[r][0] = x;
+    m[r][1] = y;
+    m[r][2] = z;
+    m[r][3] = x * x + y * y + z * z;
+  }
+  LD d = 0;
+  for (int c = 0; c < 4; ++c) {
+    LD sub[9];
+    int k = 0;
+    for (int r = 1; r < 4; ++r)
+      for (int cc = 0; cc < 4; ++cc)
+        if (cc != c) sub[k++] = m[r][cc];
+    const LD cof = det3(sub[0], sub[1], sub[2], sub[3], sub[4], sub[5], sub[6], sub[7], sub[8]);
+    d += ((c & 1) ? -1 : 1) * m[0][c] * cof;
+  }
+  return d;
+}
+
+int inside_sign() {   // the sign insphere() has at the centre of a positive unit tetrahedron
+  static const int s = [] {
+    std::vector<std::array<LD, 3>> p = {{0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0.25L, 0.25L, 0.25L}};
+    const int t[4] = {0, 1, 2, 3};
+    return insphere(p, t, 4) > 0 ? 1 : -1;
+  }();
+  return s;
+}
+
+// Delaunay tetrahedra of the points (indices into xyz), the enclosing
+// tetrahedron's removed.  Input coordinates are demeaned (PCL demeans before
+// qhull) and joggled by a deterministic relative 1e-11 (qhull's QJ joggles
+// randomly) so that cospherical / coplanar input has a well-defined answer.
+std::vector<Tet> delaunay3(const float* xyz, int n, std::vector<std::array<LD, 3>>& p) {
+  std::array<LD, 3> c{0, 0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a) c[a] += xyz[3 * i + a];
+  for (int a = 0; a < 3; ++a) c[a] /= n;
+  LD ext = 0;
+  p.assign(n + 4, {0, 0, 0});
+  uint64_t rng = 0x9E3779B97F4A7C15ull;
+  auto next = [&]() {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return (LD)((rng >> 11) * (1.0 / 9007199254740992.0)) - 0.5L;
+  };
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a) {
+      p[i][a] = (LD)xyz[3 * i + a] - c[a];
+      ext = std::max(ext, std::fabs(p[i][a]));
+    }
+  ext = std::max(ext, (LD)1e-12);
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a) p[i][a] += next() * 1e-11L * ext;
+  const LD M = 1e4L * ext;
+  p[n] = {-M, -M, -M};
+  p[n + 1] = {3 * M, -M, -M};
+  p[n + 2] = {-M, 3 * M, -M};
+  p[n + 3] = {-M, -M, 3 * M};
+  std::vector<Tet> T;
+  T.push_back({{n, n + 1, n + 2, n + 3}, true});
+  if (orient(p, n, n + 1, n + 2, n + 3) < 0) std::swap(T[0].v[2], T[0].v[3]);
+  const int ins = inside_sign();
+  for (int i = 0; i < n; ++i) {
+    std::vector<int> bad;
+    for (int t = 0; t < (int)T.size(); ++t)
+      if (T[t].alive && insphere(p, T[t].v, i) * ins > 0) bad.push_back(t);
+    // cavity boundary: faces of exactly one bad tetrahedron
+    std::map<std::array<int, 3>, std::pair<int, std::array<int, 3>>> faces;
+    for (int t : bad) {
+      T[t].alive = false;
+      const int* v = T[t].v;
+      const int fidx[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
+      for (const auto& f : fidx) {
+        std::array<int, 3> o{v[f[0]], v[f[1]], v[f[2]]};
+        std::array<int, 3> k = o;
+        std::sort(k.begin(), k.end());
+        auto it = faces.find(k);
+        if (it == faces.end()) faces[k] = {1, o};
+        else it->second.first += 1;
+      }
+    }
+    for (const auto& kv : faces) {
+      if (kv.second.first != 1) continue;
+      const auto& o = kv.second.second;
+      Tet nt{{o[0], o[1], o[2], i}, true};
+      const LD ov = orient(p, nt.v[0], nt.v[1], nt.v[2], nt.v[3]);
+      if (ov == 0) continue;   // degenerate after joggle: drop (never seen)
+      if (ov < 0) std::swap(nt.v[0], nt.v[1]);
+      T.push_back(nt);
+    }
+  }
+  std::vector<Tet> out;
+  for (const auto& t : T)
+    if (t.alive && t.v[0] < n && t.v[1] < n && t.v[2] < n && t.v[3] < n) out.push_back(t);
+  return out;
+}
+
+// circumradius of a tetrahedron (qh_pointdist(vertex, facet->center))
+LD tet_radius(const std::vector<std::array<LD, 3>>& p, const Tet& t) {
+  const auto& A = p[t.v[0]];
+  LD r[3][3], rhs[3];
+  for (int k = 0; k < 3; ++k) {
+    const auto& B = p[t.v[k + 1]];
+    for (int a = 0; a < 3; ++a) r[k][a] = B[a] - A[a];
+    rhs[k] = 0.5L * (r[k][0] * r[k][0] + r[k][1] * r[k][1] + r[k][2] * r[k][2]);
+  }
+  const LD D = det3(r[0][0], r[0][1], r[0][2], r[1][0], r[1][1], r[1][2], r[2][0], r[2][1], r[2][2]);
+  if (D == 0) return INFINITY;
+  const LD x = det3(rhs[0], r[0][1], r[0][2], rhs[1], r[1][1], r[1][2], rhs[2], r[2][1], r[2][2]) / D;
+  const LD y = det3(r[0][0], rhs[0], r[0][2], r[1][0], rhs[1], r[1][2], r[2][0], rhs[2], r[2][2]) / D;
+  const LD z = det3(r[0][0], r[0][1], rhs[0], r[1][0], r[1][1], rhs[1], r[2][0], r[2][1], rhs[2]) / D;
+  return std::sqrt(x * x + y * y + z * z);
+}
+
+// pcl::getCircumcircleRadius (common/impl/common.hpp) of a ridge, whose
+// vertices PCL reads as floats of qhull's (demeaned) coordinates: float
+// Vector4f norms (Eigen's SSE redux: (x^2 + z^2) + y^2), Heron's formula in double
+double tri_radius(const std::vector<std::array<LD, 3>>& p, int a, int b, int c) {
+  auto nrm = [&](int i, int j) {
+    const float dx = (float)p[j][0] - (float)p[i][0], dy = (float)p[j][1] - (float)p[i][1],
+                dz = (float)p[j][2] - (float)p[i][2];
+    return (double)std::sqrt((dx * dx + dz * dz) + dy * dy);
+  };
+  const double p2p1 = nrm(a, b), p3p2 = nrm(b, c), p1p3 = nrm(c, a);
+  const double s = (p2p1 + p3p2 + p1p3) / 2.0;
+  const double area = std::sqrt(s * (s - p2p1) * (s - p3p2) * (s - p1p3));
+  return (p2p1 * p3p2 * p1p3) / (4.0 * area);
+}
+
+// Vertex set of pcl::ConcaveHull's 3-D alpha shape (PCL 1.10
+// concave_hull.hpp performReconstruction, dim 3): a tetrahedron is "good"
+// iff its circumradius <= alpha; a Delaunay triangle is output iff it has a
+// side that is not a good tetrahedron (the outside, or a bad one) and its
+// circumradius <= alpha (a good tetrahedron's triangles always are);
+// setKeepInformation maps the vertices back to input indices.
 std::vector<int> concave_hull(const float* xyz, int n, double alpha) {
   std::vector<int> out;
-  for (int i = 0; i < n; ++i) {
-    double nn = INFINITY;
-    for (int j = 0; j < n; ++j) {
-      if (j == i) continue;
-      const double dx = (double)xyz[3 * i] - xyz[3 * j], dy = (double)xyz[3 * i + 1] - xyz[3 * j + 1],
-                   dz = (double)xyz[3 * i + 2] - xyz[3 * j + 2];
-      nn = std::min(nn, std::sqrt(dx * dx + dy * dy + dz * dz));
+  if (n < 4) return out;
+  std::vector<std::array<LD, 3>> p;
+  const std::vector<Tet> T = delaunay3(xyz, n, p);
+  std::vector<char> good(T.size());
+  std::map<std::array<int, 3>, std::array<int, 2>> adj;   // triangle -> its tetrahedra (-1 = outside)
+  for (size_t t = 0; t < T.size(); ++t) {
+    good[t] = tet_radius(p, T[t]) <= (LD)alpha;
+    const int* v = T[t].v;
+    const int fidx[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
+    for (const auto& f : fidx) {
+      std::array<int, 3> k{v[f[0]], v[f[1]], v[f[2]]};
+      std::sort(k.begin(), k.end());
+      auto it = adj.find(k);
+      if (it == adj.end()) adj[k] = {(int)t, -1};
+      else it->second[1] = (int)t;
     }
-    if (nn / 2 <= alpha) out.push_back(i);
   }
+  std::vector<char> on(n, 0);
+  for (const auto& kv : adj) {
+    const int a = kv.second[0], b = kv.second[1];
+    const bool ga = good[a], gb = b >= 0 && good[b];
+    if (ga && gb) continue;   // inside the good union
+    const auto& f = kv.first;
+    if (ga || gb || tri_radius(p, f[0], f[1], f[2]) <= alpha) on[f[0]] = on[f[1]] = on[f[2]] = 1;
+  }
+  for (int i = 0; i < n; ++i)
+    if (on[i]) out.push_back(i);
   return out;
 }
 
@@ -371,6 +464,7 @@ struct ddlo_odom {
   double t_phase[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   long frames = 0;
   // state
+  bool initialized = false;   // ddlo_initialized_
   bool have_target = false;
   float T[16], T_s2s[16], T_s2s_prev[16];
   float pose[3] = {0.f, 0.f, 0.f};
@@ -462,14 +556,17 @@ gicp_status make_keyframe(ddlo_odom* o, const std::shared_ptr<CloudData>& scan) 
   int m = n;
   gicp_status st = preprocess(o, n, false, 0.0, o->p.vf_submap_use != 0, o->p.vf_submap_res, &m);
   if (st) return st;
-  if (m < o->p.s2s.k_correspondences) return fail(GICP_ETOOFEW, "keyframe has fewer points than k_correspondences");
+  if (m < 1) return fail(GICP_ETOOFEW, "keyframe without points");
   kf->n = m;
   HIP_TRY(kf->pts.ensure(sizeof(float4) * (size_t)m));
   HIP_TRY(hipMemcpyAsync(kf->pts.p, o->a.p, sizeof(float4) * (size_t)m, hipMemcpyDeviceToDevice, o->s));
   Side side;
   st = cloud_from(o, o->s2s, kf->pts.as<float4>(), m, &side.cloud, true);
   if (st) return st;
-  st = compute_cov(o->s2s, side);   // s2s->params: the S2S k (gicp_s2s_.calculateSourceCovariances)
+  // s2s->params: the S2S k (gicp_s2s_.calculateSourceCovariances); a
+  // keyframe smaller than k uses all of its points (the reference reads
+  // uninitialised neighbour slots there)
+  st = compute_cov(o->s2s, side, std::min(o->p.s2s.k_correspondences, m));
   if (st) return st;
   HIP_TRY(kf->cov.ensure(sizeof(double) * 6 * (size_t)m));
   launch_gather_cov6(o->s, side.cov->cov6.as<double>(), side.cloud->perm.as<int>(), m, kf->cov.as<double>());
@@ -574,6 +671,7 @@ gicp_status ddlo_odom_default_params(ddlo_odom_params* p) {
   p->vf_scan_res = 0.1;
   p->vf_submap_use = 1;
   p->vf_submap_res = 0.1;
+  p->skip_first_scan = 1;
   return GICP_OK;
 }
 
@@ -647,6 +745,15 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
   if ((int64_t)n < o->p.min_num_points) {
     res->status = DDLO_ODOM_SKIPPED;
     return GICP_OK;
+  }
+  // DLO initialisation consumes the first valid scan (odom.cc:641-646;
+  // gravity alignment is out of scope, so it only sets ddlo_initialized_)
+  if (!o->initialized) {
+    o->initialized = true;
+    if (o->p.skip_first_scan) {
+      res->status = DDLO_ODOM_INIT;
+      return GICP_OK;
+    }
   }
   using clk = std::chrono::steady_clock;
   auto t0 = clk::now(), tl = t0;
@@ -866,18 +973,18 @@ gicp_status ddlo_preprocess(int device, const float* xyz, size_t n, size_t strid
   return GICP_OK;
 }
 
-gicp_status ddlo_convex_hull(const float* xyz, int n, int32_t* idx, int* nidx) {
-  if ((!xyz && n) || !idx || !nidx || n < 0) return fail(GICP_EINVAL, "invalid argument");
+gicp_status ddlo_convex_hull(const float* xyz, int n, int32_t* idx, int cap, int* nidx) {
+  if ((!xyz && n) || (!idx && cap > 0) || !nidx || n < 0 || cap < 0) return fail(GICP_EINVAL, "invalid argument");
   const std::vector<int> h = convex_hull(xyz, n);
-  for (size_t i = 0; i < h.size(); ++i) idx[i] = h[i];
+  for (size_t i = 0; i < h.size() && (int)i < cap; ++i) idx[i] = h[i];
   *nidx = (int)h.size();
   return GICP_OK;
 }
 
-gicp_status ddlo_concave_hull(const float* xyz, int n, double alpha, int32_t* idx, int* nidx) {
-  if ((!xyz && n) || !idx || !nidx || n < 0) return fail(GICP_EINVAL, "invalid argument");
+gicp_status ddlo_concave_hull(const float* xyz, int n, double alpha, int32_t* idx, int cap, int* nidx) {
+  if ((!xyz && n) || (!idx && cap > 0) || !nidx || n < 0 || cap < 0) return fail(GICP_EINVAL, "invalid argument");
   const std::vector<int> h = concave_hull(xyz, n, alpha);
-  for (size_t i = 0; i < h.size(); ++i) idx[i] = h[i];
+  for (size_t i = 0; i < h.size() && (int)i < cap; ++i) idx[i] = h[i];
   *nidx = (int)h.size();
   return GICP_OK;
 }

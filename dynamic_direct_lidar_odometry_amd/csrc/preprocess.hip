@@ -147,9 +147,9 @@ __global__ __launch_bounds__(256) void k_voxel_keys(const float4* __restrict__ i
 // AccumulatorXYZ).
 __global__ __launch_bounds__(256) void k_voxel_centroids(const float4* __restrict__ in, const int* __restrict__ order,
                                                          const int* __restrict__ offsets, const int* __restrict__ counts,
-                                                         const int* __restrict__ nruns, float4* __restrict__ out) {
+                                                         int nruns, float4* __restrict__ out) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= *nruns) return;
+  if (r >= nruns) return;
   const int o = offsets[r], c = counts[r];
   float sx = 0.f, sy = 0.f, sz = 0.f;
   for (int k = 0; k < c; ++k) {
@@ -281,8 +281,7 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   // and form the last run; a real voxel index never reaches UINT_MAX here)
   int nruns = h[8];
   if (h[9] < n) nruns -= 1;
-  (void)hipMemcpyAsync(small + 8, &nruns, sizeof(int), hipMemcpyHostToDevice, s);
-  k_voxel_centroids<<<cdiv_l(std::max(nruns, 1), 256), 256, 0, s>>>(in, order, offsets, counts, small + 8, out);
+  k_voxel_centroids<<<cdiv_l(std::max(nruns, 1), 256), 256, 0, s>>>(in, order, offsets, counts, nruns, out);
   *count_host = nruns;
   return 0;
 }

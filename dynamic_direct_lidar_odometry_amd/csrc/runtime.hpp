@@ -460,9 +460,10 @@ inline gicp_status publish_ties(gicp_ctx* c, hipStream_t s) {
   return GICP_OK;
 }
 
-inline gicp_status compute_cov(gicp_ctx* c, Side& side) {
+// k_use > 0 overrides the ctx's k (a keyframe smaller than k, odom.hip)
+inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   if (!side.cloud) return fail(GICP_ESTATE, "no cloud on this side");
-  const int k = c->params.k_correspondences;
+  const int k = k_use > 0 ? k_use : c->params.k_correspondences;
   if (k <= 0 || k > 64) return fail(GICP_EINVAL, "k_correspondences must be in [1, 64]");
   if (side.cloud->n < k) return fail(GICP_ETOOFEW, "cloud has fewer points than k_correspondences");
   auto cv = std::make_shared<CovData>();

@@ -15,9 +15,9 @@ import numpy as np
 from . import GicpError, GicpParams, GicpResult, _ptr, load
 
 __all__ = ["OdomParams", "OdomResult", "Odometry", "default_odom_params", "preprocess", "convex_hull",
-           "concave_hull", "TRACKED", "FIRST", "SKIPPED"]
+           "concave_hull", "TRACKED", "FIRST", "SKIPPED", "INIT"]
 
-TRACKED, FIRST, SKIPPED = 0, 1, 2
+TRACKED, FIRST, SKIPPED, INIT = 0, 1, 2, 3
 
 
 class OdomParams(C.Structure):
@@ -37,6 +37,7 @@ class OdomParams(C.Structure):
         ("vf_scan_res", C.c_double),
         ("vf_submap_use", C.c_int32),
         ("vf_submap_res", C.c_double),
+        ("skip_first_scan", C.c_int32),
     ]
 
 
@@ -79,8 +80,8 @@ def _lib():
             "ddlo_odom_submap": (I, [P, P, S, C.POINTER(S)]),
             "ddlo_odom_ctx": (I, [P, I, C.POINTER(P)]),
             "ddlo_preprocess": (I, [I, P, S, S, D, D, P, S, C.POINTER(S)]),
-            "ddlo_convex_hull": (I, [P, I, P, C.POINTER(I)]),
-            "ddlo_concave_hull": (I, [P, I, D, P, C.POINTER(I)]),
+            "ddlo_convex_hull": (I, [P, I, P, I, C.POINTER(I)]),
+            "ddlo_concave_hull": (I, [P, I, D, P, I, C.POINTER(I)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -161,7 +162,7 @@ def convex_hull(points) -> np.ndarray:
     a = _xyz(points)
     idx = np.zeros(max(a.shape[0], 1), np.int32)
     n = C.c_int()
-    _check(_lib().ddlo_convex_hull(_ptr(a), a.shape[0], _ptr(idx), C.byref(n)))
+    _check(_lib().ddlo_convex_hull(_ptr(a), a.shape[0], _ptr(idx), idx.shape[0], C.byref(n)))
     return idx[:n.value]
 
 
@@ -169,5 +170,5 @@ def concave_hull(points, alpha: float) -> np.ndarray:
     a = _xyz(points)
     idx = np.zeros(max(a.shape[0], 1), np.int32)
     n = C.c_int()
-    _check(_lib().ddlo_concave_hull(_ptr(a), a.shape[0], float(alpha), _ptr(idx), C.byref(n)))
+    _check(_lib().ddlo_concave_hull(_ptr(a), a.shape[0], float(alpha), _ptr(idx), idx.shape[0], C.byref(n)))
     return idx[:n.value]

@@ -42,12 +42,16 @@ typedef struct ddlo_odom_params {
   double vf_scan_res;              /* .../res (0.1 m) */
   int32_t vf_submap_use;           /* preprocessing/voxelFilter/submap/use (1): applied to keyframes */
   double vf_submap_res;            /* .../res (0.1 m) */
+  int32_t skip_first_scan;         /* 1 (reference): the first scan with >= min_num_points points only
+                                      initialises (initializeDDLO, odom.cc:641-646), so keyframe 0 is
+                                      the second one; 0: the first scan becomes the target at once */
 } ddlo_odom_params;
 
 typedef enum ddlo_odom_status {
   DDLO_ODOM_TRACKED = 0,   /* S2S + S2M ran, the pose was updated               */
   DDLO_ODOM_FIRST = 1,     /* first scan: became the S2S target and keyframe 0 */
-  DDLO_ODOM_SKIPPED = 2    /* fewer than min_num_points points (reference: return) */
+  DDLO_ODOM_SKIPPED = 2,   /* fewer than min_num_points points (reference: return) */
+  DDLO_ODOM_INIT = 3       /* consumed by the initialisation (initializeDDLO, odom.cc:641-646) */
 } ddlo_odom_status;
 
 typedef struct ddlo_odom_result {
@@ -71,7 +75,11 @@ gicp_status ddlo_odom_default_params(ddlo_odom_params* out);
 gicp_status ddlo_odom_create(int device, const ddlo_odom_params* p, struct ddlo_odom** out);
 gicp_status ddlo_odom_destroy(struct ddlo_odom* o);
 /* OdomNode::icpCB for one scan (odom.cc:614-729, registration part).  xyz:
- * float x, y, z of point 0, consecutive points stride_bytes apart; copied. */
+ * float x, y, z of point 0, consecutive points stride_bytes apart; copied.
+ * A keyframe whose submap-voxel-filtered cloud has fewer points than the S2S
+ * k gets covariances from all of its points (the reference reads
+ * uninitialised neighbour slots there, nanoflann.hpp:149-155).  An error
+ * return leaves the driver unusable: destroy it. */
 gicp_status ddlo_odom_process(struct ddlo_odom* o, const float* xyz, size_t n, size_t stride_bytes,
                               ddlo_odom_result* res);
 /* Keyframe k: world pose (x, y, z, qx, qy, qz, qw as the reference's pose_ /
@@ -90,11 +98,16 @@ gicp_status ddlo_preprocess(int device, const float* xyz, size_t n, size_t strid
                             float* out, size_t cap, size_t* nout);
 
 /* Hull keyframe selection (OdomNode::computeConvexHull / computeConcaveHull,
- * odom.cc:1003-1065, pcl::ConvexHull / pcl::ConcaveHull over the keyframe
- * positions): indices of the input points on the hull, ascending.  Exposed
- * for the tests. */
-gicp_status ddlo_convex_hull(const float* xyz, int n, int32_t* idx, int* nidx);
-gicp_status ddlo_concave_hull(const float* xyz, int n, double alpha, int32_t* idx, int* nidx);
+ * odom.cc:1003-1065, pcl::ConvexHull / pcl::ConcaveHull with setDimension(3),
+ * odom.cc:87-88, over the keyframe positions): indices of the input points on
+ * the hull, ascending.  Convex: qhull's 3-D vertex set, empty for fewer than
+ * 4 or coplanar points (qhull's flat-simplex error).  Concave: the vertices
+ * of the 3-D alpha shape's boundary triangles (Delaunay triangles of
+ * circumradius <= alpha not enclosed by two tetrahedra of circumradius <=
+ * alpha).  idx receives at most cap indices; *nidx = the hull's size (it may
+ * exceed cap).  Exposed for the tests. */
+gicp_status ddlo_convex_hull(const float* xyz, int n, int32_t* idx, int cap, int* nidx);
+gicp_status ddlo_concave_hull(const float* xyz, int n, double alpha, int32_t* idx, int cap, int* nidx);
 
 #ifdef __cplusplus
 }

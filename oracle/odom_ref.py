@@ -9,15 +9,20 @@ wraps) for the convex keyframe hull.  Only tests/ import it.
 
 Parity status: the GICP, filters and keyframe/submap logic follow the
 reference; PCL itself is absent from the image, so the hull steps are
-"parity unpinned" (convex hull checked against qhull through scipy; the
-concave hull is the edge criterion derived in odom.hip).
+"parity unpinned".  Both use qhull through scipy, the library pcl::ConvexHull
+and pcl::ConcaveHull wrap, with the dimension OdomNode sets (3, odom.cc:87-88)
+and PCL 1.10's options: the convex hull is qhull's 3-D vertex set (a flat set
+is qhull's "initial simplex is flat" error, i.e. an empty hull); the concave
+hull is the alpha shape PCL extracts from qhull's "d QJ" 3-D Delaunay
+(concave_hull.hpp performReconstruction, dim 3).
 """
 from __future__ import annotations
 
 import math
 
 import numpy as np
-from scipy.spatial import ConvexHull
+from scipy.spatial import ConvexHull, Delaunay
+from scipy.spatial import QhullError
 
 from . import oracle as O
 
@@ -88,36 +93,68 @@ def quat_inverse(q):
     return [F(-x / n2), F(-y / n2), F(-z / n2), F(w / n2)]
 
 
-def hull_dim_and_plane(P):
-    """pcl calculateInputDimension: planar if the smallest covariance eigenvalue is ~0 or < 1e-3 of the largest."""
-    c = P.astype(np.float64).mean(axis=0)
-    D = P.astype(np.float64) - c
-    Cm = D.T @ D / len(P)
-    lam, V = np.linalg.eigh(Cm)
-    planar = abs(lam[0]) < np.finfo(np.float64).eps or abs(lam[0] / lam[2]) < 1e-3
-    return (2 if planar else 3), D @ V[:, [2, 1]], D
-
-
 def convex_hull(P):
-    """computeConvexHull (odom.cc:1003-1031): qhull vertex set, in the keyframes' plane when planar."""
-    n = len(P)
-    if n <= 2:
-        return list(range(n))
-    dim, P2, D = hull_dim_and_plane(P)
-    h = ConvexHull(P2 if dim == 2 else D)
+    """computeConvexHull (odom.cc:993-1028) with setDimension(3): qhull's 3-D vertex set, [] when qhull fails
+    (fewer than 4 points or a flat set)."""
+    if len(P) < 4:
+        return []
+    try:
+        h = ConvexHull(np.asarray(P, np.float64))
+    except QhullError:
+        return []
     return sorted(int(i) for i in h.vertices)
 
 
+def _tri_radius(a, b, c):
+    """pcl::getCircumcircleRadius: float Vector4f norms ((x^2 + z^2) + y^2, Eigen's SSE redux), Heron in double."""
+    def nrm(u, v):
+        d = (v - u).astype(F)
+        return float(np.sqrt(F(F(d[0] * d[0] + d[2] * d[2]) + d[1] * d[1])))
+    p2p1, p3p2, p1p3 = nrm(a, b), nrm(b, c), nrm(c, a)
+    s = (p2p1 + p3p2 + p1p3) / 2.0
+    with np.errstate(invalid="ignore", divide="ignore"):
+        area = math.sqrt(s * (s - p2p1) * (s - p3p2) * (s - p1p3)) if s * (s - p2p1) * (s - p3p2) * (s - p1p3) >= 0 else float("nan")
+        return (p2p1 * p3p2 * p1p3) / (4.0 * area) if area > 0 else float("inf")
+
+
+def _tet_radius(V):
+    A = V[1:] - V[0]
+    rhs = 0.5 * (A * A).sum(axis=1)
+    try:
+        x = np.linalg.solve(A, rhs)
+    except np.linalg.LinAlgError:
+        return float("inf")
+    return float(np.sqrt((x * x).sum()))
+
+
 def concave_hull(P, alpha):
-    """computeConcaveHull (odom.cc:1033-1065): points whose nearest other point is within 2 alpha (odom.hip)."""
-    P = P.astype(np.float64)
-    out = []
-    for i in range(len(P)):
-        d = np.sqrt(((P - P[i]) ** 2).sum(axis=1))
-        d[i] = np.inf
-        if d.min() / 2 <= alpha:
-            out.append(i)
-    return out
+    """computeConcaveHull (odom.cc:1030-1065): pcl::ConcaveHull, dimension 3, alpha = keyframe_thresh_dist_.
+    qhull "d QJ" Delaunay of the demeaned points; a tetrahedron is good iff its circumradius <= alpha; a
+    triangle is kept iff one side is not a good tetrahedron (outside or bad) and it has circumradius <= alpha
+    (a good tetrahedron's triangles always do); the hull = the kept triangles' vertices."""
+    P = np.asarray(P, np.float64)
+    if len(P) < 4:
+        return []
+    D = P - P.mean(axis=0)
+    try:
+        tri = Delaunay(D, qhull_options="QJ")
+    except QhullError:
+        return []
+    S = tri.simplices
+    good = np.array([_tet_radius(D[s]) <= alpha for s in S])
+    on = np.zeros(len(P), bool)
+    for t, s in enumerate(S):
+        for j in range(4):
+            nb = tri.neighbors[t, j]
+            if nb >= 0 and nb < t:
+                continue   # each triangle once
+            gb = nb >= 0 and good[nb]
+            if good[t] and gb:
+                continue
+            f = np.delete(s, j)
+            if good[t] or gb or _tri_radius(D[f[0]], D[f[1]], D[f[2]]) <= alpha:
+                on[f] = True
+    return [int(i) for i in np.nonzero(on)[0]]
 
 
 def push_submap_indices(dists, k, frames, out):
@@ -150,6 +187,7 @@ class OdomRef:
         self.keyframe_convex = []
         self.keyframe_concave = []
         self.median_prev = None
+        self.initialized = False    # ddlo_initialized_
         self.thresh = float(params.keyframe_thresh_dist)
         self.submap = None
 
@@ -165,7 +203,7 @@ class OdomRef:
         kf = transform(scan, self.T)
         if self.p.vf_submap_use:
             kf = O.voxel_grid(kf, self.p.vf_submap_res)
-        cov = O.covariances(kf, self.s2s.k_correspondences, threads=self.threads)
+        cov = O.covariances(kf, min(self.s2s.k_correspondences, len(kf)), threads=self.threads)
         self.keyframes.append((self.pose.copy(), list(self.rotq), kf, cov))
 
     def process(self, pts):
@@ -173,6 +211,11 @@ class OdomRef:
         if len(pts) < self.p.min_num_points:
             out["status"] = 2
             return out
+        if not self.initialized:    # initializeDDLO consumes the first valid scan (odom.cc:641-646)
+            self.initialized = True
+            if getattr(self.p, "skip_first_scan", 1):
+                out["status"] = 3
+                return out
         scan = self._preprocess(pts)
         out["scan_points"] = len(scan)
         # computeSpaciousness (odom.cc:981-1001)

@@ -96,34 +96,69 @@ def test_odometry_without_gpu_fails_loudly():
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_convex_hull_matches_qhull(seed):
+    """pcl::ConvexHull with setDimension(3) (odom.cc:87): qhull's 3-D vertex set; a flat keyframe set is qhull's
+    flat-simplex error, i.e. no convex keyframes at all."""
     rng = np.random.default_rng(seed)
-    planar = rng.uniform(-20, 20, (60, 3)).astype(np.float32)
-    planar[:, 2] = 1.5                                      # keyframes of a ground vehicle: dimension 2
-    np.testing.assert_array_equal(OD.convex_hull(planar), np.sort(ConvexHull(planar[:, :2]).vertices))
-    assert OD.convex_hull(planar).tolist() == R.convex_hull(planar)
-    solid = rng.uniform(-20, 20, (80, 3)).astype(np.float32)   # dimension 3
+    solid = rng.uniform(-20, 20, (80, 3)).astype(np.float32)
     np.testing.assert_array_equal(OD.convex_hull(solid), np.sort(ConvexHull(solid).vertices))
     assert OD.convex_hull(solid).tolist() == R.convex_hull(solid)
+    thin = rng.uniform(-20, 20, (60, 3)).astype(np.float32)   # a ground vehicle's keyframes: z varies by cm
+    thin[:, 2] = (1.5 + rng.normal(0, 0.02, 60)).astype(np.float32)
+    np.testing.assert_array_equal(OD.convex_hull(thin), np.sort(ConvexHull(thin).vertices))
+    flat = thin.copy()
+    flat[:, 2] = 1.5
+    assert OD.convex_hull(flat).tolist() == [] == R.convex_hull(flat)
+    assert OD.convex_hull(solid[:3]).tolist() == []
 
 
 def test_convex_hull_of_a_trajectory():
     from dynamic_direct_lidar_odometry_amd import scene
     poses = scene.trajectory(400, 1007)
     kf = np.array([p[:3, 3] for p in poses[::10]], np.float32)
+    kf[:, 2] += np.random.default_rng(4).normal(0, 0.01, len(kf)).astype(np.float32)   # estimated poses: never level
     np.testing.assert_array_equal(OD.convex_hull(kf), np.array(R.convex_hull(kf)))
     assert len(OD.convex_hull(kf)) >= 3
 
 
-@pytest.mark.parametrize("alpha", [0.3, 1.0, 5.0])
-def test_concave_hull_edge_criterion(alpha):
+def _alpha_shape_cases():
     rng = np.random.default_rng(3)
-    P2 = rng.uniform(-10, 10, (50, 3)).astype(np.float32)
-    P2[:, 2] = 0.0
-    assert OD.concave_hull(P2, alpha).tolist() == R.concave_hull(P2, alpha)
-    # every returned point has its nearest neighbour within 2 alpha, and no other one does
-    D = np.sqrt(((P2[:, None, :].astype(np.float64) - P2[None, :, :]) ** 2).sum(-1))
-    np.fill_diagonal(D, np.inf)
-    np.testing.assert_array_equal(OD.concave_hull(P2, alpha), np.nonzero(D.min(1) / 2 <= alpha)[0])
+    blob = (rng.standard_normal((60, 3)) * [4, 4, 2]).astype(np.float32)            # interior points
+    box = rng.uniform(-10, 10, (50, 3)).astype(np.float32)
+    shell = rng.standard_normal((40, 3))
+    shell = (shell / np.linalg.norm(shell, axis=1, keepdims=True) * 6).astype(np.float32)
+    ring = np.concatenate([shell, (rng.standard_normal((15, 3)) * 0.8).astype(np.float32)])   # hollow + core
+    return {"blob": blob, "box": box, "shell_core": ring}
+
+
+@pytest.mark.parametrize("name", ["blob", "box", "shell_core"])
+@pytest.mark.parametrize("alpha", [0.8, 2.0, 4.0, 50.0, 1e7])
+def test_concave_hull_is_qhull_alpha_shape(name, alpha):
+    """pcl::ConcaveHull with setDimension(3): the boundary vertices of the alpha shape of qhull's "d QJ" 3-D
+    Delaunay (oracle via scipy's qhull); interior keyframes are not on it."""
+    P3 = _alpha_shape_cases()[name]
+    got = OD.concave_hull(P3, alpha).tolist()
+    assert got == R.concave_hull(P3, alpha)
+    if alpha == 1e7:   # every tetrahedron good: the boundary is the convex hull
+        assert got == OD.convex_hull(P3).tolist()
+
+
+def test_concave_hull_excludes_interior_keyframes():
+    rng = np.random.default_rng(11)
+    g = np.stack(np.meshgrid(np.arange(6), np.arange(6), np.arange(4), indexing="ij"), -1).reshape(-1, 3)
+    P3 = (g + rng.uniform(-0.05, 0.05, g.shape)).astype(np.float32)   # a jittered 6 x 6 x 4 block of keyframes
+    got = set(OD.concave_hull(P3, 1.5).tolist())
+    assert got == set(R.concave_hull(P3, 1.5))
+    interior = {i for i, p in enumerate(g) if 0 < p[0] < 5 and 0 < p[1] < 5 and 0 < p[2] < 3}
+    assert interior and not (got & interior)
+    assert got                                           # the block's faces are
+
+
+def test_concave_hull_of_a_straight_path_is_empty():
+    """Collinear keyframes: every Delaunay triangle is a sliver of huge circumradius."""
+    P3 = np.stack([np.arange(12, dtype=np.float32), np.zeros(12, np.float32), np.zeros(12, np.float32)], 1)
+    P3[:, 1] = (np.arange(12) % 2) * np.float32(1e-3)
+    P3[:, 2] = (np.arange(12) % 3) * np.float32(1e-3)
+    assert OD.concave_hull(P3, 1.0).tolist() == []
 
 
 def test_push_submap_indices_keeps_ties():
