@@ -10,7 +10,7 @@ LIBDIR := $(PKG)/_lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
 OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/nftree.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o $(LIBDIR)/segment.o
 
-all: lib oracle facade
+all: lib oracle facade raycast
 
 lib: $(LIBDIR)/libddlo_gicp.so
 
@@ -48,16 +48,22 @@ $(LIBDIR)/libddlo_gicp.so: $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# test / bench infrastructure: the GPU twin of scene.py's ray caster (cfg 5 frame synthesis)
+raycast: tools/raycast/libddlo_raycast.so
+
+tools/raycast/libddlo_raycast.so: tools/raycast/raycast.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+
 facade: tests/cpp/facade_replay
 
 tests/cpp/facade_replay: tests/cpp/facade_replay.cpp include/nano_gicp/nano_gicp.hpp include/ddlo_gicp.h $(LIBDIR)/libddlo_gicp.so
 	g++ -std=c++17 -O2 -Iinclude -o $@ tests/cpp/facade_replay.cpp -L$(LIBDIR) -lddlo_gicp -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 clean:
-	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so tests/cpp/facade_replay
+	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so tests/cpp/facade_replay tools/raycast/libddlo_raycast.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle facade clean
+.PHONY: all lib oracle facade raycast clean
 
 # developer variant: k_lm_step prints per-phase cycle counts (load with DDLO_GICP_LIB)
 lmprof: $(OBJS)

@@ -40,7 +40,19 @@ class Scene:
     peds_vel: np.ndarray      # (Q,2) xy velocity (m/s); zero for static ones
 
 
-def make_scene(seed: int = 1000, n_peds: int = 20, moving: bool = False) -> Scene:
+# cfg 5's closed loop (loop_trajectory): an ellipse inside the square, so a
+# 1000-frame (100 m) sequence stays in the plaza and revisits its keyframes
+LOOP_X, LOOP_Y = 14.0, 7.0
+
+
+def _near_loop(x, y, margin):
+    """|distance| from the loop ellipse below ~margin (radial measure)."""
+    r = math.sqrt((x / LOOP_X) ** 2 + (y / LOOP_Y) ** 2)
+    return abs(r - 1.0) * min(LOOP_X, LOOP_Y) < margin
+
+
+def make_scene(seed: int = 1000, n_peds: int = 20, moving: bool = False, loop: bool = False) -> Scene:
+    """loop = True: objects keep 2.5 m (pedestrians 1.5 m) clear of the cfg 5 loop path (loop_trajectory)."""
     rng = np.random.default_rng(seed)
     lo, hi = [], []
     # facade pilasters: shallow boxes attached to the four walls, irregular spacing
@@ -79,7 +91,9 @@ def make_scene(seed: int = 1000, n_peds: int = 20, moving: bool = False) -> Scen
     # benches and kiosks inside the square
     for _ in range(12):
         cx, cy = rng.uniform(-PLAZA_X + 4, PLAZA_X - 4), rng.uniform(-PLAZA_Y + 4, PLAZA_Y - 4)
-        if abs(cy) < 2.5 and -15 < cx < 15:   # keep the driving corridor free
+        while loop and _near_loop(cx, cy, 4.5):
+            cx, cy = rng.uniform(-PLAZA_X + 4, PLAZA_X - 4), rng.uniform(-PLAZA_Y + 4, PLAZA_Y - 4)
+        if abs(cy) < 2.5 and -15 < cx < 15 and not loop:   # keep the driving corridor free
             cy += 5.0 * np.sign(cy if cy != 0 else 1.0)
         ang = rng.uniform(0, math.pi)
         L = rng.uniform(1.5, 4.0)
@@ -91,13 +105,17 @@ def make_scene(seed: int = 1000, n_peds: int = 20, moving: bool = False) -> Scen
     poles = []
     for _ in range(18):
         cx, cy = rng.uniform(-PLAZA_X + 2, PLAZA_X - 2), rng.uniform(-PLAZA_Y + 2, PLAZA_Y - 2)
-        if abs(cy) < 2.0 and -15 < cx < 15:
+        while loop and _near_loop(cx, cy, 2.5):
+            cx, cy = rng.uniform(-PLAZA_X + 2, PLAZA_X - 2), rng.uniform(-PLAZA_Y + 2, PLAZA_Y - 2)
+        if abs(cy) < 2.0 and -15 < cx < 15 and not loop:
             cy += 4.0 * np.sign(cy if cy != 0 else 1.0)
         poles.append([cx, cy, rng.uniform(0.06, 0.25), rng.uniform(3.0, 8.0)])
     plo, phi, pvel = [], [], []
     for _ in range(n_peds):
         cx, cy = rng.uniform(-PLAZA_X + 3, PLAZA_X - 3), rng.uniform(-PLAZA_Y + 3, PLAZA_Y - 3)
-        if abs(cy) < 1.5 and -15 < cx < 15:
+        while loop and _near_loop(cx, cy, 1.5):
+            cx, cy = rng.uniform(-PLAZA_X + 3, PLAZA_X - 3), rng.uniform(-PLAZA_Y + 3, PLAZA_Y - 3)
+        if abs(cy) < 1.5 and -15 < cx < 15 and not loop:
             cy += 3.0 * np.sign(cy if cy != 0 else 1.0)
         w = rng.uniform(0.3, 0.6)
         plo.append([cx - w / 2, cy - w / 2, 0.0]); phi.append([cx + w / 2, cy + w / 2, rng.uniform(1.5, 1.95)])
@@ -306,3 +324,101 @@ def sequence(rows: int, cols: int, n_frames: int, n_unique: int, cfg_id: int = 5
         k += step
     order = order[:n_frames]
     return [uniq[i] for i in order], [poses[i] for i in order]
+
+
+# ---------------------------------------------------------------------------
+# cfg 5 at its named size (BASELINE.json configs[4]: 1000 frames): a closed
+# loop, pedestrians bouncing inside the square, frames synthesised by the GPU
+# twin of raycast() (tools/raycast, test/bench infrastructure) when it is
+# built and a device is visible, else by raycast() itself.
+def loop_trajectory(n_frames: int, seed: int = 1005) -> list:
+    """Ground-truth poses along the LOOP_X x LOOP_Y ellipse at 1.0 m/s, 10 Hz (0.1 m per frame), heading
+    along the path with a small yaw wobble; 1000 frames are ~1.4 laps."""
+    rng = np.random.default_rng(seed)
+    th, poses = -math.pi / 2, []
+    wob = 0.0
+    for _ in range(n_frames):
+        x, y = LOOP_X * math.cos(th), LOOP_Y * math.sin(th)
+        dx, dy = -LOOP_X * math.sin(th), LOOP_Y * math.cos(th)
+        wob = float(np.clip(0.9 * wob + rng.normal(0, 0.01), -0.05, 0.05))
+        poses.append(make_pose([x, y, SENSOR_Z], (0.0, 0.0, math.atan2(dy, dx) + wob)))
+        th += 0.1 / math.hypot(dx, dy)
+    return poses
+
+
+def _bounce(c, v, t, lo, hi):
+    """Position c + v t reflected into [lo, hi] (a pedestrian walking back and forth)."""
+    span = hi - lo
+    u = (c + v * t - lo) % (2 * span)
+    return lo + (u if u <= span else 2 * span - u)
+
+
+def ped_boxes(scene: Scene, t: float):
+    """Pedestrian AABBs at time t, bouncing inside the square (loop scenes)."""
+    lo = scene.peds_lo.copy()
+    hi = scene.peds_hi.copy()
+    for q in range(len(lo)):
+        for a, lim in ((0, PLAZA_X - 2.0), (1, PLAZA_Y - 2.0)):
+            half = 0.5 * (hi[q, a] - lo[q, a])
+            c = _bounce(0.5 * (lo[q, a] + hi[q, a]), scene.peds_vel[q, a], t, -lim, lim)
+            lo[q, a], hi[q, a] = c - half, c + half
+    return lo, hi
+
+
+def _raycast_lib():
+    import ctypes as C
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "raycast",
+                        "libddlo_raycast.so")
+    if not os.path.exists(path):
+        return None
+    L = C.CDLL(path)
+    P = C.c_void_p
+    L.ddlo_raycast.restype = C.c_int
+    L.ddlo_raycast.argtypes = [C.c_int, C.c_int, C.c_int, P, P, C.c_int, P, P, C.c_int, P, C.c_int, P, P, P, P,
+                               C.c_double, C.c_double, C.c_double]
+    return L
+
+
+def loop_sequence(rows: int, cols: int, first: int, count: int, cfg_id: int = 5, device: int = 0,
+                  gpu: bool = True):
+    """Frames first .. first+count-1 of cfg 5's 1000-frame loop (moving pedestrians), sensor frame, no-return
+    pixels dropped; frame k uses seed 1000 + cfg_id + k and time 0.1 k.  Returns (frames, world poses)."""
+    seed = 1000 + cfg_id
+    sc = make_scene(seed, moving=True, loop=True)
+    poses = loop_trajectory(first + count, seed)[first:]
+    L = _raycast_lib() if gpu else None
+    if L is None:
+        out = []
+        for j, P in enumerate(poses):
+            k = first + j
+            lo, hi = ped_boxes(sc, 0.1 * k)
+            s2 = Scene(sc.boxes_lo, sc.boxes_hi, sc.poles, lo, hi, np.zeros_like(sc.peds_vel))
+            out.append(raycast(s2, P, rows, cols, seed=seed + k))
+        return out, poses
+    import ctypes as C
+    dirs = np.ascontiguousarray(lidar_dirs(rows, cols), np.float64)
+    nr = rows * cols
+    frames = []
+    bl, bh = np.ascontiguousarray(sc.boxes_lo, np.float64), np.ascontiguousarray(sc.boxes_hi, np.float64)
+    pl = np.ascontiguousarray(sc.poles, np.float64)
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p)
+    for b0 in range(0, count, 64):
+        nb = min(64, count - b0)
+        T = np.ascontiguousarray(np.stack(poses[b0:b0 + nb]), np.float64)
+        plo = np.empty((nb, len(sc.peds_lo), 3))
+        phi = np.empty_like(plo)
+        noise = np.empty((nb, nr))
+        for j in range(nb):
+            k = first + b0 + j
+            plo[j], phi[j] = ped_boxes(sc, 0.1 * k)
+            noise[j] = np.random.default_rng(seed + k).normal(0.0, 0.01, size=nr)
+        out = np.empty((nb, nr, 3), np.float32)
+        rc = L.ddlo_raycast(device, nb, nr, ptr(dirs), ptr(T), len(bl), ptr(bl), ptr(bh), len(pl), ptr(pl),
+                            len(sc.peds_lo), ptr(plo), ptr(phi), ptr(noise), ptr(out), PLAZA_X, PLAZA_Y, FACADE_H)
+        if rc != 0:
+            raise RuntimeError(f"ddlo_raycast failed ({rc})")
+        for j in range(nb):
+            f = out[j]
+            frames.append(np.ascontiguousarray(f[np.isfinite(f[:, 0])]))
+    return frames, poses
