@@ -169,12 +169,13 @@ def sharded_leg(dist, rank, world, local_rank, args):
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
-    sh = ShardedGicp(local_rank, rank, world, uid, params)
-    slab = sh.set_target(sub, tcov)
-    sh.set_source(src, scov)
     guess = prob["guess"].astype(np.float32)
+    sh = ShardedGicp(local_rank, rank, world, uid, params, mode=args.shard_mode)
+    slab = sh.set_target(sub, tcov, source=src, guess=guess)
+    sh.set_source(src, scov)
     log(f"[rank {rank}] sharded setup {time.time() - t0:.1f}s: src {len(src)} tgt {len(sub)} "
-        f"local {len(sh.local_index)} slab axis {slab.axis} [{slab.lo:.2f}, {slab.hi:.2f})")
+        f"local {len(sh.local_index)} mode {args.shard_mode}" +
+        (f" slab axis {slab.axis} [{slab.lo:.2f}, {slab.hi:.2f})" if slab is not None else ""))
     for _ in range(2):
         out, res = sh.align(guess)
     sh.ctx.synchronize()
@@ -197,6 +198,9 @@ def sharded_leg(dist, rank, world, local_rank, args):
     sh.close()
     out_leg = {"workload": "cfg4 S2M: 262,144-pt 128x2048 scan -> 2,000,000-pt 8-keyframe submap, LM, maxCorr 2.0 m",
                "n_gpus": world, "ms_per_scan": round(1e3 * elapsed / args.sharded_steps, 4),
+               "shard_mode": (f"groups: target replicated, rank r owns the source's 16-point groups = r mod {world}"
+                              if args.shard_mode == "groups" else
+                              "slabs: spatial slabs cut on the owned source at the guess, 2 m target halo"),
                "iters_per_s": round(iters / elapsed, 2), "iterations_per_scan": res.iterations_run,
                "converged": bool(res.converged), "target_points_per_rank_max": None,
                "collective": "RCCL all-reduce, 80 fp64 per outer iteration" + (" (in graph)" if graphs else " (eager)"),
@@ -393,6 +397,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-sharded", action="store_true", help="skip the spatially sharded cfg4 leg")
     ap.add_argument("--sharded-steps", type=int, default=10)
+    ap.add_argument("--shard-mode", choices=["groups", "slabs"], default="groups",
+                    help="cfg4 ownership: interleaved source groups (replicated target) or source-balanced slabs")
     ap.add_argument("--no-batch", action="store_true", help="skip the frame-parallel S2S cfg5 leg")
     ap.add_argument("--batch-frames", type=int, default=1000, help="cfg 5 sequence length (unique frames)")
     ap.add_argument("--batch-streams", type=int, default=3)

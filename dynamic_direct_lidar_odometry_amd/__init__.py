@@ -123,6 +123,7 @@ def load():
         "gicp_get_stream": (I, [P, C.POINTER(P)]),
         "gicp_synchronize": (I, [P]),
         "gicp_set_shard": (I, [P, I, C.c_float, C.c_float]),
+        "gicp_set_shard_groups": (I, [P, I, I]),
         "gicp_comm_unique_id": (I, [P, S]),
         "gicp_set_comm": (I, [P, P, S, I, I]),
         "gicp_get_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
@@ -369,6 +370,10 @@ class Context:
     # ---- spatial sharding
     def set_shard(self, axis: int, lo: float = -np.inf, hi: float = np.inf):
         self._check(self.L.gicp_set_shard(self.h, int(axis), float(lo), float(hi)))
+
+    def set_shard_groups(self, nparts: int, part: int):
+        """Interleaved ownership: this ctx searches the 16-point groups = part (mod nparts)."""
+        self._check(self.L.gicp_set_shard_groups(self.h, int(nparts), int(part)))
 
     def set_comm(self, unique_id: bytes | None, nranks: int, rank: int):
         buf = None

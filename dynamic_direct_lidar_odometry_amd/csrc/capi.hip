@@ -177,6 +177,8 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.own_axis = c->own_axis;
   j.own_lo = c->own_lo;
   j.own_hi = c->own_hi;
+  j.own_mod = c->own_mod;
+  j.own_rem = c->own_rem;
   j.split_extent = kn.split_extent;
   j.premom = c->comm ? 1 : 0;
   j.mom = c->mom.as<double>();
@@ -1004,6 +1006,15 @@ gicp_status gicp_set_shard(gicp_ctx* c, int axis, float lo, float hi) {
   c->own_axis = axis;
   c->own_lo = axis >= 0 ? lo : -INFINITY;
   c->own_hi = axis >= 0 ? hi : INFINITY;
+  invalidate_align(c);
+  return GICP_OK;
+}
+
+gicp_status gicp_set_shard_groups(gicp_ctx* c, int nparts, int part) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  if (nparts < 0 || (nparts > 0 && (part < 0 || part >= nparts))) return fail(GICP_EINVAL, "invalid shard part");
+  c->own_mod = nparts <= 1 ? 0 : nparts;
+  c->own_rem = nparts <= 1 ? 0 : part;
   invalidate_align(c);
   return GICP_OK;
 }

@@ -111,6 +111,10 @@ struct AlignJob {
   // target holds that slab plus a max_corr halo.  own_axis < 0: unsharded.
   int own_axis;
   float own_lo, own_hi;
+  // Interleaved sharding (the target replicated on every rank): this rank
+  // owns the source points whose 16-point group of the device's spatial
+  // (Morton) order is = own_rem mod own_mod.  own_mod = 0: off.
+  int own_mod, own_rem;
   // premom = 1: k_mom_reduce writes this rank's reduced moments to mom, the
   // host's collective sums them across ranks in place, and k_lm_step reads
   // mom instead of reducing the slab itself.

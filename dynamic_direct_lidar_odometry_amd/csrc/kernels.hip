@@ -846,6 +846,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   const double tri_mv = job->tri_mv;
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
+  const int own_mod = job->own_mod, own_rem = job->own_rem;
   const int lane = lane_id();
   const int qi = lane % Q;
   const int wib = threadIdx.x >> 6;
@@ -887,7 +888,8 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
     // spatial sharding: search only the queries this rank owns
     const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
-    const bool owned = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi));
+    const bool owned = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi)) &&
+                       (own_mod == 0 || ((i >> 4) % own_mod) == own_rem);
     // Verified reuse (AlignJob::ref): every target point other than p1 was
     // at fp32 squared distance >= B^2 from q_ref, so (relative 1e-6 covers
     // the fp32 rounding of a squared distance) its true distance from q is
@@ -1491,6 +1493,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
   const double tri_mv = job->tri_mv;
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
+  const int own_mod = job->own_mod, own_rem = job->own_rem;
   float Rf[9], tf[3];
   for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
   for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
@@ -1527,7 +1530,8 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
     // spatial sharding: search only the queries this rank owns
     const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
-    const bool active = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi));
+    const bool active = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi)) &&
+                        (own_mod == 0 || ((i >> 4) % own_mod) == own_rem);
     if (!__any(active)) {
       if (inrange && lane < Q) {
         corr[i] = -1;

@@ -251,6 +251,7 @@ struct gicp_ctx {
   // spatial sharding: ownership slab + RCCL communicator
   int own_axis = -1;
   float own_lo = -INFINITY, own_hi = INFINITY;
+  int own_mod = 0, own_rem = 0;   // interleaved sharding (gicp_set_shard_groups)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   DevBuf mom;          // [kSlabStride] reduced moments, all-reduced in place

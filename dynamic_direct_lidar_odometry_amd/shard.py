@@ -17,8 +17,23 @@ outgrows one GPU, the same sum is split by SPACE instead of by thread:
   moments) are summed with ONE RCCL all-reduce per iteration inside the
   align graph, and every rank runs the identical LM step on identical sums.
 
+The work of a rank is its OWNED SOURCE points, not its target points: a
+lidar scan is dense near the sensor, so target-count-balanced slabs gave one
+rank up to 2.65x the mean query count at 8 ranks.  Two balanced modes:
+
+* ``mode="slabs"``: the cuts are quantiles of the source transformed by the
+  align's initial guess along its longest extent (plan_slabs_by_source), the
+  target keeps the slab + halo rule above;
+* ``mode="groups"`` (default while the submap fits one GPU — 2M points are
+  ~200 MB of the 288 GB): the target is replicated and rank r owns the
+  16-point groups of the source's spatial order = r (mod nranks)
+  (``gicp_set_shard_groups``), SURVEY.md §8(e)'s replicated-target
+  alternative with the same single all-reduce; query counts differ by at most
+  one group and every rank's queries span the whole scan.
+
 This module is the host side: slab planning (pure numpy, testable on CPU)
-and a per-rank driver over the C-ABI (``gicp_set_shard`` / ``gicp_set_comm``).
+and a per-rank driver over the C-ABI (``gicp_set_shard`` /
+``gicp_set_shard_groups`` / ``gicp_set_comm``).
 """
 from __future__ import annotations
 
@@ -26,7 +41,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-__all__ = ["Slab", "plan_slabs", "halo_indices", "owner_of", "ShardedGicp"]
+__all__ = ["Slab", "plan_slabs", "plan_slabs_by_source", "halo_indices", "owner_of", "group_owner",
+           "ShardedGicp"]
 
 
 @dataclass(frozen=True)
@@ -53,6 +69,25 @@ def plan_slabs(points: np.ndarray, nranks: int, axis: int | None = None) -> list
     cuts = np.maximum.accumulate(np.asarray(cuts, np.float32)) if cuts else np.zeros(0, np.float32)
     bounds = [np.float32(-np.inf)] + [np.float32(c) for c in cuts] + [np.float32(np.inf)]
     return [Slab(axis, float(bounds[r]), float(bounds[r + 1])) for r in range(nranks)]
+
+
+def transform_f32(points: np.ndarray, T: np.ndarray) -> np.ndarray:
+    """The kernels' fp32 query transform, (r0 x + r1 y) + (r2 z + t) (oracle/cpu_ref.cpp)."""
+    p = np.asarray(points, np.float32)[:, :3]
+    R = np.asarray(T, np.float64)[:3, :3].astype(np.float32)
+    t = np.asarray(T, np.float64)[:3, 3].astype(np.float32)
+    return np.stack([(R[r, 0] * p[:, 0] + R[r, 1] * p[:, 1]) + (R[r, 2] * p[:, 2] + t[r]) for r in range(3)], 1)
+
+
+def plan_slabs_by_source(source: np.ndarray, guess: np.ndarray, nranks: int, axis: int | None = None) -> list[Slab]:
+    """Slabs that balance the queries each rank OWNS: count-balanced cuts of the source transformed by the
+    align's initial guess (the pose of the first search), along its longest extent."""
+    return plan_slabs(transform_f32(source, guess), nranks, axis)
+
+
+def group_owner(n: int, nranks: int) -> np.ndarray:
+    """Rank owning each sorted source position under gicp_set_shard_groups: (position // 16) % nranks."""
+    return (np.arange(n) // 16) % nranks
 
 
 def halo_width(max_corr: float) -> float:
@@ -85,21 +120,38 @@ class ShardedGicp:
     ``nranks == 1`` runs the same code path with a one-rank communicator.
     """
 
-    def __init__(self, device: int, rank: int, nranks: int, unique_id: bytes, params):
+    def __init__(self, device: int, rank: int, nranks: int, unique_id: bytes, params, mode: str = "groups"):
         from . import Context
+        if mode not in ("groups", "slabs"):
+            raise ValueError("mode must be 'groups' or 'slabs'")
         self.rank, self.nranks = rank, nranks
         self.params = params
+        self.mode = mode
         self.ctx = Context(device)
         self.ctx.set_params(params)
         self.ctx.set_comm(unique_id, nranks, rank)
         self.slab: Slab | None = None
         self.local_index: np.ndarray | None = None
 
-    def set_target(self, points: np.ndarray, covs: np.ndarray, axis: int | None = None):
+    def set_target(self, points: np.ndarray, covs: np.ndarray, axis: int | None = None,
+                   source: np.ndarray | None = None, guess: np.ndarray | None = None):
         """Whole submap + its covariances (computed on the whole cloud, as the
-        per-keyframe covariances of odom.cc:1147-1149,1302-1310 are)."""
+        per-keyframe covariances of odom.cc:1147-1149,1302-1310 are).  Slab
+        mode balances the owned source at `guess` when source and guess are
+        given (else the target count)."""
         from . import TARGET
-        slabs = plan_slabs(points, self.nranks, axis)
+        if self.mode == "groups":
+            self.slab = None
+            self.local_index = np.arange(len(points), dtype=np.int64)
+            self.ctx.set_target(np.ascontiguousarray(np.asarray(points, np.float32)[:, :3]))
+            self.ctx.set_covariances(TARGET, np.ascontiguousarray(covs))
+            self.ctx.set_shard(-1)
+            self.ctx.set_shard_groups(self.nranks, self.rank)
+            return None
+        if source is not None and guess is not None:
+            slabs = plan_slabs_by_source(source, guess, self.nranks, axis)
+        else:
+            slabs = plan_slabs(points, self.nranks, axis)
         self.slab = slabs[self.rank]
         idx = halo_indices(points, self.slab, self.params.max_correspondence_distance)
         if len(idx) == 0:  # an empty rank still needs a valid cloud; it owns no queries
@@ -107,6 +159,7 @@ class ShardedGicp:
         self.local_index = idx
         self.ctx.set_target(np.ascontiguousarray(np.asarray(points, np.float32)[idx, :3]))
         self.ctx.set_covariances(TARGET, np.ascontiguousarray(covs[idx]))
+        self.ctx.set_shard_groups(0, 0)
         self.ctx.set_shard(self.slab.axis, self.slab.lo, self.slab.hi)
         return self.slab
 

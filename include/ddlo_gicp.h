@@ -240,6 +240,14 @@ gicp_status gicp_get_stream(const struct gicp_ctx* ctx, void** stream);
  * max_corr of an owned query lies in the slab + halo. */
 /* Ownership slab of this ctx; axis -1 removes it. */
 gicp_status gicp_set_shard(struct gicp_ctx* ctx, int axis, float lo, float hi);
+/* Interleaved sharding, for a target that fits every GPU (it is replicated):
+ * rank `part` of `nparts` owns the source points whose 16-point group in the
+ * device's spatial (Morton) order is congruent to part mod nparts, so every
+ * rank searches the same number of points spread over the whole scan.
+ * Combines with gicp_set_shard (both predicates must hold); nparts <= 1
+ * removes it.  Exact for the same reason as the slabs: every owned point
+ * sees the whole target. */
+gicp_status gicp_set_shard_groups(struct gicp_ctx* ctx, int nparts, int part);
 /* ncclGetUniqueId (128 bytes) — call on one rank and broadcast. */
 gicp_status gicp_comm_unique_id(uint8_t* out, size_t nbytes);
 /* ncclCommInitRank on the ctx's device (collective over the nranks ranks);

@@ -81,9 +81,9 @@ def test_comm1_align_identical_to_plain():
     out0, r0 = plain.align(g["guess"])
     res0 = plain.residuals()
     uid = P.comm_unique_id()
-    sh = ShardedGicp(0, 0, 1, uid, P.default_params(**S2M))
+    sh = ShardedGicp(0, 0, 1, uid, P.default_params(**S2M), mode="slabs")
     assert sh.ctx.comm_info()[0] == 1
-    sh.set_target(g["sub"], g["cov_sub"])
+    sh.set_target(g["sub"], g["cov_sub"], source=g["src"], guess=g["guess"])
     assert sh.slab.lo == -np.inf and sh.slab.hi == np.inf
     sh.set_source(g["src"], g["cov_src"])
     out1, r1 = sh.align(g["guess"])
@@ -99,6 +99,50 @@ def test_comm1_align_identical_to_plain():
     plain.close()
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_group_shards_moments_add_up(world):
+    """Interleaved ownership (gicp_set_shard_groups, replicated target): the N parts' moments sum to the
+    unsharded linearize, their matched counts add up, and every point is searched by exactly one part with
+    the unsharded answer."""
+    g = load_golden("gicp_s2m.npz")
+    pose = g["guess"].astype(np.float64)
+    full = full_ctx(g)
+    H, b, cost, nc = full.linearize(pose)
+    mom = full.moments()
+    fcorr, fsqd = full.correspondences()
+    tot = np.zeros(80)
+    ntot = 0
+    matched = np.zeros(len(g["src"]), np.int64)
+    for r in range(world):
+        c = full_ctx(g)
+        c.set_shard_groups(world, r)
+        _, _, _, n_r = c.linearize(pose)
+        tot += c.moments()
+        ntot += n_r
+        corr, _ = c.correspondences()
+        matched += corr >= 0
+        np.testing.assert_array_equal(corr[corr >= 0], fcorr[corr >= 0])
+        c.close()
+    assert ntot == nc
+    np.testing.assert_array_equal(matched, (fcorr >= 0).astype(np.int64))
+    np.testing.assert_allclose(tot[:74], mom[:74], rtol=1e-10, atol=1e-10 * np.abs(mom[:74]).max())
+    full.close()
+
+
+def test_group_shard_comm1_align_identical_to_plain():
+    g = load_golden("gicp_s2m.npz")
+    plain = full_ctx(g)
+    out0, r0 = plain.align(g["guess"])
+    sh = ShardedGicp(0, 0, 1, P.comm_unique_id(), P.default_params(**S2M))   # default mode: groups
+    sh.set_target(g["sub"], g["cov_sub"])
+    sh.set_source(g["src"], g["cov_src"])
+    out1, r1 = sh.align(g["guess"])
+    np.testing.assert_array_equal(out1, out0)
+    assert (r1.iterations_run, r1.lm_trials) == (r0.iterations_run, r0.lm_trials)
+    sh.close()
+    plain.close()
+
+
 def test_shard_arguments_rejected():
     c = P.Context(0)
     with pytest.raises(P.GicpError):
@@ -106,6 +150,8 @@ def test_shard_arguments_rejected():
     with pytest.raises(P.GicpError):
         c.set_shard(0, 1.0, 1.0)
     c.set_shard(-1)
+    with pytest.raises(P.GicpError):
+        c.set_shard_groups(4, 4)
     with pytest.raises(P.GicpError):
         c.set_comm(b"\0" * 128, 2, 5)
     c.close()

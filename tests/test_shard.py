@@ -16,7 +16,8 @@ import pytest
 
 import np_gicp as NP
 from conftest import load_golden
-from dynamic_direct_lidar_odometry_amd.shard import halo_indices, owner_of, plan_slabs
+from dynamic_direct_lidar_odometry_amd.shard import (group_owner, halo_indices, owner_of, plan_slabs,
+                                                      plan_slabs_by_source, transform_f32)
 
 
 def test_plan_slabs_partition_and_balance():
@@ -36,6 +37,30 @@ def test_plan_slabs_partition_and_balance():
         q = np.array([[s.lo, 0, 0] for s in slabs[1:]], np.float32)
         if len(q):
             np.testing.assert_array_equal(owner_of(q, slabs), np.arange(1, n))
+
+
+@pytest.fixture(scope="module")
+def cfg4():
+    from dynamic_direct_lidar_odometry_amd import scene
+    return scene.s2m_problem(128, 2048, 8, 2000000, 4)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_cfg4_owned_query_balance(cfg4, world):
+    """The work of a rank is the source points it OWNS.  On cfg 4 (262k-pt scan, 2M-pt submap, guess pose):
+    slabs cut on the target count give up to 2.65x the mean at 8 ranks; cuts on the source transformed by the
+    guess, or interleaved 16-point groups, stay within 1.25x."""
+    src, guess = cfg4["source"], cfg4["guess"]
+    sub = np.concatenate(cfg4["keyframes"])[cfg4["subset"]]
+    q = transform_f32(src, guess)
+    by_target = np.bincount(owner_of(q, plan_slabs(sub, world)), minlength=world)
+    by_source = np.bincount(owner_of(q, plan_slabs_by_source(src, guess, world)), minlength=world)
+    by_group = np.bincount(group_owner(len(src), world), minlength=world)
+    for counts in (by_source, by_group):
+        assert counts.sum() == len(src)
+        assert counts.max() / counts.mean() <= 1.25, counts
+    print(f"world {world}: target-balanced max/mean {by_target.max() / by_target.mean():.2f}, source-balanced "
+          f"{by_source.max() / by_source.mean():.3f}, groups {by_group.max() / by_group.mean():.4f}")
 
 
 def test_halo_contains_every_bounded_neighbour():
