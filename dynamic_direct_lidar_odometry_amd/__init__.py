@@ -131,6 +131,7 @@ def load():
         "gicp_residual_image": (I, [P, D, D, I, I, P, P]),
         "gicp_set_tie_order": (I, [P, I]),
         "gicp_debug_nftree": (I, [P, I, P, P, P, S, C.POINTER(S)]),
+        "gicp_debug_nfbuild": (I, [P, I, I, P, P, P, P, S]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -349,6 +350,18 @@ class Context:
         div = np.empty((nn.value, 2), np.float32)
         self._check(self.L.gicp_debug_nftree(self.h, side, _ptr(vind), _ptr(nodes), _ptr(div), nn.value, C.byref(nn)))
         return vind, nodes, div
+
+    def nfbuild_debug(self, side, stop=-1, scratch_bytes=1 << 20):
+        """A fresh device tree build stopped after `stop` big levels (development):
+        (vind, info16, (err, nnodes), raw scratch bytes)."""
+        n = self.size(side)
+        vind = np.empty(n, np.int32)
+        info = np.zeros(16, np.int64)
+        st = np.zeros(2, np.int32)
+        raw = np.zeros(scratch_bytes, np.uint8)
+        self._check(self.L.gicp_debug_nfbuild(self.h, side, int(stop), _ptr(vind), _ptr(info), _ptr(st), _ptr(raw),
+                                               raw.nbytes))
+        return vind, info, st, raw
 
     def debug_stats(self, enable=True, read=False):
         """Per 64-query group search counters of the last linearize (development)."""

@@ -963,6 +963,33 @@ gicp_status gicp_debug_nftree(gicp_ctx* c, int side, int32_t* vind, int32_t* nod
   return GICP_OK;
 }
 
+gicp_status gicp_debug_nfbuild(gicp_ctx* c, int side, int stop, int32_t* vind, int64_t* info16, int32_t* status2,
+                               void* scratch, size_t scratch_cap) {
+  if (!c || (side != 0 && side != 1) || !vind || !info16 || !status2) return fail(GICP_EINVAL, "invalid argument");
+  Side& sd = side == GICP_SIDE_SOURCE ? c->src : c->tgt;
+  if (!sd.cloud) return fail(GICP_ESTATE, "no cloud on this side");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  NfTreeData t;
+  long long off[16];
+  s = nftree_build(c, *sd.cloud, c->stream, t, stop, off);
+  if (s) return s;
+  for (int i = 0; i < 16; ++i) info16[i] = off[i];
+  HIP_TRY(hipMemcpyAsync(status2, t.status.p, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  std::vector<float4> v((size_t)t.n);
+  HIP_TRY(hipMemcpyAsync(v.data(), t.vpts.p, sizeof(float4) * (size_t)t.n, hipMemcpyDeviceToHost, c->stream));
+  if (scratch && scratch_cap)
+    HIP_TRY(hipMemcpyAsync(scratch, c->nf_scratch.p, std::min(scratch_cap, (size_t)off[13]), hipMemcpyDeviceToHost,
+                           c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < t.n; ++i) {
+    int w;
+    std::memcpy(&w, &v[(size_t)i].w, sizeof(int));
+    vind[i] = w;
+  }
+  return GICP_OK;
+}
+
 gicp_status gicp_get_moments(const gicp_ctx* c, double* out80) {
   if (!c || !out80) return fail(GICP_EINVAL, "null argument");
   std::memcpy(out80, final_state(c).last_mom, sizeof(double) * kSlabStride);

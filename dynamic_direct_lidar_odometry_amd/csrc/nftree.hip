@@ -336,17 +336,25 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(NfBuild b, int L) {
     const float x = coord(e[j], feat);
     const bool good = PASS == 1 ? (x < cut) : (x == cut);
     float4 out = e[j];
-    if (p >= zlo && p < zhi && !good) {   // misplaced left: rank among the bad ones of the zone
-      const int r = (p - zlo) - pref;
-      if (TABLE) b.tblL[tk.begin + r] = e[j];
-      else out = b.tblR[tk.begin + r];
-    } else if (p >= zhi && good) {        // misplaced right: rank from the end
-      const int r = ngood - pref - 1;
-      if (TABLE) b.tblR[tk.begin + r] = e[j];
-      else out = b.tblL[tk.begin + r];
+    bool moved = false;
+    int r = -1;
+    if (p >= zlo && p < zhi && !good) r = (p - zlo) - pref;   // misplaced left: rank among the zone's bad ones
+    else if (p >= zhi && good) r = ngood - pref - 1;          // misplaced right: rank from the end
+    else r = -2;
+    if (r == -1 || r < -2 || r >= tk.count) {   // never: a rank outside the task (guard against corrupt counts)
+      atomicOr(&b.ctl->err, 16);
+      r = -2;
+    }
+    if (r >= 0) {
+      const bool left = p < zhi;
+      if (TABLE) (left ? b.tblL : b.tblR)[tk.begin + r] = e[j];
+      else out = (left ? b.tblR : b.tblL)[tk.begin + r];
+      moved = true;
     }
     if (!TABLE) {
-      if (out.x != e[j].x || out.y != e[j].y || out.z != e[j].z || out.w != e[j].w) b.vpts[tk.begin + p] = out;
+      // (w holds the index bits: a float compare would see small indices as
+      // equal denormals, so the write follows the rank logic, not the values)
+      if (moved) b.vpts[tk.begin + p] = out;
       if (PASS == 1) ecount += coord(out, feat) == cut;
       e[j] = out;
     }
@@ -448,7 +456,8 @@ __device__ __forceinline__ float wred(float x, bool mx) {
 // v == cut for pass 2), boundary zhi: pair the r-th bad element of
 // [zlo0, zhi) with the r-th good element of [zhi, n) from the end
 template <class IT>
-__device__ void small_pass(float4* P, IT* ML, IT* MR, int zlo0, int zhi, int n, int feat, float cut, bool pass2) {
+__device__ void small_pass(float4* P, IT* ML, IT* MR, int cap, int zlo0, int zhi, int n, int feat, float cut, bool pass2,
+                           int* err) {
   const int lane = __lane_id();
   int m = 0;
   for (int i0 = zlo0; i0 < zhi; i0 += 64) {
@@ -459,7 +468,8 @@ __device__ void small_pass(float4* P, IT* ML, IT* MR, int zlo0, int zhi, int n, 
       f = !(pass2 ? x == cut : x < cut);
     }
     const unsigned long long mask = __ballot(f);
-    if (f) ML[m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u))] = (IT)i;
+    const int slot = m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+    if (f && slot < cap) ML[slot] = (IT)i;
     m += __popcll(mask);
   }
   int m2 = 0;
@@ -471,11 +481,16 @@ __device__ void small_pass(float4* P, IT* ML, IT* MR, int zlo0, int zhi, int n, 
       f = pass2 ? x == cut : x < cut;
     }
     const unsigned long long mask = __ballot(f);
-    if (f) MR[m2 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u))] = (IT)i;
+    const int slot = m2 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+    if (f && slot < cap) MR[slot] = (IT)i;
     m2 += __popcll(mask);
   }
   __syncthreads();
-  const int mm = min(m, m2);   // equal by construction
+  if (m != m2 || m > cap) {   // never (equal by construction): report, swap nothing
+    if (lane == 0) atomicOr(err, 32);
+    return;
+  }
+  const int mm = m;
   for (int r = lane; r < mm; r += 64) {
     const int a = ML[r], c = MR[r];
     const float4 t = P[a];
@@ -488,7 +503,7 @@ __device__ void small_pass(float4* P, IT* ML, IT* MR, int zlo0, int zhi, int n, 
 // divideTree below one node, depth first: P = the node's points (LDS, or
 // global for an oversized node), base = their vind offset
 template <class IT>
-__device__ void small_tree(const NfBuild& b, SmallLds* S, float4* P, IT* ML, IT* MR, const NfTask& tk) {
+__device__ void small_tree(const NfBuild& b, SmallLds* S, float4* P, IT* ML, IT* MR, int mlcap, const NfTask& tk) {
   NfCtl* ctl = b.ctl;
   const int lane = __lane_id();
   const int base = tk.begin;
@@ -548,8 +563,8 @@ __device__ void small_tree(const NfBuild& b, SmallLds* S, float4* P, IT* ML, IT*
       lim1 += __popcll(__ballot(i < n && x < cut));
       lim2 += __popcll(__ballot(i < n && x <= cut));
     }
-    small_pass(Q, ML, MR, 0, lim1, n, feat, cut, false);
-    small_pass(Q, ML, MR, lim1, lim2, n, feat, cut, true);
+    small_pass(Q, ML, MR, mlcap, 0, lim1, n, feat, cut, false, &ctl->err);
+    small_pass(Q, ML, MR, mlcap, lim1, lim2, n, feat, cut, true, &ctl->err);
     const int index = nf_index(n, lim1, lim2);
     int c1 = 0;
     if (lane == 0) c1 = atomicAdd(&ctl->nnodes, 2);
@@ -584,20 +599,20 @@ __device__ void small_tree(const NfBuild& b, SmallLds* S, float4* P, IT* ML, IT*
 }
 
 __global__ __launch_bounds__(64) void k_nf_small(NfBuild b) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  SmallLds* S = reinterpret_cast<SmallLds*>(smem);
+  __shared__ SmallLds S_lds;   // static (~79 KB: gfx950 gives one workgroup up to 160 KB)
+  SmallLds* S = &S_lds;
   if ((int)blockIdx.x >= b.ctl->nsmall) return;
   const NfTask tk = b.small[blockIdx.x];
   const int lane = __lane_id();
   if (tk.count <= kNfT) {
     for (int i = lane; i < tk.count; i += 64) S->P[i] = b.vpts[tk.begin + i];
     __syncthreads();
-    small_tree<unsigned short>(b, S, S->P, S->ML, S->MR, tk);
+    small_tree<unsigned short>(b, S, S->P, S->ML, S->MR, kNfT / 2, tk);
     __syncthreads();
     for (int i = lane; i < tk.count; i += 64) b.vpts[tk.begin + i] = S->P[i];
   } else {   // in place in global memory; the rank lists use the pairing tables' space
     small_tree<unsigned>(b, S, b.vpts + tk.begin, reinterpret_cast<unsigned*>(b.tblL + tk.begin),
-                         reinterpret_cast<unsigned*>(b.tblR + tk.begin), tk);
+                         reinterpret_cast<unsigned*>(b.tblR + tk.begin), tk.count, tk);
   }
 }
 
@@ -765,16 +780,12 @@ NfSizes nf_sizes(int n) {
 
 size_t nf_small_lds_bytes() { return sizeof(SmallLds); }
 
-void launch_nf_build(hipStream_t s, const NfBuild& b, const float4* sorted_pts) {
-  static const bool lds_ok = [] {
-    return hipFuncSetAttribute((const void*)k_nf_small, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)sizeof(SmallLds)) == hipSuccess;
-  }();
-  (void)lds_ok;
+void launch_nf_build(hipStream_t s, const NfBuild& b, const float4* sorted_pts, int stop) {
   k_nf_unsort<<<cdivl(b.n, 256), 256, 0, s>>>(sorted_pts, b.n, b.vpts);
   k_nf_init<<<1, 64, 0, s>>>(b);
   const int G = std::max(1, b.max_chunks);
   for (int L = 0; L < b.Lmax; ++L) {
+    if (stop >= 0 && L >= stop) return;
     k_nf_map<<<1, 1024, 0, s>>>(b, L);
     k_nf_count<<<G, kNfBT, 0, s>>>(b, L);
     k_nf_pass<1, true><<<G, kNfBT, 0, s>>>(b, L);
@@ -783,7 +794,7 @@ void launch_nf_build(hipStream_t s, const NfBuild& b, const float4* sorted_pts) 
     k_nf_pass<2, false><<<G, kNfBT, 0, s>>>(b, L);
   }
   k_nf_map<<<1, 1024, 0, s>>>(b, b.Lmax);
-  k_nf_small<<<b.max_small, 64, sizeof(SmallLds), s>>>(b);
+  k_nf_small<<<b.max_small, 64, 0, s>>>(b);
   k_nf_refit<<<cdivl(b.cap, 256), 256, 0, s>>>(b);
 }
 

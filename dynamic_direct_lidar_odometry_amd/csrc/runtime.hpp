@@ -373,10 +373,12 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   return GICP_OK;
 }
 
-// nanoflann's tree of a cloud (once per cloud, on the given stream)
-inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s) {
-  if (cd.nf) return GICP_OK;
-  auto t = std::make_shared<NfTreeData>();
+// Build nanoflann's tree of cd into t on the given stream.  stop >= 0 (the
+// diagnostics entry only) runs that many big levels and nothing after;
+// off (optional, 16 entries) receives the sizes and the scratch offsets.
+inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s, NfTreeData& tr, int stop = -1,
+                                long long* off = nullptr) {
+  NfTreeData* t = &tr;
   const int n = cd.n;
   t->n = n;
   t->cap = 2 * n + 2;   // a tree of n points has at most 2n - 1 nodes
@@ -421,11 +423,26 @@ inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s) {
   b.max_pend = z.max_pend;
   b.max_small = z.max_small;
   b.max_chunks = z.max_chunks;
+  if (off) {
+    const long long v[16] = {z.Lmax, z.max_task, z.max_pend, z.max_small, z.max_chunks, (long long)o_tasks,
+                             (long long)o_pend, (long long)o_small, (long long)o_cmap, (long long)o_cA,
+                             (long long)o_cAE, (long long)o_cE2, (long long)o_tblL, (long long)total, n, t->cap};
+    for (int i = 0; i < 16; ++i) off[i] = v[i];
+  }
   HIP_TRY(hipMemsetAsync(b.arrive, 0, sizeof(int) * (size_t)t->cap, s));
-  launch_nf_build(s, b, cd.pts.as<float4>());
+  launch_nf_build(s, b, cd.pts.as<float4>(), stop);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(t->status.p, &b.ctl->err, sizeof(int), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(t->status.as<int>() + 1, &b.ctl->nnodes, sizeof(int), hipMemcpyDeviceToDevice, s));
+  return GICP_OK;
+}
+
+// nanoflann's tree of a cloud (once per cloud, on the given stream)
+inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s) {
+  if (cd.nf) return GICP_OK;
+  auto t = std::make_shared<NfTreeData>();
+  gicp_status st = nftree_build(c, cd, s, *t);
+  if (st) return st;
   cd.nf = t;
   return GICP_OK;
 }

@@ -213,6 +213,14 @@ gicp_status gicp_set_tie_order(struct gicp_ctx* ctx, int nanoflann_order);
  * outputs NULL only *nnodes is returned. */
 gicp_status gicp_debug_nftree(struct gicp_ctx* ctx, int side, int32_t* vind, int32_t* nodes4, float* div2, size_t cap,
                               size_t* nnodes);
+/* Build diagnostics (development): a fresh build of a side's tree that stops
+ * after `stop` big levels (-1 = complete), returning vind[n] as it stands,
+ * info16 = {Lmax, max_task, max_pend, max_small, max_chunks, scratch offsets
+ * of tasks, pend, small, chunk map, cA, cAE, cE2, tables, total bytes, n,
+ * node capacity}, status2 = {error bits, nodes}, and the first scratch_cap
+ * bytes of the build's scratch (control word, task lists, counts). */
+gicp_status gicp_debug_nfbuild(struct gicp_ctx* ctx, int side, int stop, int32_t* vind, int64_t* info16,
+                               int32_t* status2, void* scratch, size_t scratch_cap);
 /* The 74 reduced normal-equation moments of the last linearize (80 doubles,
  * layout in DESIGN.md "Normal-equation moments"); test/debug entry. */
 gicp_status gicp_get_moments(const struct gicp_ctx* ctx, double* out80);

@@ -184,31 +184,33 @@ def ref_tree(points):
 
 
 def same_tree(a, b):
-    """Two exported trees (any node numbering) describe the same nanoflann tree: identical vind and, walked from
-    the roots, identical leaves, divfeat, divlow and divhigh.  Returns a mismatch description or None."""
+    """Two exported trees (any node numbering) describe the same nanoflann tree: walked from the roots,
+    identical leaves (vind ranges), divfeat, divlow and divhigh, then identical vind.  Returns a mismatch
+    description (the first differing node's depth and its leaf / subtree vind range) or None."""
     va, na, da = a
     vb, nb, db = b
+    st = [(0, 0, 0)]
+    seen = 0
+    while st:
+        x, y, depth = st.pop()
+        seen += 1
+        if na[x, 2] != nb[y, 2]:
+            return f"depth {depth}: node kind/divfeat differs ({x} vs {y}): {na[x, 2]} vs {nb[y, 2]}"
+        if na[x, 2] < 0:
+            if na[x, 0] != nb[y, 0] or na[x, 1] != nb[y, 1]:
+                return f"depth {depth}: leaf range differs: {na[x, :2]} vs {nb[y, :2]}"
+            if not np.array_equal(va[na[x, 0]:na[x, 1]], vb[nb[y, 0]:nb[y, 1]]):
+                return f"depth {depth}: leaf {na[x, :2]} holds different points"
+            continue
+        if not (da[x, 0] == db[y, 0] and da[x, 1] == db[y, 1]):   # +-0 are the same split
+            return f"depth {depth}: divlow/divhigh differ at ({x}, {y}): {da[x]} vs {db[y]}"
+        st.append((na[x, 1], nb[y, 1], depth + 1))
+        st.append((na[x, 0], nb[y, 0], depth + 1))
+    if seen != len(na) or seen != len(nb):
+        return f"node counts differ: walked {seen}, sizes {len(na)} / {len(nb)}"
     if not np.array_equal(va, vb):
         i = int(np.argmax(va != vb))
         return f"vind differs first at {i}: {va[i]} vs {vb[i]}"
-    st = [(0, 0)]
-    seen = 0
-    while st:
-        x, y = st.pop()
-        seen += 1
-        if na[x, 2] != nb[y, 2]:
-            return f"node kind/divfeat differs ({x} vs {y}): {na[x, 2]} vs {nb[y, 2]}"
-        if na[x, 2] < 0:
-            if na[x, 0] != nb[y, 0] or na[x, 1] != nb[y, 1]:
-                return f"leaf range differs: {na[x, :2]} vs {nb[y, :2]}"
-            continue
-        if da[x, 0].view(np.int32) != db[y, 0].view(np.int32) or da[x, 1].view(np.int32) != db[y, 1].view(np.int32):
-            if not (da[x, 0] == db[y, 0] and da[x, 1] == db[y, 1]):   # +-0 are the same split
-                return f"divlow/divhigh differ at ({x}, {y}): {da[x]} vs {db[y]}"
-        st.append((na[x, 1], nb[y, 1]))
-        st.append((na[x, 0], nb[y, 0]))
-    if seen != len(na) or seen != len(nb):
-        return f"node counts differ: walked {seen}, sizes {len(na)} / {len(nb)}"
     return None
 
 

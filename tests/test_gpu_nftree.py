@@ -98,3 +98,50 @@ def test_register_input_source_keeps_covariances():
     assert not c.has_covariances(SOURCE)
     c.set_source(b)                             # setInputSource clears them (:142)
     assert not c.has_covariances(SOURCE)
+
+
+_TASK = np.dtype([("node", "<i4"), ("begin", "<i4"), ("count", "<i4"), ("chunk0", "<i4"), ("lo", "<f4", 3),
+                  ("hi", "<f4", 3), ("mm", "<u4", 6), ("feat", "<i4"), ("cut", "<f4"), ("nch", "<i4"), ("pad", "<i4")])
+
+
+def _ctl(raw):
+    w = raw[:46 * 4].view(np.int32)
+    return dict(nnodes=int(w[0]), nsmall=int(w[1]), err=int(w[2]), ntask=w[5:46].tolist())
+
+
+@pytest.mark.parametrize("name", ["one_small_node", "duplicates", "lattice77k", "normal40k"])
+def test_device_build_levels_match_emulator(name):
+    """Level by level: the device's vind after each big level equals the
+    block-by-block transliteration (tests/nf_emu.py), and so do the task lists;
+    localises a difference in the build to its level."""
+    import nf_emu
+    pts = _clouds()[name]
+    c = P.Context(0)
+    c.set_target(pts)
+    trace = []
+    nf_emu.build(pts, trace=trace)
+    first_bad = None
+    for stop in range(int(c.nfbuild_debug(TARGET, stop=0, scratch_bytes=64)[1][0]) + 1):
+        v_dev, _, st_s, _ = c.nfbuild_debug(TARGET, stop=stop, scratch_bytes=64)
+        v_emu = nf_emu.build(pts, stop=stop)
+        same = np.array_equal(v_dev, v_emu)
+        print("stop", stop, "status", st_s.tolist(), "same", same,
+              "" if same else f"first diff at {int(np.argmax(v_dev != v_emu))}")
+        if not same and first_bad is None:
+            first_bad = stop
+    vind, info, st, raw = c.nfbuild_debug(TARGET, stop=-1, scratch_bytes=1 << 22)
+    Lmax, max_task, max_pend, max_small = (int(x) for x in info[:4])
+    ctl = _ctl(raw)
+    print(name, "info", info.tolist(), "status", st.tolist(), "ctl", ctl["nnodes"], ctl["nsmall"], ctl["err"],
+          ctl["ntask"][:Lmax + 1])
+    small = raw[info[7]:info[7] + _TASK.itemsize * max_small].view(_TASK)[:ctl["nsmall"]]
+    print("small counts (device)", sorted(small["count"].tolist())[-6:], "max", small["count"].max() if len(small) else 0)
+    for (L, tasks, nsm) in trace:
+        dev_t = raw[info[5] + _TASK.itemsize * L * max_task:][:_TASK.itemsize * max_task].view(_TASK)
+        nt = ctl["ntask"][L] if L < Lmax else 0
+        emu = sorted((t["begin"], t["count"]) for t in tasks)
+        dev = sorted((int(t["begin"]), int(t["count"])) for t in dev_t[:nt])
+        print("level", L, "emu tasks", emu[:6], "dev", dev[:6])
+    v_full = nf_emu.build(pts)
+    print("full same", np.array_equal(vind, v_full))
+    assert first_bad is None and st[0] == 0 and np.array_equal(vind, v_full)
