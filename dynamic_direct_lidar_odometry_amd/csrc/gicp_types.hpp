@@ -186,6 +186,7 @@ struct NfCtl {
   int nnodes, nsmall, err;   // err bits: 1 node capacity, 2 node left too large, 4 depth, 8 list capacity
   int nchunks[2];
   int ntask[kNfMaxLevels + 1];
+  int dbg[16];               // the first failed check's context (diagnostics)
 };
 
 // A node to split: its vind range, the box divideTree passes down (the

@@ -48,6 +48,11 @@ __device__ __forceinline__ float o2f(unsigned o) {
   return __uint_as_float(u);
 }
 __device__ __forceinline__ float coord(const float4& p, int f) { return f == 0 ? p.x : (f == 1 ? p.y : p.z); }
+// Coordinate f of a point in memory: one load at a computed address.  (The
+// select form on a memory operand was lowered by ROCm 7.2's hipcc into a
+// per-lane branch that left the f == 2 lanes loading from an unset address:
+// wrong z splits in LDS, a fault in global memory.)
+__device__ __forceinline__ float coord_at(const float4* p, int f) { return reinterpret_cast<const float*>(p)[f]; }
 
 // middleSplit_ (:1045-1087): cut dimension and value from the passed-down
 // box and the node's point min / max (computeMinMax, :965-978)
@@ -163,6 +168,7 @@ __global__ void k_nf_init(NfBuild b) {
     ctl->err = 0;
     ctl->nchunks[0] = ctl->nchunks[1] = 0;
     for (int l = 0; l <= kNfMaxLevels; ++l) ctl->ntask[l] = 0;
+    for (int l = 0; l < 16; ++l) ctl->dbg[l] = 0;
     NfTask r;
     r.node = 0;
     r.begin = 0;
@@ -274,7 +280,7 @@ __global__ __launch_bounds__(kNfBT) void k_nf_count(NfBuild b, int L) {
   const int p0 = v.c * kNfCH, p1 = min(p0 + kNfCH, v.tk.count);
   int a = 0, ae = 0;
   for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-    const float x = coord(b.vpts[v.tk.begin + p], feat);
+    const float x = coord_at(&b.vpts[v.tk.begin + p], feat);
     a += x < cut;
     ae += x <= cut;
   }
@@ -457,14 +463,14 @@ __device__ __forceinline__ float wred(float x, bool mx) {
 // [zlo0, zhi) with the r-th good element of [zhi, n) from the end
 template <class IT>
 __device__ void small_pass(float4* P, IT* ML, IT* MR, int cap, int zlo0, int zhi, int n, int feat, float cut, bool pass2,
-                           int* err) {
+                           NfCtl* ctl) {
   const int lane = __lane_id();
   int m = 0;
   for (int i0 = zlo0; i0 < zhi; i0 += 64) {
     const int i = i0 + lane;
     bool f = false;
     if (i < zhi) {
-      const float x = coord(P[i], feat);
+      const float x = coord_at(&P[i], feat);
       f = !(pass2 ? x == cut : x < cut);
     }
     const unsigned long long mask = __ballot(f);
@@ -477,7 +483,7 @@ __device__ void small_pass(float4* P, IT* ML, IT* MR, int cap, int zlo0, int zhi
     const int i = i0 - 1 - lane;   // lane order = descending positions
     bool f = false;
     if (i >= zhi) {
-      const float x = coord(P[i], feat);
+      const float x = coord_at(&P[i], feat);
       f = pass2 ? x == cut : x < cut;
     }
     const unsigned long long mask = __ballot(f);
@@ -487,7 +493,14 @@ __device__ void small_pass(float4* P, IT* ML, IT* MR, int cap, int zlo0, int zhi
   }
   __syncthreads();
   if (m != m2 || m > cap) {   // never (equal by construction): report, swap nothing
-    if (lane == 0) atomicOr(err, 32);
+    if (lane == 0) {
+      atomicOr(&ctl->err, 32);
+      int* dbg = ctl->dbg;
+      if (atomicCAS(dbg, 0, 1) == 0) {
+        dbg[1] = zlo0; dbg[2] = zhi; dbg[3] = n; dbg[4] = feat; dbg[5] = __float_as_int(cut);
+        dbg[6] = pass2; dbg[7] = m; dbg[8] = m2; dbg[9] = cap; dbg[10] = (int)blockIdx.x;
+      }
+    }
     return;
   }
   const int mm = m;
@@ -556,15 +569,17 @@ __device__ void small_tree(const NfBuild& b, SmallLds* S, float4* P, IT* ML, IT*
     int feat;
     float cut;
     nf_cut(t, &feat, &cut);
+    feat = __builtin_amdgcn_readfirstlane(feat);   // wave-uniform by construction: scalar from here on
+    cut = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cut)));
     int lim1 = 0, lim2 = 0;
     for (int i0 = 0; i0 < n; i0 += 64) {
       const int i = i0 + lane;
-      const float x = i < n ? coord(Q[i], feat) : INFINITY;
+      const float x = i < n ? coord_at(&Q[i], feat) : INFINITY;
       lim1 += __popcll(__ballot(i < n && x < cut));
       lim2 += __popcll(__ballot(i < n && x <= cut));
     }
-    small_pass(Q, ML, MR, mlcap, 0, lim1, n, feat, cut, false, &ctl->err);
-    small_pass(Q, ML, MR, mlcap, lim1, lim2, n, feat, cut, true, &ctl->err);
+    small_pass(Q, ML, MR, mlcap, 0, lim1, n, feat, cut, false, ctl);
+    small_pass(Q, ML, MR, mlcap, lim1, lim2, n, feat, cut, true, ctl);
     const int index = nf_index(n, lim1, lim2);
     int c1 = 0;
     if (lane == 0) c1 = atomicAdd(&ctl->nnodes, 2);

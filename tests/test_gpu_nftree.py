@@ -106,7 +106,8 @@ _TASK = np.dtype([("node", "<i4"), ("begin", "<i4"), ("count", "<i4"), ("chunk0"
 
 def _ctl(raw):
     w = raw[:46 * 4].view(np.int32)
-    return dict(nnodes=int(w[0]), nsmall=int(w[1]), err=int(w[2]), ntask=w[5:46].tolist())
+    return dict(nnodes=int(w[0]), nsmall=int(w[1]), err=int(w[2]), ntask=w[5:46].tolist(),
+                dbg=raw[46 * 4:62 * 4].view(np.int32).tolist())
 
 
 @pytest.mark.parametrize("name", ["one_small_node", "duplicates", "lattice77k", "normal40k"])
@@ -133,7 +134,7 @@ def test_device_build_levels_match_emulator(name):
     Lmax, max_task, max_pend, max_small = (int(x) for x in info[:4])
     ctl = _ctl(raw)
     print(name, "info", info.tolist(), "status", st.tolist(), "ctl", ctl["nnodes"], ctl["nsmall"], ctl["err"],
-          ctl["ntask"][:Lmax + 1])
+          ctl["ntask"][:Lmax + 1], "dbg", ctl["dbg"], "cut", np.int32(ctl["dbg"][5]).view(np.float32))
     small = raw[info[7]:info[7] + _TASK.itemsize * max_small].view(_TASK)[:ctl["nsmall"]]
     print("small counts (device)", sorted(small["count"].tolist())[-6:], "max", small["count"].max() if len(small) else 0)
     for (L, tasks, nsm) in trace:
