@@ -10,36 +10,39 @@ namespace ddlo {
 // ============================================================================
 // small fp64 linear algebra (per lane)
 // ============================================================================
-// Symmetric 3x3 cyclic Jacobi eigen-decomposition: lam[j], V[j][i] = v_j[i]
+// Symmetric 3x3 cyclic Jacobi eigen-decomposition: lam[j], V[j][i] = v_j[i].
+// The whole 3x3 is rotated in place (its two triangles may drift apart by an
+// ulp), operation for operation as oracle/cpu_ref.cpp sym_eig3: the
+// regularised covariance of a (near-)isotropic neighbourhood depends on the
+// last bit of the rotations, so device and oracle must share the sequence.
 __device__ inline void sym_eig3(const double A[9], double lam[3], double V[3][3]) {
-  double a00 = A[0], a01 = A[1], a02 = A[2], a11 = A[4], a12 = A[5], a22 = A[8];
+  double a[3][3] = {{A[0], A[1], A[2]}, {A[3], A[4], A[5]}, {A[6], A[7], A[8]}};
   double v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
   for (int sweep = 0; sweep < 50; ++sweep) {
-    const double off = fabs(a01) + fabs(a02) + fabs(a12);
-    const double scale = fabs(a00) + fabs(a11) + fabs(a22);
+    const double off = fabs(a[0][1]) + fabs(a[0][2]) + fabs(a[1][2]);
+    const double scale = fabs(a[0][0]) + fabs(a[1][1]) + fabs(a[2][2]);
     if (off <= 1e-300 || off <= scale * 1e-18) break;
 #pragma unroll
     for (int pq = 0; pq < 3; ++pq) {
       const int p = pq == 2 ? 1 : 0;
       const int q = pq == 0 ? 1 : 2;
-      double m[3][3] = {{a00, a01, a02}, {a01, a11, a12}, {a02, a12, a22}};
-      const double apq = m[p][q];
+      const double apq = a[p][q];
       if (apq == 0.0) continue;
-      const double theta = (m[q][q] - m[p][p]) / (2.0 * apq);
+      const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
       const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
       const double c = 1.0 / sqrt(t * t + 1.0);
       const double s = t * c;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double akp = m[k][p], akq = m[k][q];
-        m[k][p] = c * akp - s * akq;
-        m[k][q] = s * akp + c * akq;
+      for (int k = 0; k < 3; ++k) {   // A <- J^T A J
+        const double akp = a[k][p], akq = a[k][q];
+        a[k][p] = c * akp - s * akq;
+        a[k][q] = s * akp + c * akq;
       }
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const double apk = m[p][k], aqk = m[q][k];
-        m[p][k] = c * apk - s * aqk;
-        m[q][k] = s * apk + c * aqk;
+        const double apk = a[p][k], aqk = a[q][k];
+        a[p][k] = c * apk - s * aqk;
+        a[q][k] = s * apk + c * aqk;
       }
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -47,15 +50,14 @@ __device__ inline void sym_eig3(const double A[9], double lam[3], double V[3][3]
         v[k][p] = c * vkp - s * vkq;
         v[k][q] = s * vkp + c * vkq;
       }
-      a00 = m[0][0]; a01 = m[0][1]; a02 = m[0][2];
-      a11 = m[1][1]; a12 = m[1][2]; a22 = m[2][2];
     }
   }
-  lam[0] = a00; lam[1] = a11; lam[2] = a22;
 #pragma unroll
-  for (int j = 0; j < 3; ++j)
+  for (int j = 0; j < 3; ++j) {
+    lam[j] = a[j][j];
 #pragma unroll
     for (int i = 0; i < 3; ++i) V[j][i] = v[i][j];
+  }
 }
 
 // 3x3 inverse by adjugate (general, row-major)

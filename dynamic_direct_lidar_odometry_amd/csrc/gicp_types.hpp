@@ -242,6 +242,8 @@ struct KnnJob {
   unsigned* n2;                  // second-round lists handed out
   int cap2, max2;
   float split_extent;
+  int* tie_list;                 // optional: sorted positions whose k-th distance is tied (nanoflann re-runs them)
+  int* tie_count;
 };
 
 }  // namespace ddlo

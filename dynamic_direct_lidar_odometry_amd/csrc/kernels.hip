@@ -418,7 +418,10 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
     vis.qz = q.z;
     knn_self_search(c, vis, 2 * g - 1, 2 * g + 2, gp(c.keys)[min(i, c.n - 1)], L);
     if (!vis.active) continue;
-    if (ties.list && vis.outside_min() == vis.kth_dist()) ties.list[atomicAdd(ties.count, 1)] = i;
+    // a tie at the k-th distance changes the set; one inside the k changes the
+    // summation order, which the eigen-decomposition of a degenerate
+    // (isotropic) neighbourhood turns into a different regularized covariance
+    if (ties.list && (vis.outside_min() == vis.kth_dist() || vis.inner_tie())) ties.list[atomicAdd(ties.count, 1)] = i;
     cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
   }
 }
@@ -529,7 +532,7 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
     }
     vis.merge_halves();
     if (!vis.active || lane_id() >= 32) continue;
-    if (ties.list && vis.td == vis.kth_dist()) ties.list[atomicAdd(ties.count, 1)] = i;
+    if (ties.list && (vis.td == vis.kth_dist() || vis.inner_tie())) ties.list[atomicAdd(ties.count, 1)] = i;
     cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
   }
 }

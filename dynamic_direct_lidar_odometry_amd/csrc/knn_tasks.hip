@@ -281,6 +281,7 @@ __global__ __launch_bounds__(256) void k_knn_select(KnnJob j) {
   const unsigned long long* cl = j.round == 2 ? j.cand2 + (size_t)j.slot2[i] * j.cap2 : j.cand + i;
   const size_t stride = j.round == 2 ? 1 : (size_t)c.n;
   const unsigned ne = min(nc, cap);
+  unsigned long long out_min = ~0ull;   // the smallest key not kept (the exact-tie test below)
   for (unsigned e = 0; e < ne; ++e) {
     unsigned long long key = cl[(size_t)e * stride];
 #pragma unroll
@@ -290,6 +291,7 @@ __global__ __launch_bounds__(256) void k_knn_select(KnnJob j) {
       key = key < K[s] ? K[s] : key;
       K[s] = lo;
     }
+    out_min = key < out_min ? key : out_min;
   }
   if (nc > cap) {
     // first-round overflow: the k-th of the stored candidates (k real points)
@@ -309,6 +311,20 @@ __global__ __launch_bounds__(256) void k_knn_select(KnnJob j) {
     j.slot2[i] = sl;
     j.again[i] = 1;
     return;
+  }
+  if (j.tie_list) {
+    // a point at exactly the k-th distance left out: nanoflann's walk decides
+    // which of the tied points is kept (nftree.hip re-runs this query)
+    // (or two of the kept k equidistant: their order is nanoflann's walk order)
+    unsigned long long kth = K[0];
+    bool inner = false;
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      if (s == k - 1) kth = K[s];
+      if (!EXACT && s >= k && K[s] < out_min) out_min = K[s];
+      if (s >= 1 && s < k) inner |= (K[s] >> 32) == (K[s - 1] >> 32);
+    }
+    if (inner || (out_min != ~0ull && (out_min >> 32) == (kth >> 32))) j.tie_list[atomicAdd(j.tie_count, 1)] = i;
   }
   // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
   double mx = 0, my = 0, mz = 0;

@@ -492,6 +492,14 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   const char* tv = std::getenv("DDLO_COV_TASKS");
   const bool tasks = tv && *tv == '1';
   const CloudDev cd = side.cloud->dev();
+  // exact ties: the points whose k-th neighbour distance is tied get their
+  // neighbourhood from nanoflann's own search (nftree.hip)
+  TieList tl{nullptr, nullptr};
+  if (c->tie_exact) {
+    gicp_status st = ensure_nftree(c, *side.cloud, c->stream);
+    if (!st) st = tie_scratch(c, side.cloud->n, c->stream, &tl);
+    if (st) return st;
+  }
   if (tasks && k <= 32) {
     // scratch of the task-based kNN; a queued covariance launch may still
     // read the old block, so growing it waits for the stream
@@ -534,9 +542,11 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     j.cap = cap;
     j.task_cap_r = cap_r;
     j.split_extent = 5.0f;
+    j.tie_list = tl.list;
+    j.tie_count = tl.count;
     if (!launch_knn_covariances(c->stream, j, side.cloud->upper_count()))
       return fail(GICP_EINVAL, "unsupported k");
-    launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), j.redo);
+    launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), j.redo, tl);
     if (std::getenv("DDLO_COV_DEBUG")) {   // development: how many groups needed the fallback
       std::vector<unsigned char> r((n + 63) / 64);
       std::vector<unsigned> cn(n);
@@ -549,23 +559,14 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
       std::fprintf(stderr, "[cov] n %d k %d redo groups %zu / %zu, points over cap %zu, mean cand %.1f max %zu\n", n, k,
                    nr, r.size(), over, (double)sum / n, mx);
     }
-  } else {
-    // exact ties: the points whose k-th neighbour distance is tied get their
-    // neighbourhood from nanoflann's own search (nftree.hip)
-    TieList tl{nullptr, nullptr};
-    if (c->tie_exact) {
-      gicp_status st = ensure_nftree(c, *side.cloud, c->stream);
-      if (!st) st = tie_scratch(c, side.cloud->n, c->stream, &tl);
-      if (st) return st;
-    }
-    if (!launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), nullptr, tl))
-      return fail(GICP_EINVAL, "unsupported k");
-    if (c->tie_exact) {
-      launch_nf_resolve_cov(c->stream, side.cloud->nf->dev(), cd, tl.list, tl.count, k, c->params.regularization,
-                            cv->cov6.as<double>(), side.cloud->nf->status.as<int>(), c->nf_err.as<int>());
-      gicp_status st = publish_ties(c, c->stream);
-      if (st) return st;
-    }
+  } else if (!launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), nullptr, tl)) {
+    return fail(GICP_EINVAL, "unsupported k");
+  }
+  if (c->tie_exact) {
+    launch_nf_resolve_cov(c->stream, side.cloud->nf->dev(), cd, tl.list, tl.count, k, c->params.regularization,
+                          cv->cov6.as<double>(), side.cloud->nf->status.as<int>(), c->nf_err.as<int>());
+    gicp_status st = publish_ties(c, c->stream);
+    if (st) return st;
   }
   HIP_TRY(hipGetLastError());
   side.cov = cv;

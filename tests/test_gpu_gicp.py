@@ -72,23 +72,28 @@ def test_covariances_ragged_sizes_vs_oracle(n, k):
 
 @pytest.mark.parametrize("k", [10, 20, 7, 32])
 def test_covariances_task_knn_matches(s2s_golden, k, monkeypatch):
-    """The opt-in task-based kNN (knn_tasks.hip, DDLO_COV_TASKS=1) is exact:
-    bit-identical covariances to the lane-per-query kernel, on the ray-cast
-    scan (dense near range, sparse far range: exercises the second round)
-    and on a sparse random cloud with exact ties (integer lattice)."""
+    """The opt-in task-based kNN (knn_tasks.hip, DDLO_COV_TASKS=1) and the
+    lane-per-query kernel both give the reference's covariances, on the
+    ray-cast scan (dense near range, sparse far range: exercises the second
+    round) and on a sparse random cloud with exact ties and duplicates
+    (integer lattice): nanoflann's neighbour set at every point, within
+    1e-12 x scale (the order among equidistant neighbours inside the set
+    only changes the double rounding)."""
     rng = np.random.default_rng(7)
     lattice = rng.integers(0, 40, size=(20000, 3)).astype(np.float32)
-    for cloud in (s2s_golden["src"], lattice):
-        out = []
+    for name, cloud in (("scan", s2s_golden["src"]), ("lattice", lattice)):
+        ref = O.covariances(cloud, k)
+        scale = max(np.abs(ref).max(), 1.0)
         for flag in ("0", "1"):
             monkeypatch.setenv("DDLO_COV_TASKS", flag)
             c = P.Context(0)
             c.set_params(P.default_params(k_correspondences=k))
             c.set_target(cloud)
             c.compute_covariances(TARGET)
-            out.append(c.get_covariances(TARGET))
+            got = c.get_covariances(TARGET)
             c.close()
-        np.testing.assert_array_equal(out[0], out[1])
+            bad = np.where(np.abs(got - ref).max(axis=1) > 1e-12 * scale)[0]
+            assert len(bad) == 0, f"{name} tasks={flag}: {len(bad)} rows differ, e.g. {bad[:8]}"
 
 
 def test_covariance_layouts_roundtrip(s2s_golden):

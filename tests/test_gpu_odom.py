@@ -65,6 +65,8 @@ def test_driver_vs_oracle(seq):
         g = gpu.process(f)
         o = ref.process(f)
         assert g.status == o["status"], i
+        if g.status == OD.INIT:   # initializeDDLO consumed the scan (odom.cc:641-646): nothing else is reported
+            continue
         assert g.scan_points == o["scan_points"], i
         assert g.keyframe_added == o["keyframe_added"], i
         assert abs(g.spaciousness - o["spaciousness"]) <= 1e-5 * o["spaciousness"], i
@@ -88,16 +90,16 @@ def test_driver_vs_oracle(seq):
 def test_driver_default_params_tracks_ground_truth(seq):
     frames, poses = seq
     gpu = OD.Odometry(0)        # cfg/ddlo.yaml parameters, adaptive keyframe threshold
-    T0inv = np.linalg.inv(poses[0])
+    T0inv = np.linalg.inv(poses[1])   # the first scan initialises; the second is the map origin
     statuses = []
-    for i, f in enumerate(frames[:8]):
+    for i, f in enumerate(frames[:9]):
         r = gpu.process(f)
         statuses.append(r.status)
         if r.status == OD.TRACKED:
             truth = T0inv @ poses[i]
             assert np.abs(r.pose()[:3, 3] - truth[:3, 3]).max() < 0.05
             assert r.keyframe_thresh_dist in (0.5, 1.0, 5.0, 10.0)
-    assert statuses == [OD.FIRST] + [OD.TRACKED] * 7
+    assert statuses == [OD.INIT, OD.FIRST] + [OD.TRACKED] * 7
     # the S2M context serves the residual image of the last scan (odom.cc:804-827)
     import ctypes as C
     ctx = C.c_void_p()
