@@ -478,7 +478,8 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   c->device = device;
   gicp_default_params(&c->params);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming));
   HIP_TRY(hipHostMalloc((void**)&c->job_host, sizeof(AlignJob), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&c->state_host, 2 * sizeof(AlignState), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&c->flag_host, sizeof(int) * 4, hipHostMallocDefault));
@@ -505,6 +506,7 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   if (std::getenv("DDLO_GRAPH_DEBUG")) std::fprintf(stderr, "[graphs] ctx %p: %ld chunk captures\n", (void*)c, c->captures);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->aux_stream);
   drop_graphs(c);
   if (c->comm) (void)rccl().comm_destroy(c->comm);
   for (auto e : c->prof_ev) (void)hipEventDestroy(e);
@@ -518,7 +520,9 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   c->src = Side();
   c->tgt = Side();
   (void)hipStreamDestroy(c->stream);
-  (void)hipStreamDestroy(c->copy_stream);
+  (void)hipStreamSynchronize(c->aux_stream);
+  (void)hipStreamDestroy(c->aux_stream);
+  (void)hipEventDestroy(c->aux_ev);
   delete c;
   return GICP_OK;
 }
@@ -914,7 +918,8 @@ gicp_status gicp_knn_target(gicp_ctx* c, const float* q, size_t nq, size_t strid
   if (!launch_knn_query(c->stream, c->tgt.cloud->dev(), c->raw_pts.as<float4>(), (int)nq, k, didx, dd, tl))
     return fail(GICP_EINVAL, "unsupported k");
   if (c->tie_exact) {
-    launch_nf_resolve_knn(c->stream, c->tgt.cloud->nf->dev(), c->raw_pts.as<float4>(), tl.list, tl.count, k, didx, dd,
+    HIP_TRY(nftree_join(*c->tgt.cloud->nf, c->stream));
+    launch_nf_resolve_knn(c->stream, c->tgt.cloud->nf->dev(), c->raw_pts.as<float4>(), tl, k, didx, dd,
                           c->tgt.cloud->nf->status.as<int>(), c->nf_err.as<int>());
     s = publish_ties(c, c->stream);
     if (s) return s;
@@ -942,6 +947,7 @@ gicp_status gicp_debug_nftree(gicp_ctx* c, int side, int32_t* vind, int32_t* nod
   s = ensure_nftree(c, *sd.cloud, c->stream);
   if (s) return s;
   const NfTreeData& t = *sd.cloud->nf;
+  HIP_TRY(nftree_join(t, c->stream));
   int st[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(st, t.status.p, sizeof(st), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -974,6 +980,7 @@ gicp_status gicp_debug_nfbuild(gicp_ctx* c, int side, int stop, int32_t* vind, i
   long long off[16];
   s = nftree_build(c, *sd.cloud, c->stream, t, stop, off);
   if (s) return s;
+  HIP_TRY(nftree_join(t, c->stream));
   for (int i = 0; i < 16; ++i) info16[i] = off[i];
   HIP_TRY(hipMemcpyAsync(status2, t.status.p, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
   std::vector<float4> v((size_t)t.n);
@@ -1022,7 +1029,7 @@ gicp_status gicp_synchronize(gicp_ctx* c) {
   gicp_status s = set_device(c);
   if (s) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipStreamSynchronize(c->copy_stream));
+  HIP_TRY(hipStreamSynchronize(c->aux_stream));
   return GICP_OK;
 }
 

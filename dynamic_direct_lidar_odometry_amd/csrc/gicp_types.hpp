@@ -176,14 +176,14 @@ struct NfNode {
 struct NfTreeDev {
   const float4* vpts;  // [n] points in vind order: x, y, z, original index (int bits)
   const NfNode* nodes; // node 0 = root
-  const float4* box;   // [2 * node + 0/1] the node's bounding box (lo / hi); node 0's = root_bbox
+  const float4* box;   // [2]: root_bbox (lo, hi), computeInitialDistances
   int n;
 };
 
 constexpr int kNfMaxLevels = 40;   // big levels of the device build (deeper: the build reports a failure)
 
 struct NfCtl {
-  int nnodes, nsmall, err;   // err bits: 1 node capacity, 2 node left too large, 4 depth, 8 list capacity
+  int nnodes, nsmall, err;   // err bits: 1 node capacity, 4 depth, 8 list capacity, 16/32 pairing checks
   int nchunks[2];
   int ntask[kNfMaxLevels + 1];
   int dbg[16];               // the first failed check's context (diagnostics)
@@ -203,7 +203,7 @@ struct NfTask {
 struct NfBuild {
   float4* vpts;            // [n] in: original order (x, y, z, index); out: vind order
   NfNode* nodes;
-  float4* box;             // [2 * cap]
+  float4* box;             // [2] root_bbox
   int cap;                 // node capacity
   NfCtl* ctl;
   NfTask* tasks;           // [(Lmax + 1) * max_task]
@@ -212,13 +212,14 @@ struct NfBuild {
   int* chunk_task;         // [2 * max_chunks]
   int *cA, *cAE, *cE2;     // [max_chunks] per-chunk counts
   float4 *tblL, *tblR;     // [n] rank tables of the Hoare pairing
-  int* arrive;             // [cap] refit arrival counters (zeroed)
   const float* quant;      // the cloud's bbox: min [0..2], max [4..6]
   int n, Lmax, max_task, max_pend, max_small, max_chunks;
+  int big_ids;             // node ids [0, big_ids) for the big levels; a small task of vind range
+                           // [b, b + c) numbers its subtree in [big_ids + 2b, big_ids + 2(b + c))
 };
 
 struct NfSizes {
-  int Lmax, max_task, max_pend, max_small, max_chunks;
+  int Lmax, max_task, max_pend, max_small, max_chunks, big_ids;
 };
 
 // Task-based kNN-k of a cloud's own points (covariances, knn_tasks.hip).
@@ -244,6 +245,7 @@ struct KnnJob {
   float split_extent;
   int* tie_list;                 // optional: sorted positions whose k-th distance is tied (nanoflann re-runs them)
   int* tie_count;
+  int tie_cap;
 };
 
 }  // namespace ddlo

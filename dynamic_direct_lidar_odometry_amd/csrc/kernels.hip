@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
     // a tie at the k-th distance changes the set; one inside the k changes the
     // summation order, which the eigen-decomposition of a degenerate
     // (isotropic) neighbourhood turns into a different regularized covariance
-    if (ties.list && (vis.outside_min() == vis.kth_dist() || vis.inner_tie())) ties.list[atomicAdd(ties.count, 1)] = i;
+    if (ties.list && (vis.outside_min() == vis.kth_dist() || vis.inner_tie())) ties.push(i);
     cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
   }
 }
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
     }
     vis.merge_halves();
     if (!vis.active || lane_id() >= 32) continue;
-    if (ties.list && (vis.td == vis.kth_dist() || vis.inner_tie())) ties.list[atomicAdd(ties.count, 1)] = i;
+    if (ties.list && (vis.td == vis.kth_dist() || vis.inner_tie())) ties.push(i);
     cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
   }
 }
@@ -566,7 +566,7 @@ __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __r
     const int leaf = min(pos, c.n - 1) / kLeafSize;
     knn_search(c, vis, leaf - 1, leaf + 1, L);
     if (!vis.active) continue;
-    if (ties.list && (vis.outside_min() == vis.kth_dist() || vis.inner_tie())) ties.list[atomicAdd(ties.count, 1)] = i;
+    if (ties.list && (vis.outside_min() == vis.kth_dist() || vis.inner_tie())) ties.push(i);
 #pragma unroll
     for (int s = 0; s < KCAP; ++s) {
       if (s < k) {

@@ -324,7 +324,10 @@ __global__ __launch_bounds__(256) void k_knn_select(KnnJob j) {
       if (!EXACT && s >= k && K[s] < out_min) out_min = K[s];
       if (s >= 1 && s < k) inner |= (K[s] >> 32) == (K[s - 1] >> 32);
     }
-    if (inner || (out_min != ~0ull && (out_min >> 32) == (kth >> 32))) j.tie_list[atomicAdd(j.tie_count, 1)] = i;
+    if (inner || (out_min != ~0ull && (out_min >> 32) == (kth >> 32))) {
+      const int slot = atomicAdd(j.tie_count, 1);
+      if (slot < j.tie_cap) j.tie_list[slot] = i;
+    }
   }
   // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
   double mx = 0, my = 0, mz = 0;

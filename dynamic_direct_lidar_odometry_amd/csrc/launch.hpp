@@ -25,6 +25,11 @@ void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int
 struct TieList {
   int* list;
   int* count;
+  int cap = 0;   // list capacity: an append beyond it is dropped and the resolver reports the overflow
+  __device__ __forceinline__ void push(int i) const {
+    const int slot = atomicAdd(count, 1);
+    if (slot < cap) list[slot] = i;
+  }
 };
 bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo,
                         TieList ties = TieList{nullptr, nullptr});
@@ -73,10 +78,10 @@ void launch_nf_export(hipStream_t s, const NfTreeDev& t, const int* status, int 
 // re-run the listed (tied) queries with nanoflann's search; status: the
 // tree build's error bits (nonzero: nothing resolved, *err |= 2); *err |= 1
 // on a failed search
-bool launch_nf_resolve_cov(hipStream_t s, const NfTreeDev& t, const CloudDev& c, const int* list, const int* count,
-                           int k, int method, double* cov6, const int* status, int* err);
-bool launch_nf_resolve_knn(hipStream_t s, const NfTreeDev& t, const float4* q, const int* list, const int* count, int k,
-                           int* out_idx, float* out_d, const int* status, int* err);
+bool launch_nf_resolve_cov(hipStream_t s, const NfTreeDev& t, const CloudDev& c, TieList ties, int k, int method,
+                           double* cov6, const int* status, int* err);
+bool launch_nf_resolve_knn(hipStream_t s, const NfTreeDev& t, const float4* q, TieList ties, int k, int* out_idx,
+                           float* out_d, const int* status, int* err);
 void launch_cov_remap(hipStream_t s, const double* old_cov6, const int* old_inv_perm, const int* new_perm, int n,
                       double* cov6);
 

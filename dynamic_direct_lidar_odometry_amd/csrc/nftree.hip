@@ -34,10 +34,13 @@ namespace ddlo {
 
 namespace {
 
-constexpr int kNfT = 4096;     // nodes up to this size are split by one wavefront in LDS
+constexpr int kNfT = 8192;     // nodes up to this size are split by one workgroup in LDS (k_nf_sub)
 constexpr int kNfCH = 2048;    // points per block in the big-level passes
 constexpr int kNfBT = 256;     // threads per big-level block (8 points each)
 constexpr int kNfPer = kNfCH / kNfBT;
+constexpr int kNfLevelMargin = 9;   // big levels beyond log2(n / kNfT): ray-cast scans need 5-7 of them
+constexpr int kNfSubWaves = 16;     // k_nf_sub: wavefronts per workgroup
+constexpr int kNfSubQ = 168;        // k_nf_sub: nodes per depth (<= 2 x kNfT / (kNfLeafMax + 1))
 
 __device__ __forceinline__ unsigned f2o(float f) {   // order-preserving float -> uint
   const unsigned u = __float_as_uint(f);
@@ -55,34 +58,57 @@ __device__ __forceinline__ float coord(const float4& p, int f) { return f == 0 ?
 __device__ __forceinline__ float coord_at(const float4* p, int f) { return reinterpret_cast<const float*>(p)[f]; }
 
 // middleSplit_ (:1045-1087): cut dimension and value from the passed-down
-// box and the node's point min / max (computeMinMax, :965-978)
-__device__ __forceinline__ void nf_cut(const NfTask& t, int* feat, float* cut) {
+// box (lo, hi) and the node's point min / max (computeMinMax, :965-978).
+// Constant indices only (registers, no private-memory arrays).
+__device__ __forceinline__ void nf_cut3(const float lo[3], const float hi[3], const float mn[3], const float mx[3],
+                                        int* feat, float* cut) {
   const float EPS = 0.00001f;
-  float max_span = t.hi[0] - t.lo[0];
+  float max_span = hi[0] - lo[0];
+#pragma unroll
   for (int i = 1; i < 3; ++i) {
-    const float span = t.hi[i] - t.lo[i];
+    const float span = hi[i] - lo[i];
     if (span > max_span) max_span = span;
   }
   float max_spread = -1;
   int cf = 0;
+#pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const float span = t.hi[i] - t.lo[i];
+    const float span = hi[i] - lo[i];
     if (span > (1 - EPS) * max_span) {
-      const float spread = o2f(t.mm[3 + i]) - o2f(t.mm[i]);
+      const float spread = mx[i] - mn[i];
       if (spread > max_spread) {
         cf = i;
         max_spread = spread;
       }
     }
   }
-  const float split_val = (t.lo[cf] + t.hi[cf]) / 2;
-  const float mn = o2f(t.mm[cf]), mx = o2f(t.mm[3 + cf]);
+  const float lc = cf == 0 ? lo[0] : (cf == 1 ? lo[1] : lo[2]);
+  const float hc = cf == 0 ? hi[0] : (cf == 1 ? hi[1] : hi[2]);
+  const float mnc = cf == 0 ? mn[0] : (cf == 1 ? mn[1] : mn[2]);
+  const float mxc = cf == 0 ? mx[0] : (cf == 1 ? mx[1] : mx[2]);
+  const float split_val = (lc + hc) / 2;
   float cv;
-  if (split_val < mn) cv = mn;
-  else if (split_val > mx) cv = mx;
+  if (split_val < mnc) cv = mnc;
+  else if (split_val > mxc) cv = mxc;
   else cv = split_val;
   *feat = cf;
   *cut = cv;
+}
+__device__ __forceinline__ void nf_cut(const NfTask& t, int* feat, float* cut) {
+  const float lo[3] = {t.lo[0], t.lo[1], t.lo[2]}, hi[3] = {t.hi[0], t.hi[1], t.hi[2]};
+  const float mn[3] = {o2f(t.mm[0]), o2f(t.mm[1]), o2f(t.mm[2])};
+  const float mx[3] = {o2f(t.mm[3]), o2f(t.mm[4]), o2f(t.mm[5])};
+  nf_cut3(lo, hi, mn, mx, feat, cut);
+}
+
+// divlow / divhigh of node p (:1032-1033): the max of its left child's points
+// along the cut dimension, the min of its right child's
+__device__ __forceinline__ void nf_set_div(NfNode* nodes, int child, const float mn[3], const float mx[3]) {
+  const int p = nodes[child].parent;
+  if (p < 0) return;
+  const int f = nodes[p].feat;
+  if (nodes[p].c1 == child) nodes[p].divlow = f == 0 ? mx[0] : (f == 1 ? mx[1] : mx[2]);
+  else nodes[p].divhigh = f == 0 ? mn[0] : (f == 1 ? mn[1] : mn[2]);
 }
 
 // :1090-1095
@@ -187,6 +213,8 @@ __global__ void k_nf_init(NfBuild b) {
     }
     b.pend[0] = r;
     b.nodes[0].parent = -1;
+    b.box[0] = make_float4(b.quant[0], b.quant[1], b.quant[2], 0.f);   // root_bbox
+    b.box[1] = make_float4(b.quant[4], b.quant[5], b.quant[6], 0.f);
   }
 }
 
@@ -240,6 +268,7 @@ __global__ __launch_bounds__(1024) void k_nf_map(NfBuild b, int L) {
   if (threadIdx.x == 0) {
     if (s_big > b.max_task || s_small0 + s_small > b.max_small || s_ch > b.max_chunks) atomicOr(&ctl->err, 8);
     ctl->ntask[L] = final ? 0 : nbig;
+    if (final) ctl->nnodes = b.cap;   // the small subtrees number their nodes in their own ranges
     ctl->nsmall = min(s_small0 + s_small, b.max_small);
     ctl->nchunks[L & 1] = final ? 0 : min(s_ch, b.max_chunks);
   }
@@ -293,6 +322,9 @@ __global__ __launch_bounds__(kNfBT) void k_nf_count(NfBuild b, int L) {
       NfTask* T = b.tasks + (size_t)L * b.max_task;
       T[v.t].feat = feat;
       T[v.t].cut = cut;
+      const float mn[3] = {o2f(v.tk.mm[0]), o2f(v.tk.mm[1]), o2f(v.tk.mm[2])};
+      const float mx[3] = {o2f(v.tk.mm[3]), o2f(v.tk.mm[4]), o2f(v.tk.mm[5])};
+      nf_set_div(b.nodes, v.tk.node, mn, mx);   // the children's min / max are final now
     }
   }
 }
@@ -397,6 +429,7 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(NfBuild b, int L) {
       }
     }
     NfTask* C = b.pend + (size_t)(L + 1) * b.max_pend;
+    __shared__ unsigned smm[kNfBT / 64][12];
     for (int s = 0; s < 2; ++s)
       for (int a = 0; a < 6; ++a) {
         float x = m[s][a];
@@ -404,16 +437,24 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(NfBuild b, int L) {
           const float o = __shfl_xor(x, d);
           x = a < 3 ? fminf(x, o) : fmaxf(x, o);
         }
-        if (__lane_id() == 0 && x == x && !isinf(x)) {
-          unsigned* dst = &C[2 * v.t + s].mm[a];
-          if (a < 3) atomicMin(dst, f2o(x));
-          else atomicMax(dst, f2o(x));
-        }
+        if (__lane_id() == 0) smm[threadIdx.x >> 6][6 * s + a] = f2o(x);
       }
+    __syncthreads();
+    if (threadIdx.x < 12) {   // one atomic per block and value
+      const int s = threadIdx.x / 6, a = threadIdx.x % 6;
+      unsigned u = smm[0][threadIdx.x];
+      for (int w = 1; w < kNfBT / 64; ++w) u = a < 3 ? min(u, smm[w][threadIdx.x]) : max(u, smm[w][threadIdx.x]);
+      const float x = o2f(u);
+      if (x == x && !isinf(x)) {
+        unsigned* dst = &C[2 * v.t + s].mm[a];
+        if (a < 3) atomicMin(dst, u);
+        else atomicMax(dst, u);
+      }
+    }
     if (v.c == 0 && threadIdx.x == 0) {
       NfCtl* ctl = b.ctl;
       const int c1 = atomicAdd(&ctl->nnodes, 2);
-      if (c1 + 2 > b.cap) {
+      if (c1 + 2 > b.big_ids) {
         atomicOr(&ctl->err, 1);
         return;
       }
@@ -440,15 +481,14 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(NfBuild b, int L) {
   }
 }
 
-// One wavefront per small node: its whole subtree, depth first, in LDS.  A
-// node the big levels left larger than kNfT (a very unbalanced cloud) is
-// split the same way in global memory (rank lists in the pairing tables).
-struct SmallLds {
-  float4 P[kNfT];
-  unsigned short ML[kNfT / 2], MR[kNfT / 2];
-  int sb[kNfStack], sc[kNfStack], sn[kNfStack];
-  float slo[3][kNfStack], shi[3][kNfStack];
-};
+// Small nodes (<= kNfT points): one workgroup per node, its whole subtree in
+// LDS, breadth first — all nodes of one depth at once, one wavefront per
+// node (k_nf_sub).  A node the big levels left larger than kNfT (a very
+// unbalanced cloud) is split depth first by one wavefront in global memory
+// (k_nf_small_global, rank lists in the pairing tables).  Node ids of a
+// subtree come from the task's own range (NfBuild::big_ids), and every node
+// writes its parent's divlow / divhigh from its own min / max, so no global
+// atomics and no bottom-up pass.
 
 __device__ __forceinline__ float wred(float x, bool mx) {
   for (int d = 32; d >= 1; d >>= 1) {
@@ -457,13 +497,19 @@ __device__ __forceinline__ float wred(float x, bool mx) {
   }
   return x;
 }
+// wave-scope ordering of LDS / memory between lanes (a node is one wavefront's)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // one Hoare pass over [zlo0, n) of the node at P (good = v < cut, or
 // v == cut for pass 2), boundary zhi: pair the r-th bad element of
-// [zlo0, zhi) with the r-th good element of [zhi, n) from the end
+// [zlo0, zhi) with the r-th good element of [zhi, n) from the end.
+// One wavefront; returns false on an (impossible) count mismatch.
 template <class IT>
-__device__ void small_pass(float4* P, IT* ML, IT* MR, int cap, int zlo0, int zhi, int n, int feat, float cut, bool pass2,
-                           NfCtl* ctl) {
+__device__ bool wave_pass(float4* P, IT* ML, IT* MR, int cap, int zlo0, int zhi, int n, int feat, float cut, bool pass2,
+                          NfCtl* ctl) {
   const int lane = __lane_id();
   int m = 0;
   for (int i0 = zlo0; i0 < zhi; i0 += 64) {
@@ -491,7 +537,7 @@ __device__ void small_pass(float4* P, IT* ML, IT* MR, int cap, int zlo0, int zhi
     if (f && slot < cap) MR[slot] = (IT)i;
     m2 += __popcll(mask);
   }
-  __syncthreads();
+  wave_sync();
   if (m != m2 || m > cap) {   // never (equal by construction): report, swap nothing
     if (lane == 0) {
       atomicOr(&ctl->err, 32);
@@ -501,216 +547,476 @@ __device__ void small_pass(float4* P, IT* ML, IT* MR, int cap, int zlo0, int zhi
         dbg[6] = pass2; dbg[7] = m; dbg[8] = m2; dbg[9] = cap; dbg[10] = (int)blockIdx.x;
       }
     }
-    return;
+    return false;
   }
-  const int mm = m;
-  for (int r = lane; r < mm; r += 64) {
+  for (int r = lane; r < m; r += 64) {
     const int a = ML[r], c = MR[r];
     const float4 t = P[a];
     P[a] = P[c];
     P[c] = t;
   }
-  __syncthreads();
+  wave_sync();
+  return true;
 }
 
-// divideTree below one node, depth first: P = the node's points (LDS, or
-// global for an oversized node), base = their vind offset
+// A node to split (or a leaf to record), as the subtree kernels queue it.
+struct NfSubNode {
+  int lb, n, node, par;   // first point (local), count, node id, parent id
+  float lo[3], hi[3];     // the box divideTree passes down
+};
+
+// One wavefront splits one node whose points are Q[0, n) (local offset lb
+// from the task's first point `base`): computeMinMax, the parent's div,
+// leaf or middleSplit_ + planeSplit + the children's entries.  Returns the
+// children through ch[2] (count 0 = a leaf was recorded).
 template <class IT>
-__device__ void small_tree(const NfBuild& b, SmallLds* S, float4* P, IT* ML, IT* MR, int mlcap, const NfTask& tk) {
+__device__ int wave_split(const NfBuild& b, float4* Q, IT* ML, IT* MR, int cap, const NfSubNode& nd, int base,
+                          int c1, NfSubNode ch[2]) {
   NfCtl* ctl = b.ctl;
   const int lane = __lane_id();
-  const int base = tk.begin;
+  const int n = nd.n;
+  // computeMinMax over the node (also the leaf's bbox, :998-1013)
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = lane; i < n; i += 64) {
+    const float4 p = Q[i];
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  for (int a = 0; a < 3; ++a) {
+    mn[a] = wred(mn[a], false);
+    mx[a] = wred(mx[a], true);
+  }
+  if (lane == 0 && nd.par >= 0) {   // the parent's divlow / divhigh (:1032-1033)
+    const int f = b.nodes[nd.par].feat;
+    if (b.nodes[nd.par].c1 == nd.node) b.nodes[nd.par].divlow = f == 0 ? mx[0] : (f == 1 ? mx[1] : mx[2]);
+    else b.nodes[nd.par].divhigh = f == 0 ? mn[0] : (f == 1 ? mn[1] : mn[2]);
+  }
+  if (n <= kNfLeafMax) {   // leaf (:992-1014)
+    if (lane == 0) {
+      b.nodes[nd.node].c1 = base + nd.lb;
+      b.nodes[nd.node].c2 = base + nd.lb + n;
+      b.nodes[nd.node].feat = -1;
+    }
+    return 0;
+  }
+  int feat;
+  float cut;
+  nf_cut3(nd.lo, nd.hi, mn, mx, &feat, &cut);
+  feat = __builtin_amdgcn_readfirstlane(feat);   // wave-uniform by construction: scalar from here on
+  cut = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cut)));
+  int lim1 = 0, lim2 = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const float x = i < n ? coord_at(&Q[i], feat) : INFINITY;
+    lim1 += __popcll(__ballot(i < n && x < cut));
+    lim2 += __popcll(__ballot(i < n && x <= cut));
+  }
+  if (!wave_pass(Q, ML, MR, cap, 0, lim1, n, feat, cut, false, ctl)) return -1;
+  if (!wave_pass(Q, ML, MR, cap, lim1, lim2, n, feat, cut, true, ctl)) return -1;
+  const int index = nf_index(n, lim1, lim2);
   if (lane == 0) {
-    S->sb[0] = 0;
-    S->sc[0] = tk.count;
-    S->sn[0] = tk.node;
+    b.nodes[nd.node].c1 = c1;
+    b.nodes[nd.node].c2 = c1 + 1;
+    b.nodes[nd.node].feat = feat;
+    b.nodes[c1].parent = nd.node;
+    b.nodes[c1 + 1].parent = nd.node;
+  }
+  // left_bbox / right_bbox (:1024-1030)
+  for (int s = 0; s < 2; ++s) {
+    ch[s].lb = nd.lb + (s == 0 ? 0 : index);
+    ch[s].n = s == 0 ? index : n - index;
+    ch[s].node = c1 + s;
+    ch[s].par = nd.node;
     for (int a = 0; a < 3; ++a) {
-      S->slo[a][0] = tk.lo[a];
-      S->shi[a][0] = tk.hi[a];
+      ch[s].lo[a] = nd.lo[a];
+      ch[s].hi[a] = nd.hi[a];
+    }
+  }
+  if (feat == 0) { ch[0].hi[0] = cut; ch[1].lo[0] = cut; }
+  else if (feat == 1) { ch[0].hi[1] = cut; ch[1].lo[1] = cut; }
+  else { ch[0].hi[2] = cut; ch[1].lo[2] = cut; }
+  return 2;
+}
+
+struct SubLds {
+  float4 P[kNfT];
+  unsigned short ML[kNfT / 2], MR[kNfT / 2];   // per node: the slots [lb / 2, (lb + n) / 2)
+  NfSubNode q[2][kNfSubQ];
+  int qn[2], next_id, pad;
+  // a depth of few nodes is split by groups of wavefronts (group_depth)
+  float gred[kNfSubWaves][6];
+  int gcnt[kNfSubWaves][2];
+  int gfeat[kNfSubWaves], gleaf[kNfSubWaves];
+  float gcut[kNfSubWaves];
+};
+
+// One Hoare pass of a node by a group of G wavefronts (gw = this one's
+// index), every wavefront of the workgroup in lockstep (barriers inside; a
+// wavefront without a node passes act = false).  The zone [zlo0, zhi) is
+// cut into 64-position chunks from its start, the rest [zhi, n) from its
+// end; chunk counts (kept in `cnt`, 256 slots of this group's, the ML
+// space: they are read into registers before ML is written) give every
+// chunk its first rank slot.
+__device__ void group_pass(float4* Q, unsigned short* ML, unsigned short* MR, unsigned short* cnt, bool act, int gw,
+                           int G, int zlo0, int zhi, int n, int feat, float cut, bool pass2, NfCtl* ctl) {
+  const int lane = __lane_id();
+  const int nz = act ? (zhi - zlo0 + 63) / 64 : 0;   // zone chunks, ascending
+  const int nr = act ? (n - zhi + 63) / 64 : 0;       // right chunks, descending from n
+  for (int z = gw; z < nz; z += G) {
+    const int i = zlo0 + 64 * z + lane;
+    bool f = false;
+    if (i < zhi) {
+      const float x = coord_at(&Q[i], feat);
+      f = !(pass2 ? x == cut : x < cut);
+    }
+    const int c = __popcll(__ballot(f));
+    if (lane == 0) cnt[z] = (unsigned short)c;
+  }
+  for (int r = gw; r < nr; r += G) {
+    const int i = n - 1 - 64 * r - lane;
+    bool f = false;
+    if (i >= zhi) {
+      const float x = coord_at(&Q[i], feat);
+      f = pass2 ? x == cut : x < cut;
+    }
+    const int c = __popcll(__ballot(f));
+    if (lane == 0) cnt[128 + r] = (unsigned short)c;
+  }
+  __syncthreads();
+  // exclusive chunk prefixes (<= 128 chunks each: two per lane)
+  const int a0 = lane < nz ? cnt[lane] : 0, a1 = lane + 64 < nz ? cnt[lane + 64] : 0;
+  const int b0 = lane < nr ? cnt[128 + lane] : 0, b1 = lane + 64 < nr ? cnt[128 + lane + 64] : 0;
+  const int sa0 = wave_incl_scan(a0), ta = __builtin_amdgcn_readlane(sa0, 63);
+  const int sa1 = wave_incl_scan(a1) + ta;
+  const int sb0 = wave_incl_scan(b0), tb = __builtin_amdgcn_readlane(sb0, 63);
+  const int sb1 = wave_incl_scan(b1) + tb;
+  const int ea0 = sa0 - a0, ea1 = sa1 - a1, eb0 = sb0 - b0, eb1 = sb1 - b1;
+  const int m = __builtin_amdgcn_readlane(sa1, 63), m2 = __builtin_amdgcn_readlane(sb1, 63);
+  __syncthreads();   // the counts are in registers: ML may be written
+  const bool ok = m == m2;
+  if (act && !ok && gw == 0 && lane == 0) atomicOr(&ctl->err, 32);
+  if (act && ok) {
+    for (int z = gw; z < nz; z += G) {
+      const int i = zlo0 + 64 * z + lane;
+      bool f = false;
+      if (i < zhi) {
+        const float x = coord_at(&Q[i], feat);
+        f = !(pass2 ? x == cut : x < cut);
+      }
+      const unsigned long long mask = __ballot(f);
+      const int off = __builtin_amdgcn_readlane(z < 64 ? ea0 : ea1, z & 63);
+      const int slot = off + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+      if (f) ML[slot] = (unsigned short)i;
+    }
+    for (int r = gw; r < nr; r += G) {
+      const int i = n - 1 - 64 * r - lane;
+      bool f = false;
+      if (i >= zhi) {
+        const float x = coord_at(&Q[i], feat);
+        f = pass2 ? x == cut : x < cut;
+      }
+      const unsigned long long mask = __ballot(f);
+      const int off = __builtin_amdgcn_readlane(r < 64 ? eb0 : eb1, r & 63);
+      const int slot = off + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+      if (f) MR[slot] = (unsigned short)i;
     }
   }
   __syncthreads();
+  if (act && ok) {
+    for (int rr = gw * 64 + lane; rr < m; rr += 64 * G) {
+      const int a = ML[rr], c = MR[rr];
+      const float4 t = Q[a];
+      Q[a] = Q[c];
+      Q[c] = t;
+    }
+  }
+  __syncthreads();
+}
+
+// A depth of nq <= kNfSubWaves / 2 nodes: node j by the G = kNfSubWaves /
+// pow2(nq) wavefronts [j G, (j + 1) G); the same steps as wave_split.
+__device__ void group_depth(const NfBuild& b, SubLds& S, int cur, int nq, int base, int id_end) {
+  const int lane = __lane_id(), wave = threadIdx.x >> 6;
+  int p2 = 1;
+  while (p2 < nq) p2 <<= 1;
+  const int G = kNfSubWaves / p2;
+  const int j = wave / G, gw = wave % G;
+  const bool has = j < nq;
+  NfSubNode nd;
+  if (has) nd = S.q[cur][j];
+  else {
+    nd.lb = 0;
+    nd.n = 0;
+  }
+  float4* Q = S.P + nd.lb;
+  // computeMinMax (:965-978, leaf bbox :998-1013)
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = gw * 64 + lane; i < nd.n; i += 64 * G) {
+    const float4 p = Q[i];
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  for (int a = 0; a < 3; ++a) {
+    mn[a] = wred(mn[a], false);
+    mx[a] = wred(mx[a], true);
+  }
+  if (lane == 0)
+    for (int a = 0; a < 3; ++a) {
+      S.gred[wave][a] = mn[a];
+      S.gred[wave][3 + a] = mx[a];
+    }
+  __syncthreads();
+  if (has && gw == 0 && lane == 0) {
+    for (int g = 1; g < G; ++g)
+      for (int a = 0; a < 3; ++a) {
+        mn[a] = fminf(mn[a], S.gred[wave + g][a]);
+        mx[a] = fmaxf(mx[a], S.gred[wave + g][3 + a]);
+      }
+    if (nd.par >= 0) {   // the parent's divlow / divhigh (:1032-1033)
+      const int f = b.nodes[nd.par].feat;
+      if (b.nodes[nd.par].c1 == nd.node) b.nodes[nd.par].divlow = f == 0 ? mx[0] : (f == 1 ? mx[1] : mx[2]);
+      else b.nodes[nd.par].divhigh = f == 0 ? mn[0] : (f == 1 ? mn[1] : mn[2]);
+    }
+    if (nd.n <= kNfLeafMax) {   // leaf (:992-1014)
+      b.nodes[nd.node].c1 = base + nd.lb;
+      b.nodes[nd.node].c2 = base + nd.lb + nd.n;
+      b.nodes[nd.node].feat = -1;
+      S.gleaf[j] = 1;
+    } else {
+      int feat;
+      float cut;
+      nf_cut3(nd.lo, nd.hi, mn, mx, &feat, &cut);
+      S.gfeat[j] = feat;
+      S.gcut[j] = cut;
+      S.gleaf[j] = 0;
+    }
+  }
+  __syncthreads();
+  const bool act = has && !S.gleaf[j];
+  const int feat = act ? S.gfeat[j] : 0;
+  const float cut = act ? S.gcut[j] : 0.f;
+  int c_lt = 0, c_le = 0;
+  for (int i0 = gw * 64; act && i0 < nd.n; i0 += 64 * G) {
+    const int i = i0 + lane;
+    const float x = i < nd.n ? coord_at(&Q[i], feat) : INFINITY;
+    c_lt += __popcll(__ballot(i < nd.n && x < cut));
+    c_le += __popcll(__ballot(i < nd.n && x <= cut));
+  }
+  if (lane == 0) {
+    S.gcnt[wave][0] = c_lt;
+    S.gcnt[wave][1] = c_le;
+  }
+  __syncthreads();
+  int lim1 = 0, lim2 = 0;
+  if (has)
+    for (int g = 0; g < G; ++g) {
+      lim1 += S.gcnt[j * G + g][0];
+      lim2 += S.gcnt[j * G + g][1];
+    }
+  unsigned short* cnt = S.ML + 256 * (has ? j : 0);
+  group_pass(Q, S.ML + nd.lb / 2, S.MR + nd.lb / 2, cnt, act, gw, G, 0, lim1, nd.n, feat, cut, false, b.ctl);
+  group_pass(Q, S.ML + nd.lb / 2, S.MR + nd.lb / 2, cnt, act, gw, G, lim1, lim2, nd.n, feat, cut, true, b.ctl);
+  if (act && gw == 0 && lane == 0) {
+    const int index = nf_index(nd.n, lim1, lim2);
+    const int c1 = atomicAdd(&S.next_id, 2);
+    if (c1 + 2 > id_end) {
+      atomicOr(&b.ctl->err, 1);
+    } else {
+      b.nodes[nd.node].c1 = c1;
+      b.nodes[nd.node].c2 = c1 + 1;
+      b.nodes[nd.node].feat = feat;
+      b.nodes[c1].parent = nd.node;
+      b.nodes[c1 + 1].parent = nd.node;
+      NfSubNode ch[2];
+      for (int s2 = 0; s2 < 2; ++s2) {   // left_bbox / right_bbox (:1024-1030)
+        ch[s2].lb = nd.lb + (s2 == 0 ? 0 : index);
+        ch[s2].n = s2 == 0 ? index : nd.n - index;
+        ch[s2].node = c1 + s2;
+        ch[s2].par = nd.node;
+        for (int a = 0; a < 3; ++a) {
+          ch[s2].lo[a] = nd.lo[a];
+          ch[s2].hi[a] = nd.hi[a];
+        }
+      }
+      if (feat == 0) { ch[0].hi[0] = cut; ch[1].lo[0] = cut; }
+      else if (feat == 1) { ch[0].hi[1] = cut; ch[1].lo[1] = cut; }
+      else { ch[0].hi[2] = cut; ch[1].lo[2] = cut; }
+      const int slot = atomicAdd(&S.qn[cur ^ 1], 2);
+      if (slot + 2 <= kNfSubQ) {
+        S.q[cur ^ 1][slot] = ch[0];
+        S.q[cur ^ 1][slot + 1] = ch[1];
+      } else {
+        atomicOr(&b.ctl->err, 4);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * kNfSubWaves) void k_nf_sub(NfBuild b) {
+  __shared__ SubLds S;   // ~157 KB: one workgroup per CU
+  if ((int)blockIdx.x >= b.ctl->nsmall) return;
+  const NfTask tk = b.small[blockIdx.x];
+  if (tk.count > kNfT) return;   // k_nf_small_global's
+  const int lane = __lane_id(), wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < tk.count; i += blockDim.x) S.P[i] = b.vpts[tk.begin + i];
+  if (threadIdx.x == 0) {
+    NfSubNode r;
+    r.lb = 0;
+    r.n = tk.count;
+    r.node = tk.node;
+    r.par = b.nodes[tk.node].parent;
+    for (int a = 0; a < 3; ++a) {
+      r.lo[a] = tk.lo[a];
+      r.hi[a] = tk.hi[a];
+    }
+    S.q[0][0] = r;
+    S.qn[0] = 1;
+    S.qn[1] = 0;
+    S.next_id = b.big_ids + 2 * tk.begin;   // this subtree's ids: [big_ids + 2 begin, big_ids + 2 (begin + count))
+  }
+  __syncthreads();
+  const int id_end = b.big_ids + 2 * (tk.begin + tk.count);
+  for (int depth = 0, cur = 0; depth < kNfStack; ++depth, cur ^= 1) {
+    const int nq = S.qn[cur];
+    if (nq == 0) break;
+    if (nq <= kNfSubWaves / 2) {
+      group_depth(b, S, cur, nq, tk.begin, id_end);
+    } else for (int j = wave; j < nq; j += kNfSubWaves) {
+      const NfSubNode nd = S.q[cur][j];
+      int c1 = 0;
+      if (nd.n > kNfLeafMax) {
+        if (lane == 0) c1 = atomicAdd(&S.next_id, 2);
+        c1 = __builtin_amdgcn_readfirstlane(c1);
+        if (c1 + 2 > id_end) {
+          if (lane == 0) atomicOr(&b.ctl->err, 1);
+          continue;
+        }
+      }
+      NfSubNode ch[2];
+      const int nc = wave_split(b, S.P + nd.lb, S.ML + nd.lb / 2, S.MR + nd.lb / 2, nd.n / 2, nd, tk.begin, c1, ch);
+      if (nc == 2 && lane == 0) {
+        const int slot = atomicAdd(&S.qn[cur ^ 1], 2);
+        if (slot + 2 <= kNfSubQ) {
+          S.q[cur ^ 1][slot] = ch[0];
+          S.q[cur ^ 1][slot + 1] = ch[1];
+        } else {
+          atomicOr(&b.ctl->err, 4);
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      S.qn[cur] = 0;
+      if (S.qn[cur ^ 1] > kNfSubQ) S.qn[cur ^ 1] = kNfSubQ;
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < tk.count; i += blockDim.x) b.vpts[tk.begin + i] = S.P[i];
+}
+
+// a task larger than kNfT: depth first by one wavefront, in global memory
+struct NfGStack {
+  NfSubNode e[kNfStack];
+};
+__global__ __launch_bounds__(64) void k_nf_small_global(NfBuild b) {
+  __shared__ NfGStack S;
+  if ((int)blockIdx.x >= b.ctl->nsmall) return;
+  const NfTask tk = b.small[blockIdx.x];
+  if (tk.count <= kNfT) return;   // k_nf_sub's
+  const int lane = __lane_id();
+  float4* P = b.vpts + tk.begin;
+  unsigned* ML = reinterpret_cast<unsigned*>(b.tblL + tk.begin);   // the pairing tables' space: slots [lb / 2, ...)
+  unsigned* MR = reinterpret_cast<unsigned*>(b.tblR + tk.begin);
+  int next_id = b.big_ids + 2 * tk.begin;
+  const int id_end = b.big_ids + 2 * (tk.begin + tk.count);
+  if (lane == 0) {
+    NfSubNode r;
+    r.lb = 0;
+    r.n = tk.count;
+    r.node = tk.node;
+    r.par = b.nodes[tk.node].parent;
+    for (int a = 0; a < 3; ++a) {
+      r.lo[a] = tk.lo[a];
+      r.hi[a] = tk.hi[a];
+    }
+    S.e[0] = r;
+  }
+  wave_sync();
   int sp = 1;
   while (sp > 0) {
     --sp;
-    const int lb = S->sb[sp], n = S->sc[sp], node = S->sn[sp];
-    NfTask t;
-    for (int a = 0; a < 3; ++a) {
-      t.lo[a] = S->slo[a][sp];
-      t.hi[a] = S->shi[a][sp];
-    }
-    __syncthreads();
-    float4* Q = P + lb;
-    // computeMinMax over the node (also the leaf's bbox, :998-1013)
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = lane; i < n; i += 64) {
-      const float4 p = Q[i];
-      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-    }
-    for (int a = 0; a < 3; ++a) {
-      mn[a] = wred(mn[a], false);
-      mx[a] = wred(mx[a], true);
-    }
-    if (n <= kNfLeafMax) {   // leaf (:992-1014)
-      if (lane == 0) {
-        b.nodes[node].c1 = base + lb;
-        b.nodes[node].c2 = base + lb + n;
-        b.nodes[node].feat = -1;
-        b.box[2 * node] = make_float4(mn[0], mn[1], mn[2], 0.f);
-        b.box[2 * node + 1] = make_float4(mx[0], mx[1], mx[2], 0.f);
-      }
-      continue;
-    }
-    for (int a = 0; a < 3; ++a) {
-      t.mm[a] = f2o(mn[a]);
-      t.mm[3 + a] = f2o(mx[a]);
-    }
-    int feat;
-    float cut;
-    nf_cut(t, &feat, &cut);
-    feat = __builtin_amdgcn_readfirstlane(feat);   // wave-uniform by construction: scalar from here on
-    cut = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cut)));
-    int lim1 = 0, lim2 = 0;
-    for (int i0 = 0; i0 < n; i0 += 64) {
-      const int i = i0 + lane;
-      const float x = i < n ? coord_at(&Q[i], feat) : INFINITY;
-      lim1 += __popcll(__ballot(i < n && x < cut));
-      lim2 += __popcll(__ballot(i < n && x <= cut));
-    }
-    small_pass(Q, ML, MR, mlcap, 0, lim1, n, feat, cut, false, ctl);
-    small_pass(Q, ML, MR, mlcap, lim1, lim2, n, feat, cut, true, ctl);
-    const int index = nf_index(n, lim1, lim2);
+    const NfSubNode nd = S.e[sp];
+    wave_sync();
     int c1 = 0;
-    if (lane == 0) c1 = atomicAdd(&ctl->nnodes, 2);
-    c1 = __builtin_amdgcn_readfirstlane(c1);
-    if (c1 + 2 > b.cap || sp + 2 > kNfStack) {
-      if (lane == 0) atomicOr(&ctl->err, c1 + 2 > b.cap ? 1 : 4);
-      return;
-    }
-    if (lane == 0) {
-      b.nodes[node].c1 = c1;
-      b.nodes[node].c2 = c1 + 1;
-      b.nodes[node].feat = feat;
-      b.nodes[c1].parent = node;
-      b.nodes[c1 + 1].parent = node;
-      // left_bbox / right_bbox (:1024-1030); the left child is popped first
-      for (int s = 1; s >= 0; --s) {
-        const int k = sp + (1 - s);
-        S->sb[k] = lb + (s == 0 ? 0 : index);
-        S->sc[k] = s == 0 ? index : n - index;
-        S->sn[k] = c1 + s;
-        for (int a = 0; a < 3; ++a) {
-          S->slo[a][k] = t.lo[a];
-          S->shi[a][k] = t.hi[a];
-        }
-        if (s == 0) S->shi[feat][k] = cut;
-        else S->slo[feat][k] = cut;
+    if (nd.n > kNfLeafMax) {
+      c1 = next_id;
+      next_id += 2;
+      if (c1 + 2 > id_end || sp + 2 > kNfStack) {
+        if (lane == 0) atomicOr(&b.ctl->err, c1 + 2 > id_end ? 1 : 4);
+        return;
       }
     }
-    sp += 2;
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(64) void k_nf_small(NfBuild b) {
-  __shared__ SmallLds S_lds;   // static (~79 KB: gfx950 gives one workgroup up to 160 KB)
-  SmallLds* S = &S_lds;
-  if ((int)blockIdx.x >= b.ctl->nsmall) return;
-  const NfTask tk = b.small[blockIdx.x];
-  const int lane = __lane_id();
-  if (tk.count <= kNfT) {
-    for (int i = lane; i < tk.count; i += 64) S->P[i] = b.vpts[tk.begin + i];
-    __syncthreads();
-    small_tree<unsigned short>(b, S, S->P, S->ML, S->MR, kNfT / 2, tk);
-    __syncthreads();
-    for (int i = lane; i < tk.count; i += 64) b.vpts[tk.begin + i] = S->P[i];
-  } else {   // in place in global memory; the rank lists use the pairing tables' space
-    small_tree<unsigned>(b, S, b.vpts + tk.begin, reinterpret_cast<unsigned*>(b.tblL + tk.begin),
-                         reinterpret_cast<unsigned*>(b.tblR + tk.begin), tk.count, tk);
-  }
-}
-
-// Bottom-up boxes: one thread per leaf walks to the root; the second child
-// to arrive at a node computes the node (device-scope ordering, no waiting).
-__device__ __forceinline__ float4 ld_box(const float4* p) {
-  const unsigned* u = reinterpret_cast<const unsigned*>(p);
-  float4 r;
-  r.x = __uint_as_float(__hip_atomic_load(u + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  r.y = __uint_as_float(__hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  r.z = __uint_as_float(__hip_atomic_load(u + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  r.w = 0.f;
-  return r;
-}
-__device__ __forceinline__ void st_box(float4* p, float4 v) {
-  unsigned* u = reinterpret_cast<unsigned*>(p);
-  __hip_atomic_store(u + 0, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(u + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(u + 2, __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(256) void k_nf_refit(NfBuild b) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nn = min(b.ctl->nnodes, b.cap);
-  if (i >= nn || b.ctl->err) return;
-  if (b.nodes[i].feat != -1) return;
-  int cur = i;
-  for (int step = 0; step < kNfMaxLevels + kNfStack + 8; ++step) {   // bounded: a tree is never deeper
-    const int p = b.nodes[cur].parent;
-    if (p < 0) break;
-    __threadfence();
-    if (atomicAdd(&b.arrive[p], 1) == 0) break;   // the sibling's thread finishes the node
-    __threadfence();
-    const NfNode nd = b.nodes[p];
-    const float4 l1 = ld_box(&b.box[2 * nd.c1]), h1 = ld_box(&b.box[2 * nd.c1 + 1]);
-    const float4 l2 = ld_box(&b.box[2 * nd.c2]), h2 = ld_box(&b.box[2 * nd.c2 + 1]);
-    // bbox = (std::min / std::max of the children's boxes) (:1035-1039)
-    const float4 lo = make_float4(l2.x < l1.x ? l2.x : l1.x, l2.y < l1.y ? l2.y : l1.y, l2.z < l1.z ? l2.z : l1.z, 0.f);
-    const float4 hi = make_float4(h1.x < h2.x ? h2.x : h1.x, h1.y < h2.y ? h2.y : h1.y, h1.z < h2.z ? h2.z : h1.z, 0.f);
-    st_box(&b.box[2 * p], lo);
-    st_box(&b.box[2 * p + 1], hi);
-    b.nodes[p].divlow = coord(h1, nd.feat);    // left_bbox[cutfeat].high
-    b.nodes[p].divhigh = coord(l2, nd.feat);   // right_bbox[cutfeat].low
-    cur = p;
+    NfSubNode ch[2];
+    const int nc = wave_split(b, P + nd.lb, ML + nd.lb / 2, MR + nd.lb / 2, nd.n / 2, nd, tk.begin, c1, ch);
+    if (nc < 0) return;
+    if (nc == 2) {
+      if (lane == 0) {   // the left child is popped first
+        S.e[sp] = ch[1];
+        S.e[sp + 1] = ch[0];
+      }
+      sp += 2;
+      wave_sync();
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
-// tie resolution: re-run the flagged queries with nanoflann's search
-template <int KMAX>
-__global__ __launch_bounds__(64) void k_nf_resolve_cov(NfTreeDev t, CloudDev c, const int* __restrict__ list,
-                                                       const int* __restrict__ count, int k, int method,
-                                                       double* __restrict__ cov6, const int* __restrict__ status,
-                                                       int* __restrict__ err) {
-  const int nl = *count;
+// tie resolution: re-run the flagged queries with nanoflann's search, one
+// wavefront per query (nf_search_wave)
+constexpr int kNfResolveWaves = 4;
+
+__global__ __launch_bounds__(64 * kNfResolveWaves) void k_nf_resolve_cov(NfTreeDev t, CloudDev c, TieList ties, int k,
+                                                                        int method, double* __restrict__ cov6,
+                                                                        const int* __restrict__ status,
+                                                                        int* __restrict__ err) {
+  __shared__ NfWaveStack stk[kNfResolveWaves];
+  NfWaveStack* S = &stk[threadIdx.x >> 6];
+  const int lane = __lane_id();
+  const int nc = *ties.count;
+  const int nl = min(nc, ties.cap);
+  if (nc > ties.cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 8);   // list overflow (never: cap = 2n)
+  const int* list = ties.list;
   if (*status) {   // the tree build failed: report, keep the Morton-order answers
-    if (blockIdx.x == 0 && threadIdx.x == 0 && nl > 0) atomicOr(err, 2);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nl > 0) atomicOr(err, 2 | (*status << 8));
     return;
   }
-  for (int li = blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += gridDim.x * blockDim.x) {
-    const int s = list[li];              // sorted position of the query point
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int li = wave; li < nl; li += nwaves) {
+    const int s = list[li];   // sorted position of the query point
     const float4 q = c.pts[s];
-    NfResult<KMAX> rs;
-    rs.init(k);
-    if (!nf_search<KMAX>(t, q.x, q.y, q.z, rs) || rs.count < k) {
-      atomicOr(err, 1);
+    float rd;
+    int rix;
+    if (!nf_search_wave(t, q.x, q.y, q.z, k, S, &rd, &rix)) {   // 1: deeper than kNfStack, 4: fewer than k
+      if (lane == 0) atomicOr(err, rix == -2 ? 1 : 4);
       continue;
     }
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane < k) p = c.pts[c.inv_perm[rix]];
     // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
     double mx = 0, my = 0, mz = 0;
     for (int j = 0; j < k; ++j) {
-      const float4 p = c.pts[c.inv_perm[rs.ix[j]]];
-      mx += (double)p.x;
-      my += (double)p.y;
-      mz += (double)p.z;
+      mx += (double)__shfl(p.x, j);
+      my += (double)__shfl(p.y, j);
+      mz += (double)__shfl(p.z, j);
     }
     mx /= k;
     my /= k;
     mz /= k;
     double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < k; ++j) {
-      const float4 p = c.pts[c.inv_perm[rs.ix[j]]];
-      const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
+      const double d0 = (double)__shfl(p.x, j) - mx, d1 = (double)__shfl(p.y, j) - my,
+                   d2 = (double)__shfl(p.z, j) - mz;
       C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
       C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
       C[6] += d2 * d0; C[7] += d2 * d1; C[8] += d2 * d2;
@@ -718,33 +1024,44 @@ __global__ __launch_bounds__(64) void k_nf_resolve_cov(NfTreeDev t, CloudDev c, 
     for (int e = 0; e < 9; ++e) C[e] /= k;
     double out[6];
     regularize(C, method, out);
-    double* o = cov6 + 6 * (size_t)s;
-    for (int e = 0; e < 6; ++e) o[e] = out[e];
+    if (lane == 0) {
+      double* o = cov6 + 6 * (size_t)s;
+      for (int e = 0; e < 6; ++e) o[e] = out[e];
+    }
   }
 }
 
-template <int KMAX>
-__global__ __launch_bounds__(64) void k_nf_resolve_knn(NfTreeDev t, const float4* __restrict__ q,
-                                                       const int* __restrict__ list, const int* __restrict__ count,
-                                                       int k, int* __restrict__ out_idx, float* __restrict__ out_d,
-                                                       const int* __restrict__ status, int* __restrict__ err) {
-  const int nl = *count;
+__global__ __launch_bounds__(64 * kNfResolveWaves) void k_nf_resolve_knn(NfTreeDev t, const float4* __restrict__ q,
+                                                                        TieList ties, int k,
+                                                                        int* __restrict__ out_idx,
+                                                                        float* __restrict__ out_d,
+                                                                        const int* __restrict__ status,
+                                                                        int* __restrict__ err) {
+  __shared__ NfWaveStack stk[kNfResolveWaves];
+  NfWaveStack* S = &stk[threadIdx.x >> 6];
+  const int lane = __lane_id();
+  const int nc = *ties.count;
+  const int nl = min(nc, ties.cap);
+  if (nc > ties.cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 8);   // list overflow (never: cap = 2n)
+  const int* list = ties.list;
   if (*status) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && nl > 0) atomicOr(err, 2);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nl > 0) atomicOr(err, 2 | (*status << 8));
     return;
   }
-  for (int li = blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += gridDim.x * blockDim.x) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int li = wave; li < nl; li += nwaves) {
     const int i = list[li];   // query row
     const float4 p = q[i];
-    NfResult<KMAX> rs;
-    rs.init(k);
-    if (!nf_search<KMAX>(t, p.x, p.y, p.z, rs) || rs.count < k) {
-      atomicOr(err, 1);
+    float rd;
+    int rix;
+    if (!nf_search_wave(t, p.x, p.y, p.z, k, S, &rd, &rix)) {
+      if (lane == 0) atomicOr(err, rix == -2 ? 1 : 4);
       continue;
     }
-    for (int j = 0; j < k; ++j) {
-      out_idx[(size_t)i * k + j] = rs.ix[j];
-      out_d[(size_t)i * k + j] = rs.d[j];
+    if (lane < k) {
+      out_idx[(size_t)i * k + lane] = rix;
+      out_d[(size_t)i * k + lane] = rd;
     }
   }
 }
@@ -781,19 +1098,19 @@ static inline int cdivl(long a, long b) { return (int)((a + b - 1) / b); }
 NfSizes nf_sizes(int n) {
   NfSizes z;
   z.Lmax = 0;
-  if (n > kNfT) {
-    int l = 0;
-    while ((long)kNfT << l < n) ++l;
-    z.Lmax = std::min(l + 2, kNfMaxLevels);
+  if (n > kNfT) {   // levels until halving nodes are <= kNfT, plus margin: middleSplit_ cuts the box, not
+    int l = 0;      // the points, so clustered clouds split unevenly (a node still larger after the last
+    while ((long)kNfT << l < n) ++l;   // level is split by the small kernel in global memory, slowly)
+    z.Lmax = std::min(l + kNfLevelMargin, kNfMaxLevels);
   }
   z.max_task = n / kNfT + 2;
   z.max_pend = 2 * z.max_task;
   z.max_small = 2 * (z.Lmax + 1) * z.max_task + 2;
   z.max_chunks = cdivl(n, kNfCH) + z.max_task;
+  z.big_ids = 2 * (z.Lmax + 1) * z.max_task + 2;   // the root and two children per big task
   return z;
 }
 
-size_t nf_small_lds_bytes() { return sizeof(SmallLds); }
 
 void launch_nf_build(hipStream_t s, const NfBuild& b, const float4* sorted_pts, int stop) {
   k_nf_unsort<<<cdivl(b.n, 256), 256, 0, s>>>(sorted_pts, b.n, b.vpts);
@@ -809,31 +1126,25 @@ void launch_nf_build(hipStream_t s, const NfBuild& b, const float4* sorted_pts, 
     k_nf_pass<2, false><<<G, kNfBT, 0, s>>>(b, L);
   }
   k_nf_map<<<1, 1024, 0, s>>>(b, b.Lmax);
-  k_nf_small<<<b.max_small, 64, 0, s>>>(b);
-  k_nf_refit<<<cdivl(b.cap, 256), 256, 0, s>>>(b);
+  k_nf_sub<<<b.max_small, 64 * kNfSubWaves, 0, s>>>(b);
+  k_nf_small_global<<<b.max_small, 64, 0, s>>>(b);
 }
 
 void launch_nf_export(hipStream_t s, const NfTreeDev& t, const int* status, int cap, int* vind, int* nodes, float* f) {
   k_nf_export<<<cdivl(std::max(t.n, cap), 256), 256, 0, s>>>(t, status, cap, vind, nodes, f);
 }
 
-bool launch_nf_resolve_cov(hipStream_t s, const NfTreeDev& t, const CloudDev& c, const int* list, const int* count,
-                           int k, int method, double* cov6, const int* status, int* err) {
-  const int nb = 64;
-  if (k <= 16) k_nf_resolve_cov<16><<<nb, 64, 0, s>>>(t, c, list, count, k, method, cov6, status, err);
-  else if (k <= 32) k_nf_resolve_cov<32><<<nb, 64, 0, s>>>(t, c, list, count, k, method, cov6, status, err);
-  else if (k <= 64) k_nf_resolve_cov<64><<<nb, 64, 0, s>>>(t, c, list, count, k, method, cov6, status, err);
-  else return false;
+bool launch_nf_resolve_cov(hipStream_t s, const NfTreeDev& t, const CloudDev& c, TieList ties, int k, int method,
+                           double* cov6, const int* status, int* err) {
+  if (k > 64) return false;
+  k_nf_resolve_cov<<<256, 64 * kNfResolveWaves, 0, s>>>(t, c, ties, k, method, cov6, status, err);
   return true;
 }
 
-bool launch_nf_resolve_knn(hipStream_t s, const NfTreeDev& t, const float4* q, const int* list, const int* count, int k,
-                           int* out_idx, float* out_d, const int* status, int* err) {
-  const int nb = 64;
-  if (k <= 16) k_nf_resolve_knn<16><<<nb, 64, 0, s>>>(t, q, list, count, k, out_idx, out_d, status, err);
-  else if (k <= 32) k_nf_resolve_knn<32><<<nb, 64, 0, s>>>(t, q, list, count, k, out_idx, out_d, status, err);
-  else if (k <= 64) k_nf_resolve_knn<64><<<nb, 64, 0, s>>>(t, q, list, count, k, out_idx, out_d, status, err);
-  else return false;
+bool launch_nf_resolve_knn(hipStream_t s, const NfTreeDev& t, const float4* q, TieList ties, int k, int* out_idx,
+                           float* out_d, const int* status, int* err) {
+  if (k > 64) return false;
+  k_nf_resolve_knn<<<256, 64 * kNfResolveWaves, 0, s>>>(t, q, ties, k, out_idx, out_d, status, err);
   return true;
 }
 

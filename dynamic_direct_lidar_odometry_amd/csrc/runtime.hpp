@@ -134,6 +134,13 @@ struct DevBuf {
 struct NfTreeData {
   int n = 0, cap = 0;
   DevBuf vpts, nodes, box, status;   // status: {the build's error bits, node count} (device ints)
+  hipEvent_t ready = nullptr;        // recorded after the build on the ctx's aux stream; users wait on it
+  NfTreeData() = default;
+  NfTreeData(const NfTreeData&) = delete;
+  NfTreeData& operator=(const NfTreeData&) = delete;
+  ~NfTreeData() {
+    if (ready) (void)hipEventDestroy(ready);
+  }
   NfTreeDev dev() const {
     NfTreeDev t;
     t.vpts = vpts.as<float4>();
@@ -244,7 +251,10 @@ struct gicp_ctx {
   std::array<long long, 7> graph_key{{-1, -1, -1, -1, -1, -1, -1}};
   int predicted_iters = kDefaultPredictedIters;   // iterations of the previous align on this ctx
   std::vector<hipEvent_t> chunk_ev;
-  hipStream_t copy_stream = nullptr;
+  // second stream: nanoflann's tree (tie order) is built here while the
+  // covariance / kNN kernels run on `stream`; the resolvers wait for it
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t aux_ev = nullptr;
   bool profiling = false;
   std::vector<hipEvent_t> prof_ev;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -376,17 +386,25 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
 // Build nanoflann's tree of cd into t on the given stream.  stop >= 0 (the
 // diagnostics entry only) runs that many big levels and nothing after;
 // off (optional, 16 entries) receives the sizes and the scratch offsets.
-inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s, NfTreeData& tr, int stop = -1,
+inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, NfTreeData& tr, int stop = -1,
                                 long long* off = nullptr) {
   NfTreeData* t = &tr;
   const int n = cd.n;
+  // the cloud is ready on s_in; the build runs on the aux stream
+  static const bool same_stream = std::getenv("DDLO_NF_SAME_STREAM") != nullptr;   // A/B, diagnostics
+  const hipStream_t s = same_stream ? s_in : c->aux_stream;
+  if (!same_stream) {
+    HIP_TRY(hipEventRecord(c->aux_ev, s_in));
+    HIP_TRY(hipStreamWaitEvent(s, c->aux_ev, 0));
+  }
+  if (!t->ready) HIP_TRY(hipEventCreateWithFlags(&t->ready, hipEventDisableTiming));
   t->n = n;
-  t->cap = 2 * n + 2;   // a tree of n points has at most 2n - 1 nodes
+  const NfSizes z = nf_sizes(n);
+  t->cap = z.big_ids + 2 * n;   // big-level ids, then 2 per point for the small subtrees' ranges
   HIP_TRY(t->vpts.ensure(sizeof(float4) * (size_t)n));
   HIP_TRY(t->nodes.ensure(sizeof(NfNode) * (size_t)t->cap));
-  HIP_TRY(t->box.ensure(2 * sizeof(float4) * (size_t)t->cap));
+  HIP_TRY(t->box.ensure(2 * sizeof(float4)));   // root_bbox
   HIP_TRY(t->status.ensure(2 * sizeof(int)));
-  const NfSizes z = nf_sizes(n);
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t o_ctl = 0, o_tasks = o_ctl + al(sizeof(NfCtl)),
                o_pend = o_tasks + al(sizeof(NfTask) * (size_t)(z.Lmax + 1) * z.max_task),
@@ -396,8 +414,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s, NfTre
                o_cAE = o_cA + al(sizeof(int) * (size_t)z.max_chunks),
                o_cE2 = o_cAE + al(sizeof(int) * (size_t)z.max_chunks),
                o_tblL = o_cE2 + al(sizeof(int) * (size_t)z.max_chunks),
-               o_tblR = o_tblL + al(sizeof(float4) * (size_t)n), o_arrive = o_tblR + al(sizeof(float4) * (size_t)n),
-               total = o_arrive + al(sizeof(int) * (size_t)t->cap);
+               o_tblR = o_tblL + al(sizeof(float4) * (size_t)n), total = o_tblR + al(sizeof(float4) * (size_t)n);
   HIP_TRY(grow(c->nf_scratch, total, s));
   char* u = c->nf_scratch.as<char>();
   NfBuild b;
@@ -415,7 +432,6 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s, NfTre
   b.cE2 = reinterpret_cast<int*>(u + o_cE2);
   b.tblL = reinterpret_cast<float4*>(u + o_tblL);
   b.tblR = reinterpret_cast<float4*>(u + o_tblR);
-  b.arrive = reinterpret_cast<int*>(u + o_arrive);
   b.quant = cd.quant.as<float>();
   b.n = n;
   b.Lmax = z.Lmax;
@@ -423,19 +439,23 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s, NfTre
   b.max_pend = z.max_pend;
   b.max_small = z.max_small;
   b.max_chunks = z.max_chunks;
+  b.big_ids = z.big_ids;
   if (off) {
     const long long v[16] = {z.Lmax, z.max_task, z.max_pend, z.max_small, z.max_chunks, (long long)o_tasks,
                              (long long)o_pend, (long long)o_small, (long long)o_cmap, (long long)o_cA,
                              (long long)o_cAE, (long long)o_cE2, (long long)o_tblL, (long long)total, n, t->cap};
     for (int i = 0; i < 16; ++i) off[i] = v[i];
   }
-  HIP_TRY(hipMemsetAsync(b.arrive, 0, sizeof(int) * (size_t)t->cap, s));
   launch_nf_build(s, b, cd.pts.as<float4>(), stop);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(t->status.p, &b.ctl->err, sizeof(int), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(t->status.as<int>() + 1, &b.ctl->nnodes, sizeof(int), hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipEventRecord(t->ready, s));
   return GICP_OK;
 }
+
+// stream s waits for the tree's build (enqueued, no host wait)
+inline hipError_t nftree_join(const NfTreeData& t, hipStream_t s) { return hipStreamWaitEvent(s, t.ready, 0); }
 
 // nanoflann's tree of a cloud (once per cloud, on the given stream)
 inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s) {
@@ -449,7 +469,8 @@ inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s) {
 
 // the tied-query list ([count][list n]) and the resolvers' error word, reset on the stream
 inline gicp_status tie_scratch(gicp_ctx* c, int n, hipStream_t s, TieList* tl) {
-  HIP_TRY(grow(c->tie_buf, sizeof(int) * ((size_t)n + 64), s));
+  // a point is listed at most twice (the task-based kNN, then the lane-per-query kernel for its group)
+  HIP_TRY(grow(c->tie_buf, sizeof(int) * (2 * (size_t)n + 64), s));
   HIP_TRY(c->nf_err.ensure(sizeof(int)));
   if (!c->nf_err_host) HIP_TRY(hipHostMalloc((void**)&c->nf_err_host, sizeof(int), hipHostMallocDefault));
   if (!c->nf_err_pending) {
@@ -459,6 +480,7 @@ inline gicp_status tie_scratch(gicp_ctx* c, int n, hipStream_t s, TieList* tl) {
   HIP_TRY(hipMemsetAsync(c->tie_buf.p, 0, sizeof(int), s));
   tl->count = c->tie_buf.as<int>();
   tl->list = c->tie_buf.as<int>() + 64;
+  tl->cap = 2 * n;
   return GICP_OK;
 }
 
@@ -467,8 +489,10 @@ inline gicp_status tie_scratch(gicp_ctx* c, int n, hipStream_t s, TieList* tl) {
 inline gicp_status check_ties(gicp_ctx* c) {
   if (!c->nf_err_pending) return GICP_OK;
   c->nf_err_pending = false;
-  if (*(volatile int*)c->nf_err_host)
-    return fail(GICP_EHIP, "nanoflann tie order: the device kd-tree build or search failed (tree deeper than supported)");
+  const int e = *(volatile int*)c->nf_err_host;
+  if (e)
+    return fail(GICP_EHIP, "nanoflann tie order: the device kd-tree build or search failed (resolver bits " +
+                               std::to_string(e & 255) + ", build bits " + std::to_string(e >> 8) + ")");
   return GICP_OK;
 }
 
@@ -544,6 +568,7 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     j.split_extent = 5.0f;
     j.tie_list = tl.list;
     j.tie_count = tl.count;
+    j.tie_cap = tl.cap;
     if (!launch_knn_covariances(c->stream, j, side.cloud->upper_count()))
       return fail(GICP_EINVAL, "unsupported k");
     launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), j.redo, tl);
@@ -563,7 +588,8 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     return fail(GICP_EINVAL, "unsupported k");
   }
   if (c->tie_exact) {
-    launch_nf_resolve_cov(c->stream, side.cloud->nf->dev(), cd, tl.list, tl.count, k, c->params.regularization,
+    HIP_TRY(nftree_join(*side.cloud->nf, c->stream));
+    launch_nf_resolve_cov(c->stream, side.cloud->nf->dev(), cd, tl, k, c->params.regularization,
                           cv->cov6.as<double>(), side.cloud->nf->status.as<int>(), c->nf_err.as<int>());
     gicp_status st = publish_ties(c, c->stream);
     if (st) return st;

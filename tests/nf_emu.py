@@ -4,7 +4,7 @@ tests to localise a device-build difference to a level.  Not the oracle:
 the tree itself is checked against oracle.tree (pinned to the reference's
 nanoflann in test_nftree_cpu.py)."""
 import numpy as np
-T=4096; CH=2048; BT=256; PER=8; LEAF=100
+T=8192; CH=2048; BT=256; PER=8; LEAF=100
 f32=np.float32
 def f2o(f):
     u=np.array([f],np.float32).view(np.uint32)[0]
@@ -39,7 +39,7 @@ def build(P, stop=-1, trace=None):
     if n>T:
         l=0
         while (T<<l)<n: l+=1
-        Lmax=min(l+2,40)
+        Lmax=min(l+9,40)
     nodes={}; nnodes=[1]
     lo=P.min(0).astype(np.float32); hi=P.max(0).astype(np.float32)
     pend={0:[dict(node=0,begin=0,count=n,lo=lo.copy(),hi=hi.copy(),mm=[f2o(lo[0]),f2o(lo[1]),f2o(lo[2]),f2o(hi[0]),f2o(hi[1]),f2o(hi[2])])]}
