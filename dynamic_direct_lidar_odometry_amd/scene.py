@@ -40,9 +40,13 @@ class Scene:
     peds_vel: np.ndarray      # (Q,2) xy velocity (m/s); zero for static ones
 
 
-# cfg 5's closed loop (loop_trajectory): an ellipse inside the square, so a
-# 1000-frame (100 m) sequence stays in the plaza and revisits its keyframes
-LOOP_X, LOOP_Y = 14.0, 7.0
+# cfg 5's closed loop (loop_trajectory): an ellipse inside the square
+# (~110 m around), driven at 1.5 m/s, so a 1000-frame (150 m) sequence stays
+# in the plaza and revisits its first keyframes; range noise 3 cm (a
+# 64-beam sensor's spec), so scan-to-scan leaves work for scan-to-map
+LOOP_X, LOOP_Y = 22.0, 12.0
+LOOP_STEP = 0.15
+LOOP_NOISE = 0.03
 
 
 def _near_loop(x, y, margin):
@@ -166,7 +170,7 @@ def lidar_dirs(rows: int, cols: int) -> np.ndarray:
 
 
 def raycast(scene: Scene, pose: np.ndarray, rows: int, cols: int, seed: int, t: float = 0.0,
-            organized: bool = False) -> np.ndarray:
+            organized: bool = False, noise: float = 0.01) -> np.ndarray:
     """Ray-cast one scan from world pose ``pose`` (4x4, world <- sensor).
 
     Returns float32 points (N,3) in the SENSOR frame, organized row-major with
@@ -200,7 +204,7 @@ def raycast(scene: Scene, pose: np.ndarray, rows: int, cols: int, seed: int, t: 
     for lo, hi, v in zip(scene.peds_lo, scene.peds_hi, scene.peds_vel):
         shift = np.array([v[0] * t, v[1] * t, 0.0])
         _ray_box(o, inv, lo + shift, hi + shift, tbest)
-    rng_noise = rng.normal(0.0, 0.01, size=tbest.shape)
+    rng_noise = rng.normal(0.0, noise, size=tbest.shape)
     r = tbest + rng_noise
     valid = np.isfinite(tbest) & (r >= 0.5) & (r <= 80.0)
     if organized:
@@ -332,7 +336,7 @@ def sequence(rows: int, cols: int, n_frames: int, n_unique: int, cfg_id: int = 5
 # twin of raycast() (tools/raycast, test/bench infrastructure) when it is
 # built and a device is visible, else by raycast() itself.
 def loop_trajectory(n_frames: int, seed: int = 1005) -> list:
-    """Ground-truth poses along the LOOP_X x LOOP_Y ellipse at 1.0 m/s, 10 Hz (0.1 m per frame), heading
+    """Ground-truth poses along the LOOP_X x LOOP_Y ellipse at 10 Hz, LOOP_STEP m per frame, heading
     along the path with a small yaw wobble; 1000 frames are ~1.4 laps."""
     rng = np.random.default_rng(seed)
     th, poses = -math.pi / 2, []
@@ -342,7 +346,7 @@ def loop_trajectory(n_frames: int, seed: int = 1005) -> list:
         dx, dy = -LOOP_X * math.sin(th), LOOP_Y * math.cos(th)
         wob = float(np.clip(0.9 * wob + rng.normal(0, 0.01), -0.05, 0.05))
         poses.append(make_pose([x, y, SENSOR_Z], (0.0, 0.0, math.atan2(dy, dx) + wob)))
-        th += 0.1 / math.hypot(dx, dy)
+        th += LOOP_STEP / math.hypot(dx, dy)
     return poses
 
 
@@ -394,7 +398,7 @@ def loop_sequence(rows: int, cols: int, first: int, count: int, cfg_id: int = 5,
             k = first + j
             lo, hi = ped_boxes(sc, 0.1 * k)
             s2 = Scene(sc.boxes_lo, sc.boxes_hi, sc.poles, lo, hi, np.zeros_like(sc.peds_vel))
-            out.append(raycast(s2, P, rows, cols, seed=seed + k))
+            out.append(raycast(s2, P, rows, cols, seed=seed + k, noise=LOOP_NOISE))
         return out, poses
     import ctypes as C
     dirs = np.ascontiguousarray(lidar_dirs(rows, cols), np.float64)
@@ -412,7 +416,7 @@ def loop_sequence(rows: int, cols: int, first: int, count: int, cfg_id: int = 5,
         for j in range(nb):
             k = first + b0 + j
             plo[j], phi[j] = ped_boxes(sc, 0.1 * k)
-            noise[j] = np.random.default_rng(seed + k).normal(0.0, 0.01, size=nr)
+            noise[j] = np.random.default_rng(seed + k).normal(0.0, LOOP_NOISE, size=nr)
         out = np.empty((nb, nr, 3), np.float32)
         rc = L.ddlo_raycast(device, nb, nr, ptr(dirs), ptr(T), len(bl), ptr(bl), ptr(bh), len(pl), ptr(pl),
                             len(sc.peds_lo), ptr(plo), ptr(phi), ptr(noise), ptr(out), PLAZA_X, PLAZA_Y, FACADE_H)
