@@ -209,6 +209,10 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.reuse = kn.reuse;
   j.reuse_gap = kn.reuse_gap;
   j.reuse_gap0 = kn.reuse_gap0;
+  j.cap2_d = (double)j.cap2;
+  j.tri_mv_d = (double)j.tri_mv;
+  j.reuse_gap_d = (double)j.reuse_gap;
+  j.reuse_gap0_d = (double)j.reuse_gap0;
   j.reuse_rec0 = kn.reuse_rec0;
   j.reuse_rec_eps = kn.reuse_rec_eps;
   j.reuse_rec_conv = kn.reuse_rec_conv;

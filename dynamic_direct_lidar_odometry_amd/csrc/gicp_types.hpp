@@ -98,6 +98,9 @@ struct AlignJob {
   double guess_t[3];
   double max_corr2;        // max_correspondence_distance^2 (double compare)
   float cap2;              // nextafter(float(max_corr2), +inf), the search bound
+  // fp64 copies of the seed kernel's float knobs (scalar loads where they are
+  // compared: a device-side conversion holds them in vector registers)
+  double cap2_d, tri_mv_d, reuse_gap_d, reuse_gap0_d;
   int nblocks;             // linearize grid size (blocks)
   int max_iterations;      // outer loop bound (max or fixed iterations)
   int fixed_iterations;

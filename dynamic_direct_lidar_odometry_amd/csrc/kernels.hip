@@ -846,7 +846,13 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   const float cap2 = job->cap2;
   const int have_prev = st->have_prev;
   const int prev_window = job->prev_window;
-  const double tri_mv = job->tri_mv;
+  const double tri_mv = job->tri_mv_d;
+  // walk-radius inflation of this search, wave-uniform (scalar registers for the whole kernel)
+  const double gap_sel = have_prev ? job->reuse_gap_d : job->reuse_gap0_d;
+  const long long gap_bits = __double_as_longlong(gap_sel);
+  const double gap_u = __longlong_as_double(
+      ((long long)__builtin_amdgcn_readfirstlane((int)(gap_bits >> 32)) << 32) |
+      (unsigned)__builtin_amdgcn_readfirstlane((int)gap_bits));
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
   const int own_mod = job->own_mod, own_rem = job->own_rem;
@@ -863,7 +869,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   const int rec = st->rec;   // this search records references
   // fused walk: dynamic LDS = [kLinWaves x TaskLds][upper-level box cache]
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  TaskLds* const TL = reinterpret_cast<TaskLds*>(dsm) + wib;
+  TaskLds* const TL = reinterpret_cast<TaskLds*>(dsm) + __builtin_amdgcn_readfirstlane(wib);   // scalar base
   f4v* const upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kTaskLdsBytes);
   if constexpr (FUSED) {
     fill_upper(tgt, upper);
@@ -891,8 +897,9 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
     // spatial sharding: search only the queries this rank owns
     const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
+    static_assert(Q == 16, "interleaved ownership is per 16-point group: i >> 4 == g");
     const bool owned = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi)) &&
-                       (own_mod == 0 || ((i >> 4) % own_mod) == own_rem);
+                       (own_mod == 0 || (g % own_mod) == own_rem);   // scalar: g is wave-uniform
     // Verified reuse (AlignJob::ref): every target point other than p1 was
     // at fp32 squared distance >= B^2 from q_ref, so (relative 1e-6 covers
     // the fp32 rounding of a squared distance) its true distance from q is
@@ -917,7 +924,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
           passed = true;
           pass_key = umin64(pass_key, dkey(dn, rj));
         }
-      } else if (lb2 > (double)cap2) {
+      } else if (lb2 > job->cap2_d) {
         passed = true;
       }
     }
@@ -975,7 +982,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         if (mv < tri_mv) {
           const double r = sqrt((double)sqprev) + mv;
           const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
-          if (b2 < (double)cap2) {
+          if (b2 < job->cap2_d) {
             vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
             seeded = true;
           }
@@ -1121,9 +1128,9 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     // walk radius: the seed bound, widened by the reuse gap so that the
     // reference recorded from this search has B well above d1
     float wr = vis.best;
-    const float gap = have_prev ? job->reuse_gap : job->reuse_gap0;
-    if (rec && active && gap > 0.f) {
-      const double r = sqrt((double)vis.best) + (double)gap;
+    const double gap = gap_u;
+    if (rec && active && gap > 0.0) {
+      const double r = sqrt((double)vis.best) + gap;
       wr = __uint_as_float(__float_as_uint((float)(r * r)) + 1);   // rounded up
     }
     // FUSED: the query state and key are stored after the walk -- a store
@@ -1493,7 +1500,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
   const double max_corr2 = job->max_corr2;
   const int have_prev = st->have_prev;
   const int prev_window = job->prev_window;
-  const double tri_mv = job->tri_mv;
+  const double tri_mv = job->tri_mv_d;
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
   const int own_mod = job->own_mod, own_rem = job->own_rem;
@@ -1575,7 +1582,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restr
         if (mv < tri_mv) {
           const double r = sqrt((double)sqprev) + mv;
           const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
-          if (b2 < (double)cap2) {
+          if (b2 < job->cap2_d) {
             vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
             seeded = true;
           }

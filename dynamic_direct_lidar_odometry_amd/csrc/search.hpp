@@ -401,13 +401,13 @@ __device__ __forceinline__ int morton_jump_split(unsigned long long key, int lo,
   // query index (lane % Q) with the largest (key ^ previous key) in (lo, hi)
   const int lane = lane_id();
   const int qi = lane % Q;
-  const unsigned long long prev = __shfl_up(key, 1);
+  // previous lane's key by DPP wave_shr:1 (no LDS-permute address registers)
+  const unsigned plo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)key, 0x138, 0xf, 0xf, false);
+  const unsigned phi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(key >> 32), 0x138, 0xf, 0xf, false);
+  const unsigned long long prev = ((unsigned long long)phi << 32) | plo;
   int score = -1;
   if (lane < Q && qi > lo && qi < hi) score = (64 - __clzll(key ^ prev)) * 64 + qi;
-  int best = score;
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) best = max(best, __shfl_xor(best, m));
-  best = __builtin_amdgcn_readfirstlane(best);
+  const int best = (int)wave_max((float)score);   // |score| < 2^13: exact in fp32
   return best < 0 ? (lo + hi) / 2 : (best & 63);
 }
 
