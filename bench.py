@@ -47,12 +47,13 @@ METRIC = "GICP iters/sec + ms/scan, 131k-pt source → 500k-pt submap; pose Δ v
 HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same workload
 # (tools/pmc_traffic.sh -> tools/pmc_traffic.py), committed per round
-TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r02_traffic.json"))
+TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r03_traffic.json"))
 
 
 def pmc_traffic():
-    """Measured HBM-side bytes per linearize launch (FETCH_SIZE x2 + WRITE_SIZE,
-    MI355X_MICROARCH.md corrections), or None when no PMC pass is on file."""
+    """Measured HBM-side bytes per linearize launch (FETCH_SIZE + WRITE_SIZE as read:
+    the search kernels are gathers, outside the x2 calibration of MI355X_MICROARCH.md),
+    or None when no PMC pass is on file."""
     try:
         with open(TRAFFIC_JSON) as f:
             d = json.load(f)
@@ -498,7 +499,7 @@ def main():
                    "parallelism": f"replicas x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
-                     "traffic_unit": "bytes per linearize launch (L2->fabric, Infinity-Cache hits included)",
+                     "traffic_unit": "bytes per linearize launch (L2->fabric, Infinity-Cache hits included; counters as read)",
                      "traffic_source": traffic_src,
                      "kernel": "linearize = k_nn_seed (seed + tree walk) + k_nn_scan + k_moments (per outer iteration)",
                      "avg_launch_us": round(avg_launch_s * 1e6, 2),

@@ -1,41 +1,53 @@
-"""Per-launch HBM-side traffic of the linearize (k_nn_seed + k_nn_collect +
-k_nn_scan + k_moments, or the single-kernel k_nn_search + k_moments) from
-two rocprofv3 --pmc passes over bench.py (FETCH_SIZE, WRITE_SIZE; kB units).
+"""Per-launch HBM-side traffic of the linearize (k_nn_seed [+ k_nn_collect] +
+k_nn_scan + k_moments) from two rocprofv3 --pmc passes over bench.py
+(FETCH_SIZE, WRITE_SIZE; kB units), per kernel.
 
-Corrections (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports
-half of the bytes of wide coalesced reads -> doubled here; WRITE_SIZE is
-taken as reported.  Both count L2 -> fabric requests, i.e. Infinity-Cache
-hits are included (upper bound of the HBM bytes).  Active iterations only:
-search dispatches that together ran >= 20 us (no-op iterations exit at once).
+Counters (MI355X_MICROARCH.md, HBM section): both count L2 -> fabric
+requests, so Infinity-Cache hits are included (an upper bound of the HBM
+bytes).  On gfx950 FETCH_SIZE reads exactly half of the bytes of a WIDE
+COALESCED streaming read (16 B per lane); other access widths are
+uncalibrated.  The search kernels are gathers (leaf SoA blocks, query
+states, 8-byte keys), so their FETCH_SIZE is reported as read, without the
+x2; k_moments streams its own 16 B / 48 B per point but gathers the
+target's covariances, so it is reported raw too, with the x2 figure beside
+it as the upper bound.  `bytes_per_linearize` (what bench.py reports as
+roofline.traffic) is the raw sum.  Active iterations only: search
+dispatches that together ran >= 20 us (a no-op iteration exits at once).
 
 usage: python tools/pmc_traffic.py fetch.csv write.csv [out.json]
 """
 import csv
 import json
 import sys
-
+from collections import defaultdict
 
 SEARCH = ("k_nn_seed", "k_nn_collect", "k_nn_scan", "k_nn_search")
 
 
+def short(name):
+    for k in SEARCH + ("k_moments",):
+        if k in name:
+            return k
+    return None
+
+
 def per_iteration(path, counter):
-    rows = list(csv.DictReader(open(path)))
+    """[{kernel: bytes}] per active linearize, in dispatch order."""
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    out = []
-    val_s, dur_s = 0.0, 0.0
+    out, cur, dur_s = [], defaultdict(float), 0.0
     for r in rows:
-        if r["Counter_Name"] != counter:
+        k = short(r["Kernel_Name"])
+        if k is None:
             continue
-        name = r["Kernel_Name"]
-        dur_us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        val = float(r["Counter_Value"]) * 1024.0  # kB -> bytes
-        if any(k in name for k in SEARCH):
-            val_s += val
-            dur_s += dur_us
-        elif "k_moments" in name:
+        val = float(r["Counter_Value"]) * 1024.0   # kB -> bytes
+        cur[k] += val
+        if k in SEARCH:
+            dur_s += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        else:   # k_moments closes the iteration
             if dur_s >= 20.0:
-                out.append((val_s, val))
-            val_s, dur_s = 0.0, 0.0
+                out.append(dict(cur))
+            cur, dur_s = defaultdict(float), 0.0
     return out
 
 
@@ -43,15 +55,21 @@ def main():
     f = per_iteration(sys.argv[1], "FETCH_SIZE")
     w = per_iteration(sys.argv[2], "WRITE_SIZE")
     n = min(len(f), len(w))
-    fetch_search = 2.0 * sum(x[0] for x in f[:n]) / n
-    fetch_mom = 2.0 * sum(x[1] for x in f[:n]) / n
-    write_search = sum(x[0] for x in w[:n]) / n
-    write_mom = sum(x[1] for x in w[:n]) / n
-    res = {"iterations": n,
-           "bytes_per_linearize": round(fetch_search + fetch_mom + write_search + write_mom),
-           "search": {"fetch": round(fetch_search), "write": round(write_search)},
-           "moments": {"fetch": round(fetch_mom), "write": round(write_mom)},
-           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; Infinity-Cache hits included"}
+    kernels = sorted({k for it in f[:n] + w[:n] for k in it})
+    per = {}
+    for k in kernels:
+        fr = sum(it.get(k, 0.0) for it in f[:n]) / n
+        wr = sum(it.get(k, 0.0) for it in w[:n]) / n
+        per[k] = {"fetch_raw": round(fr), "write": round(wr)}
+        if k == "k_moments":
+            per[k]["fetch_x2_upper"] = round(2 * fr)
+    raw = sum(v["fetch_raw"] + v["write"] for v in per.values())
+    search_w = sum(v["write"] for k, v in per.items() if k in SEARCH)
+    res = {"iterations": n, "bytes_per_linearize": raw, "per_kernel": per,
+           "search_write": search_w,
+           "bytes_per_linearize_upper": raw + per.get("k_moments", {}).get("fetch_raw", 0),
+           "correction": "none on the gather kernels (FETCH_SIZE as read); k_moments also raw, x2 upper bound "
+                         "beside it; WRITE_SIZE as read; Infinity-Cache hits included"}
     print(json.dumps(res))
     if len(sys.argv) > 3:
         json.dump(res, open(sys.argv[3], "w"), indent=1)
