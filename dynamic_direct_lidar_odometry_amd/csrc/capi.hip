@@ -525,6 +525,7 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   c->tgt = Side();
   (void)hipStreamDestroy(c->stream);
   (void)hipStreamSynchronize(c->aux_stream);
+  if (c->nf_graph) (void)hipGraphExecDestroy(c->nf_graph);
   (void)hipStreamDestroy(c->aux_stream);
   (void)hipEventDestroy(c->aux_ev);
   delete c;

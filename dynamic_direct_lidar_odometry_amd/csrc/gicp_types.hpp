@@ -216,7 +216,9 @@ struct NfBuild {
   int *cA, *cAE, *cE2;     // [max_chunks] per-chunk counts
   float4 *tblL, *tblR;     // [n] rank tables of the Hoare pairing
   const float* quant;      // the cloud's bbox: min [0..2], max [4..6]
+  const float4* sorted;    // the cloud's Morton-sorted points (w = original index bits)
   int n, Lmax, max_task, max_pend, max_small, max_chunks;
+  int nbucket;             // the size the grids are sized for (>= n): one captured graph per bucket
   int big_ids;             // node ids [0, big_ids) for the big levels; a small task of vind range
                            // [b, b + c) numbers its subtree in [big_ids + 2b, big_ids + 2(b + c))
 };

@@ -72,7 +72,7 @@ void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr,
 NfSizes nf_sizes(int n);
 // sorted_pts: the cloud's Morton-sorted points (w = original index)
 // stop >= 0: run only that many big levels (diagnostics)
-void launch_nf_build(hipStream_t s, const NfBuild& b, const float4* sorted_pts, int stop = -1);
+void launch_nf_build(hipStream_t s, const NfBuild& hb, const NfBuild* db, int stop = -1);
 // status = {build error bits, node count}; nodes: 4 ints per node (c1, c2, feat, parent), f: divlow, divhigh
 void launch_nf_export(hipStream_t s, const NfTreeDev& t, const int* status, int cap, int* vind, int* nodes, float* f);
 // re-run the listed (tied) queries with nanoflann's search; status: the

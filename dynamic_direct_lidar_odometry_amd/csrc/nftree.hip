@@ -186,7 +186,8 @@ __device__ void task_chunk_sums(const int* cnt, const NfTask& tk, int blk, int* 
 
 // ---------------------------------------------------------------------------
 // build kernels
-__global__ void k_nf_init(NfBuild b) {
+__global__ void k_nf_init(const NfBuild* __restrict__ bp) {
+  const NfBuild& b = *bp;
   if (threadIdx.x == 0) {
     NfCtl* ctl = b.ctl;
     ctl->nnodes = 1;
@@ -221,7 +222,8 @@ __global__ void k_nf_init(NfBuild b) {
 // Level L's task list from the children its parent level produced (pend[L]):
 // nodes > kNfT points become big tasks (their chunks listed), the others
 // small tasks; the final call lists every remaining node as small.
-__global__ __launch_bounds__(1024) void k_nf_map(NfBuild b, int L) {
+__global__ __launch_bounds__(1024) void k_nf_map(const NfBuild* __restrict__ bp, int L) {
+  const NfBuild& b = *bp;
   __shared__ int sh[17];
   __shared__ int s_big, s_small, s_ch, s_small0;
   NfCtl* ctl = b.ctl;
@@ -299,7 +301,8 @@ __global__ __launch_bounds__(1024) void k_nf_map(NfBuild b, int L) {
 }
 
 // middleSplit_'s cut per task; #{v < cut} and #{v <= cut} per chunk
-__global__ __launch_bounds__(kNfBT) void k_nf_count(NfBuild b, int L) {
+__global__ __launch_bounds__(kNfBT) void k_nf_count(const NfBuild* __restrict__ bp, int L) {
+  const NfBuild& b = *bp;
   __shared__ int sh[17];
   TaskView v;
   if (!task_of_block(b, L, &v)) return;
@@ -334,7 +337,8 @@ __global__ __launch_bounds__(kNfBT) void k_nf_count(NfBuild b, int L) {
 // there), boundary lim2.  TABLE: write each misplaced element into its rank
 // slot; else (APPLY) overwrite each misplaced position with its partner.
 template <int PASS, bool TABLE>
-__global__ __launch_bounds__(kNfBT) void k_nf_pass(NfBuild b, int L) {
+__global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ bp, int L) {
+  const NfBuild& b = *bp;
   __shared__ int sh[17];
   TaskView v;
   if (!task_of_block(b, L, &v)) return;
@@ -852,7 +856,8 @@ __device__ void group_depth(const NfBuild& b, SubLds& S, int cur, int nq, int ba
   }
 }
 
-__global__ __launch_bounds__(64 * kNfSubWaves) void k_nf_sub(NfBuild b) {
+__global__ __launch_bounds__(64 * kNfSubWaves) void k_nf_sub(const NfBuild* __restrict__ bp) {
+  const NfBuild& b = *bp;
   __shared__ SubLds S;   // ~157 KB: one workgroup per CU
   if ((int)blockIdx.x >= b.ctl->nsmall) return;
   const NfTask tk = b.small[blockIdx.x];
@@ -918,7 +923,8 @@ __global__ __launch_bounds__(64 * kNfSubWaves) void k_nf_sub(NfBuild b) {
 struct NfGStack {
   NfSubNode e[kNfStack];
 };
-__global__ __launch_bounds__(64) void k_nf_small_global(NfBuild b) {
+__global__ __launch_bounds__(64) void k_nf_small_global(const NfBuild* __restrict__ bp) {
+  const NfBuild& b = *bp;
   __shared__ NfGStack S;
   if ((int)blockIdx.x >= b.ctl->nsmall) return;
   const NfTask tk = b.small[blockIdx.x];
@@ -1067,11 +1073,11 @@ __global__ __launch_bounds__(64 * kNfResolveWaves) void k_nf_resolve_knn(NfTreeD
 }
 
 // vind starts as the identity (init_vind): the cloud's points in original order
-__global__ __launch_bounds__(256) void k_nf_unsort(const float4* __restrict__ sorted, int n, float4* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_nf_unsort(const NfBuild* __restrict__ bp) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  const float4 p = sorted[s];
-  out[__float_as_int(p.w)] = p;
+  if (s >= bp->n) return;
+  const float4 p = bp->sorted[s];
+  bp->vpts[__float_as_int(p.w)] = p;
 }
 
 // diagnostics / tests: the tree as nanoflann would hold it (status[1] = nodes)
@@ -1112,22 +1118,26 @@ NfSizes nf_sizes(int n) {
 }
 
 
-void launch_nf_build(hipStream_t s, const NfBuild& b, const float4* sorted_pts, int stop) {
-  k_nf_unsort<<<cdivl(b.n, 256), 256, 0, s>>>(sorted_pts, b.n, b.vpts);
-  k_nf_init<<<1, 64, 0, s>>>(b);
-  const int G = std::max(1, b.max_chunks);
-  for (int L = 0; L < b.Lmax; ++L) {
+// hb: the descriptor on the host (grid sizes); db: the same in device memory
+// (the kernels' argument, so that a captured graph serves any cloud of the
+// size bucket: only the descriptor is rewritten).  stop >= 0: that many big
+// levels, nothing after (diagnostics).
+void launch_nf_build(hipStream_t s, const NfBuild& hb, const NfBuild* db, int stop) {
+  k_nf_unsort<<<cdivl(hb.nbucket, 256), 256, 0, s>>>(db);
+  k_nf_init<<<1, 64, 0, s>>>(db);
+  const int G = std::max(1, hb.max_chunks);
+  for (int L = 0; L < hb.Lmax; ++L) {
     if (stop >= 0 && L >= stop) return;
-    k_nf_map<<<1, 1024, 0, s>>>(b, L);
-    k_nf_count<<<G, kNfBT, 0, s>>>(b, L);
-    k_nf_pass<1, true><<<G, kNfBT, 0, s>>>(b, L);
-    k_nf_pass<1, false><<<G, kNfBT, 0, s>>>(b, L);
-    k_nf_pass<2, true><<<G, kNfBT, 0, s>>>(b, L);
-    k_nf_pass<2, false><<<G, kNfBT, 0, s>>>(b, L);
+    k_nf_map<<<1, 1024, 0, s>>>(db, L);
+    k_nf_count<<<G, kNfBT, 0, s>>>(db, L);
+    k_nf_pass<1, true><<<G, kNfBT, 0, s>>>(db, L);
+    k_nf_pass<1, false><<<G, kNfBT, 0, s>>>(db, L);
+    k_nf_pass<2, true><<<G, kNfBT, 0, s>>>(db, L);
+    k_nf_pass<2, false><<<G, kNfBT, 0, s>>>(db, L);
   }
-  k_nf_map<<<1, 1024, 0, s>>>(b, b.Lmax);
-  k_nf_sub<<<b.max_small, 64 * kNfSubWaves, 0, s>>>(b);
-  k_nf_small_global<<<b.max_small, 64, 0, s>>>(b);
+  k_nf_map<<<1, 1024, 0, s>>>(db, hb.Lmax);
+  k_nf_sub<<<hb.max_small, 64 * kNfSubWaves, 0, s>>>(db);
+  k_nf_small_global<<<hb.max_small, 64, 0, s>>>(db);
 }
 
 void launch_nf_export(hipStream_t s, const NfTreeDev& t, const int* status, int cap, int* vind, int* nodes, float* f) {

@@ -255,6 +255,9 @@ struct gicp_ctx {
   // covariance / kNN kernels run on `stream`; the resolvers wait for it
   hipStream_t aux_stream = nullptr;
   hipEvent_t aux_ev = nullptr;
+  DevBuf nf_desc;                    // the build descriptor the tree kernels read
+  hipGraphExec_t nf_graph = nullptr;  // the build, captured for one size bucket
+  int nf_graph_key = -1;
   bool profiling = false;
   std::vector<hipEvent_t> prof_ev;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -399,7 +402,11 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   }
   if (!t->ready) HIP_TRY(hipEventCreateWithFlags(&t->ready, hipEventDisableTiming));
   t->n = n;
-  const NfSizes z = nf_sizes(n);
+  // grids sized for a bucket of 16k points: one captured build graph serves
+  // every cloud of the bucket (the kernels read the descriptor, and n, from
+  // device memory), so a build is one graph launch, not ~80 kernel launches
+  const int nbucket = (int)(((long)n + 16383) / 16384 * 16384);
+  const NfSizes z = nf_sizes(nbucket);
   t->cap = z.big_ids + 2 * n;   // big-level ids, then 2 per point for the small subtrees' ranges
   HIP_TRY(t->vpts.ensure(sizeof(float4) * (size_t)n));
   HIP_TRY(t->nodes.ensure(sizeof(NfNode) * (size_t)t->cap));
@@ -414,7 +421,8 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
                o_cAE = o_cA + al(sizeof(int) * (size_t)z.max_chunks),
                o_cE2 = o_cAE + al(sizeof(int) * (size_t)z.max_chunks),
                o_tblL = o_cE2 + al(sizeof(int) * (size_t)z.max_chunks),
-               o_tblR = o_tblL + al(sizeof(float4) * (size_t)n), total = o_tblR + al(sizeof(float4) * (size_t)n);
+               o_tblR = o_tblL + al(sizeof(float4) * (size_t)nbucket),
+               total = o_tblR + al(sizeof(float4) * (size_t)nbucket);
   HIP_TRY(grow(c->nf_scratch, total, s));
   char* u = c->nf_scratch.as<char>();
   NfBuild b;
@@ -433,7 +441,9 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   b.tblL = reinterpret_cast<float4*>(u + o_tblL);
   b.tblR = reinterpret_cast<float4*>(u + o_tblR);
   b.quant = cd.quant.as<float>();
+  b.sorted = cd.pts.as<float4>();
   b.n = n;
+  b.nbucket = nbucket;
   b.Lmax = z.Lmax;
   b.max_task = z.max_task;
   b.max_pend = z.max_pend;
@@ -446,8 +456,34 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
                              (long long)o_cAE, (long long)o_cE2, (long long)o_tblL, (long long)total, n, t->cap};
     for (int i = 0; i < 16; ++i) off[i] = v[i];
   }
-  launch_nf_build(s, b, cd.pts.as<float4>(), stop);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(c->nf_desc.ensure(sizeof(NfBuild)));
+  NfBuild* db = c->nf_desc.as<NfBuild>();
+  // pageable source: staged by the runtime before the call returns, so the
+  // next build may rewrite b at once (the copies run in stream order)
+  HIP_TRY(hipMemcpyAsync(db, &b, sizeof(NfBuild), hipMemcpyHostToDevice, s));
+  static const bool no_graph = std::getenv("DDLO_NF_NO_GRAPH") != nullptr;   // A/B, diagnostics
+  if (stop >= 0 || no_graph || same_stream) {
+    launch_nf_build(s, b, db, stop);
+    HIP_TRY(hipGetLastError());
+  } else {
+    if (c->nf_graph_key != nbucket) {
+      if (c->nf_graph) HIP_TRY(hipGraphExecDestroy(c->nf_graph));
+      c->nf_graph = nullptr;
+      c->nf_graph_key = -1;
+      hipGraph_t g = nullptr;
+      HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      launch_nf_build(s, b, db, -1);
+      const hipError_t e1 = hipGetLastError();
+      const hipError_t e2 = hipStreamEndCapture(s, &g);
+      HIP_TRY(e1);
+      HIP_TRY(e2);
+      const hipError_t e3 = hipGraphInstantiate(&c->nf_graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIP_TRY(e3);
+      c->nf_graph_key = nbucket;
+    }
+    HIP_TRY(hipGraphLaunch(c->nf_graph, s));
+  }
   HIP_TRY(hipMemcpyAsync(t->status.p, &b.ctl->err, sizeof(int), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(t->status.as<int>() + 1, &b.ctl->nnodes, sizeof(int), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipEventRecord(t->ready, s));

@@ -32,14 +32,15 @@ def nf_index(c,l1,l2):
     if l1>c//2: return l1
     if l2<c//2: return l2
     return c//2
-def build(P, stop=-1, trace=None):
+def build(P, stop=-1, trace=None, Lmax=None):
     n=len(P); vp=np.concatenate([P.astype(np.float32), np.arange(n)[:,None].astype(np.float32)],1)  # w as index (float ok here)
     idxs=np.arange(n)
-    Lmax=0
-    if n>T:
-        l=0
-        while (T<<l)<n: l+=1
-        Lmax=min(l+9,40)
+    if Lmax is None:   # the device sizes its levels for a 16k-point bucket: pass its Lmax to compare stop by stop
+        Lmax=0
+        if n>T:
+            l=0
+            while (T<<l)<n: l+=1
+            Lmax=min(l+9,40)
     nodes={}; nnodes=[1]
     lo=P.min(0).astype(np.float32); hi=P.max(0).astype(np.float32)
     pend={0:[dict(node=0,begin=0,count=n,lo=lo.copy(),hi=hi.copy(),mm=[f2o(lo[0]),f2o(lo[1]),f2o(lo[2]),f2o(hi[0]),f2o(hi[1]),f2o(hi[2])])]}

@@ -119,12 +119,13 @@ def test_device_build_levels_match_emulator(name):
     pts = _clouds()[name]
     c = P.Context(0)
     c.set_target(pts)
+    Ldev = int(c.nfbuild_debug(TARGET, stop=0, scratch_bytes=64)[1][0])
     trace = []
-    nf_emu.build(pts, trace=trace)
+    nf_emu.build(pts, trace=trace, Lmax=Ldev)
     first_bad = None
-    for stop in range(int(c.nfbuild_debug(TARGET, stop=0, scratch_bytes=64)[1][0]) + 1):
+    for stop in range(Ldev + 1):
         v_dev, _, st_s, _ = c.nfbuild_debug(TARGET, stop=stop, scratch_bytes=64)
-        v_emu = nf_emu.build(pts, stop=stop)
+        v_emu = nf_emu.build(pts, stop=stop, Lmax=Ldev)
         same = np.array_equal(v_dev, v_emu)
         print("stop", stop, "status", st_s.tolist(), "same", same,
               "" if same else f"first diff at {int(np.argmax(v_dev != v_emu))}")
@@ -143,6 +144,6 @@ def test_device_build_levels_match_emulator(name):
         emu = sorted((t["begin"], t["count"]) for t in tasks)
         dev = sorted((int(t["begin"]), int(t["count"])) for t in dev_t[:nt])
         print("level", L, "emu tasks", emu[:6], "dev", dev[:6])
-    v_full = nf_emu.build(pts)
+    v_full = nf_emu.build(pts, Lmax=Ldev)
     print("full same", np.array_equal(vind, v_full))
     assert first_bad is None and st[0] == 0 and np.array_equal(vind, v_full)
