@@ -269,12 +269,39 @@ def batched_leg(dist, rank, world, local_rank, args):
     elapsed = time.perf_counter() - c0
     iters = sum(r.iterations_run for r in res[1:])
     elapsed, iters_total = reduce_over_ranks(dist, elapsed, iters, f"cuda:{local_rank}")
+    # the same pairs with ties in the device's Morton order (gicp_set_tie_order(0): no nanoflann tree)
+    with tie_order_env("0"):
+        if dist is not None:
+            dist.barrier()
+        c0 = time.perf_counter()
+        P.s2s_batch(mine, params, device=local_rank, nstreams=args.batch_streams)
+        el_m = time.perf_counter() - c0
+    el_m, _ = reduce_over_ranks(dist, el_m, 0, f"cuda:{local_rank}")
     return {"workload": f"cfg5 frame-parallel S2S: {npairs} pairs of {args.batch_frames} unique 64x2048 scans "
                         f"(closed plaza loop, moving pedestrians), k=10, maxCorr 1.0 m",
             "n_gpus": world, "streams_per_gpu": args.batch_streams, "pairs": npairs,
             "pairs_per_s": round(npairs / elapsed, 2), "ms_per_pair": round(1e3 * elapsed / npairs, 4),
-            "iters_per_s": round(iters_total / elapsed, 2),
-            "per_pair_work": "H2D + index build + covariances + align", "collective": "none (frames split by rank)"}
+            "iters_per_s": round(iters_total / elapsed, 2), "tie_order": "nanoflann (exact)",
+            "ms_per_pair_morton_tie_order": round(1e3 * el_m / npairs, 4),
+            "per_pair_work": "H2D + index build + covariances (+ nanoflann's tree for the tie order) + align",
+            "collective": "none (frames split by rank)"}
+
+
+class tie_order_env:
+    """Contexts created inside the block use the Morton tie order (DDLO_TIE_EXACT=0; read at ctx creation)."""
+
+    def __init__(self, v):
+        self.v = v
+
+    def __enter__(self):
+        self.old = os.environ.get("DDLO_TIE_EXACT")
+        os.environ["DDLO_TIE_EXACT"] = self.v
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("DDLO_TIE_EXACT", None)
+        else:
+            os.environ["DDLO_TIE_EXACT"] = self.old
 
 
 def s2s_gn_leg(local_rank, args):
@@ -370,11 +397,23 @@ def odometry_leg(dist, rank, world, local_rank, args, frames=None):
     sub_pts = int(r.submap_points)
     odo.close()
     el, nframes = reduce_over_ranks(dist, el, len(mine), f"cuda:{local_rank}")
+    with tie_order_env("0"):   # the same chain with ties in Morton order (no nanoflann trees)
+        odo = OD.Odometry(local_rank)
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for f in mine:
+            odo.process(f)
+        el_m = time.perf_counter() - t0
+        odo.close()
+    el_m, _ = reduce_over_ranks(dist, el_m, 0, f"cuda:{local_rank}")
     return {"workload": f"cfg5 S2M chain: odometry driver over {args.batch_frames} unique 64x2048 frames "
-                        "(closed plaza loop, ~1.4 laps, moving pedestrians), ddlo.yaml parameters "
+                        "(closed plaza loop: 22 x 12 m ellipse at 1.5 m/s, ~1.4 laps, 3 cm range noise, moving pedestrians), "
+                        "ddlo.yaml parameters "
                         "(crop 1 m, voxel 0.1 m, S2S k=10 / S2M k=20, adaptive keyframes, knn/kcv/kcc 10)",
             "n_gpus": world, "frames": int(nframes), "frames_per_s": round(nframes / el, 2),
-            "ms_per_frame": round(1e3 * el / nframes, 4),
+            "ms_per_frame": round(1e3 * el / nframes, 4), "tie_order": "nanoflann (exact)",
+            "ms_per_frame_morton_tie_order": round(1e3 * el_m / nframes, 4),
             "per_frame_work": "H2D + crop + voxel + metrics + S2S (index, covariances, align) + submap + S2M + keyframes",
             "rank0": {"keyframes": nk, "last_submap_points": sub_pts, "max_submap_points": max_sub,
                       "submap_changes": changes, "tracked": tracked,
