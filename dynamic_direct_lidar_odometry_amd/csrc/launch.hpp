@@ -73,6 +73,8 @@ NfSizes nf_sizes(int n);
 // sorted_pts: the cloud's Morton-sorted points (w = original index)
 // stop >= 0: run only that many big levels (diagnostics)
 void launch_nf_build(hipStream_t s, const NfBuild& hb, const NfBuild* db, int stop = -1);
+// *db = b on the stream (the descriptor the build kernels read)
+void launch_nf_set_desc(hipStream_t s, const NfBuild& b, NfBuild* db);
 // status = {build error bits, node count}; nodes: 4 ints per node (c1, c2, feat, parent), f: divlow, divhigh
 void launch_nf_export(hipStream_t s, const NfTreeDev& t, const int* status, int cap, int* vind, int* nodes, float* f);
 // re-run the listed (tied) queries with nanoflann's search; status: the

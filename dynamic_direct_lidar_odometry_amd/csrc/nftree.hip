@@ -1118,6 +1118,11 @@ NfSizes nf_sizes(int n) {
 }
 
 
+__global__ void k_nf_set_desc(NfBuild b, NfBuild* __restrict__ db) {
+  if (threadIdx.x == 0) *db = b;
+}
+void launch_nf_set_desc(hipStream_t s, const NfBuild& b, NfBuild* db) { k_nf_set_desc<<<1, 64, 0, s>>>(b, db); }
+
 // hb: the descriptor on the host (grid sizes); db: the same in device memory
 // (the kernels' argument, so that a captured graph serves any cloud of the
 // size bucket: only the descriptor is rewritten).  stop >= 0: that many big

@@ -458,9 +458,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   }
   HIP_TRY(c->nf_desc.ensure(sizeof(NfBuild)));
   NfBuild* db = c->nf_desc.as<NfBuild>();
-  // pageable source: staged by the runtime before the call returns, so the
-  // next build may rewrite b at once (the copies run in stream order)
-  HIP_TRY(hipMemcpyAsync(db, &b, sizeof(NfBuild), hipMemcpyHostToDevice, s));
+  launch_nf_set_desc(s, b, db);   // by value as a kernel argument: no host buffer has to outlive the call
   static const bool no_graph = std::getenv("DDLO_NF_NO_GRAPH") != nullptr;   // A/B, diagnostics
   if (stop >= 0 || no_graph || same_stream) {
     launch_nf_build(s, b, db, stop);
