@@ -14,6 +14,15 @@ constexpr int kLeafSize = 32;
 constexpr int kFanout = 64;
 constexpr int kMaxLevels = 5;   // leaves + 4 internal levels: n <= 32*64^4
 constexpr int kDirBits = 18;    // key directory: top 18 of the 63 Morton-key bits (1 MB per cloud)
+// Fine directory (search.hpp seed_pos): a coarse bucket holding more than
+// kFineMin keys gets a slot of 2^kFineBits 16-bit offsets, the lower bound of
+// each 6-bit refinement of its prefix.  Layout after dir's 2^kDirBits + 1
+// entries: [slot counter][slot per coarse bucket, -1: none][slots].
+constexpr int kFineBits = 6;
+constexpr int kFineMin = 32;
+__host__ __device__ constexpr long fine_dir_ints(int n) {   // ints of the whole directory buffer
+  return (1L << kDirBits) + 2 + (1L << kDirBits) + ((long)(n / (kFineMin + 1) + 1) << kFineBits) / 2;
+}
 
 // Number of moment slots the linearize kernel reduces per source point
 // (see DESIGN.md "Normal-equation moments"): 6 (sum M) + 18 (sum q_k M) +
@@ -42,7 +51,7 @@ struct CloudDev {
   const float4* box_hi;
   const float* quant;             // device [lo.x, lo.y, lo.z, scale]
   const float* soa;               // per leaf: x[32], y[32], z[32] (sorted, sentinel-padded)
-  const int* dir;                 // key directory [2^kDirBits + 1] (see search.hpp dir_range)
+  const int* dir;                 // key directory [2^kDirBits + 1] + the fine directory (kFineBits)
   int n;
   int nlevels;
   // per-level node offset/count, kept as scalars (no array => no scratch

@@ -156,6 +156,37 @@ __global__ __launch_bounds__(256) void k_key_dir(const unsigned long long* __res
   dir[p] = lo;
 }
 
+// Fine directory: one wavefront per coarse bucket; a bucket of more than
+// kFineMin keys (and fewer than 2^16) takes a slot, and lane f stores the
+// lower bound of refinement f (the next kFineBits Morton bits) relative to
+// the bucket start.  Slot order depends on scheduling, the contents do not.
+__global__ __launch_bounds__(256) void k_key_fine(const unsigned long long* __restrict__ keys, int* __restrict__ dir) {
+  const int c = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const int lane = lane_id();
+  if (c >= (1 << kDirBits)) return;
+  int* const ctr = dir + (1 << kDirBits) + 1;
+  int* const fslot = ctr + 1;
+  unsigned short* const fine = reinterpret_cast<unsigned short*>(fslot + (1 << kDirBits));
+  const int lo = dir[c], hi = dir[c + 1];
+  if (hi - lo <= kFineMin || hi - lo > 65535) {
+    if (lane == 0) fslot[c] = -1;
+    return;
+  }
+  int slot = 0;
+  if (lane == 0) slot = atomicAdd(ctr, 1);
+  slot = __builtin_amdgcn_readfirstlane(slot);
+  constexpr int sh = 63 - kDirBits - kFineBits;
+  const unsigned long long want = ((unsigned long long)c << kFineBits) | (unsigned long long)lane;
+  int a = lo, b = hi;
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    if ((keys[mid] >> sh) < want) a = mid + 1;
+    else b = mid;
+  }
+  fine[((size_t)slot << kFineBits) + lane] = (unsigned short)(a - lo);
+  if (lane == 0) fslot[c] = slot;
+}
+
 // Per-leaf SoA copy of the sorted points: leaf l = x[32], y[32], z[32], so
 // that a lane's 8 consecutive coordinates are two 16-B loads per axis and
 // pairs of them feed the packed-math distance directly (k_nn_scan).
@@ -1026,10 +1057,13 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       int pos = large_step ? jprev : 0;
       if (__any(need_seed)) {
         const unsigned long long qk = morton_key(qx, qy, qz, tgt.quant);
-        int dlo, dhi;
-        dir_range(tgt.dir, qk, dlo, dhi);   // one load instead of ~5 dependent search steps
-        const int lb = group_lower_bound<Q>(tgt.keys, tgt.n, qk, dlo, dhi);
-        if (need_seed) pos = lb;
+        int dlo, dhi, sp;
+        const bool found = seed_pos(tgt.dir, qk, sp, dlo, dhi);   // directory + fine directory: <= 2 loads
+        if (__any(!found)) {   // a bucket of >= 2^16 keys: searched
+          const bool srch = need_seed && !found;
+          sp = group_lower_bound<Q>(tgt.keys, tgt.n, qk, srch ? dlo : sp, srch ? dhi : sp);
+        }
+        if (need_seed) pos = sp;
       }
       const int s = lane / Q;
       const int w0 = pos - (64 / Q) * kSeedW / 2 + s * kSeedW;
@@ -1074,9 +1108,9 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         const float oy = pr == 2 ? d : pr == 3 ? -d : pr == 6 ? dd : pr == 7 ? -dd : 0.f;
         const float oz = pr == 4 ? d : pr == 5 ? -d : 0.f;
         const unsigned long long pk = morton_key(cx + ox, cy + oy, cz + oz, tgt.quant);
-        int plo, phi;
-        dir_range(tgt.dir, pk, plo, phi);
-        const int plb = group_lower_bound<8>(tgt.keys, tgt.n, pk, plo, phi);
+        int plo, phi, plb;
+        const bool pfound = seed_pos(tgt.dir, pk, plb, plo, phi);
+        if (__any(!pfound)) plb = group_lower_bound<8>(tgt.keys, tgt.n, pk, pfound ? plb : plo, pfound ? plb : phi);
         const int cand = min(max(plb - 4 + (lane >> 3), 0), tgt.n - 1);
         const float4 p = ldg4(tgt.pts, cand);
         f4v* const CP = TL->sb_lo;   // 64 staged candidates (the walk's box stage, free until the walk)
@@ -2574,6 +2608,8 @@ void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, int
 }
 void launch_key_dir(hipStream_t s, const unsigned long long* keys, int n, int* dir) {
   k_key_dir<<<cdiv((1 << kDirBits) + 1, 256), 256, 0, s>>>(keys, n, dir);
+  (void)hipMemsetAsync(dir + (1 << kDirBits) + 1, 0, sizeof(int), s);   // fine-slot counter
+  k_key_fine<<<(1 << kDirBits) / 4, 256, 0, s>>>(keys, dir);
 }
 void launch_leaf_soa(hipStream_t s, const float4* pts, int npad, float* soa) {
   k_leaf_soa<<<cdiv(npad, 256), 256, 0, s>>>(pts, npad, soa);

@@ -170,32 +170,36 @@ struct TaskCollector {
   __device__ __forceinline__ void pair_filter(int cm, unsigned qmask) {
     const int lane = lane_id();
     const int nq = __popc(qmask);
+    // the queries come from registers: lane l holds query l & 15 (its slices
+    // too), so the lane-per-leaf loop reads query k with v_readlane at a
+    // constant lane (no LDS round trip per query step)
+    const float qw = active ? wr : -1.f;
     if (nq <= 2 || (!knn && nq < pf_ratio * ((cm + 3) >> 2))) {
+      const unsigned qm_u = (unsigned)__builtin_amdgcn_readfirstlane((int)qmask);
       unsigned m16 = 0u;
+      f4v blo = f4v{0.f, 0.f, 0.f, 0.f}, bhi = blo;
       if (lane < cm) {
-        const f4v blo = L->sb_lo[lane], bhi = L->sb_hi[lane];
-        unsigned qm = qmask;
-        while (qm) {
-          const int k = __builtin_ctz(qm);
-          qm &= qm - 1;
-          const f4v qk = L->q[k];
-          if (qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, make_float4(blo.x, blo.y, blo.z, 0.f),
-                                       make_float4(bhi.x, bhi.y, bhi.z, 0.f)) <= qk.w)
-            m16 |= 1u << k;
+        blo = L->sb_lo[lane];
+        bhi = L->sb_hi[lane];
+      }
+      const float4 lo4 = make_float4(blo.x, blo.y, blo.z, 0.f), hi4 = make_float4(bhi.x, bhi.y, bhi.z, 0.f);
+#pragma unroll
+      for (int k = 0; k < kTaskQ; ++k) {
+        if ((qm_u >> k) & 1u) {
+          const float kx = readlane_f(qx, k), ky = readlane_f(qy, k), kz = readlane_f(qz, k), kw = readlane_f(qw, k);
+          if (lane < cm && kw >= 0.f && box_dist2(kx, ky, kz, lo4, hi4) <= kw) m16 |= 1u << k;
         }
       }
       if (knn) {   // per query: the nearest full leaf's farthest corner bounds its k-th neighbour
-        unsigned qm = qmask;
-        while (qm) {
-          const int k = __builtin_ctz(qm);
-          qm &= qm - 1;
-          float v = INFINITY;
-          if (lane < cm && L->sb_leaf[lane] < nfull) {
-            const f4v qk = L->q[k];
-            v = box_maxdist2(qk.x, qk.y, qk.z, L->sb_lo[lane], L->sb_hi[lane]);
+        const bool full = lane < cm && L->sb_leaf[lane] < nfull;
+#pragma unroll
+        for (int k = 0; k < kTaskQ; ++k) {
+          if ((qm_u >> k) & 1u) {
+            const float kx = readlane_f(qx, k), ky = readlane_f(qy, k), kz = readlane_f(qz, k);
+            float v = full ? box_maxdist2(kx, ky, kz, blo, bhi) : INFINITY;
+            v = wave_min(v);
+            if ((lane & 15) == k) tight = fminf(tight, v);
           }
-          v = wave_min(v);
-          if ((lane & 15) == k) tight = fminf(tight, v);
         }
       }
       const unsigned long long lm = __ballot(m16 != 0u);
@@ -216,11 +220,10 @@ struct TaskCollector {
       const int li = r0 + (lane >> 4);
       bool need = false;
       if (li < cm && ((qmask >> (lane & 15)) & 1u)) {
-        const f4v qk = L->q[lane & 15];
-        const f4v blo = L->sb_lo[li], bhi = L->sb_hi[li];
-        need = qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, make_float4(blo.x, blo.y, blo.z, 0.f),
-                                        make_float4(bhi.x, bhi.y, bhi.z, 0.f)) <= qk.w;
-        if (knn && L->sb_leaf[li] < nfull) tight = fminf(tight, box_maxdist2(qk.x, qk.y, qk.z, blo, bhi));
+        const f4v blo = L->sb_lo[li], bhi = L->sb_hi[li];   // the lane's own query (lane & 15) is in its registers
+        need = qw >= 0.f && box_dist2(qx, qy, qz, make_float4(blo.x, blo.y, blo.z, 0.f),
+                                      make_float4(bhi.x, bhi.y, bhi.z, 0.f)) <= qw;
+        if (knn && L->sb_leaf[li] < nfull) tight = fminf(tight, box_maxdist2(qx, qy, qz, blo, bhi));
       }
       const unsigned long long bal = __ballot(need);
       const unsigned m16 = (unsigned)((bal >> (lane & ~15)) & 0xffffull);

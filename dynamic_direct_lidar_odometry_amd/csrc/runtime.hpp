@@ -365,7 +365,7 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(cd->pts.ensure(sizeof(float4) * npad));
   HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
   launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
-  HIP_TRY(cd->dir.ensure(sizeof(int) * ((1u << kDirBits) + 1)));
+  HIP_TRY(cd->dir.ensure(sizeof(int) * (size_t)fine_dir_ints(N)));
   launch_key_dir(s, cd->keys.as<unsigned long long>(), N, cd->dir.as<int>());
   HIP_TRY(cd->soa.ensure(sizeof(float) * 3 * (size_t)npad));
   launch_leaf_soa(s, cd->pts.as<float4>(), npad, cd->soa.as<float>());

@@ -125,6 +125,27 @@ __device__ __forceinline__ void dir_range(const int* dir, unsigned long long key
   hi = gp(dir)[p + 1];
 }
 
+// Seed position of a key in the sorted keys (a Morton window is centred on
+// it): the coarse bucket's range and its fine slot in one round trip, the
+// refinement's lower bound in a second.  A bucket of <= kFineMin keys gives
+// its middle (the window covers the bucket); an empty bucket gives the exact
+// lower bound.  Returns false, with the coarse range, for a bucket without a
+// slot (>= 2^16 keys): the caller searches it.
+__device__ __forceinline__ bool seed_pos(const int* dir, unsigned long long key, int& pos, int& lo, int& hi) {
+  const unsigned c = (unsigned)(key >> (63 - kDirBits));
+  const int* fslot = dir + (1 << kDirBits) + 2;
+  lo = gp(dir)[c];
+  hi = gp(dir)[c + 1];
+  const int slot = gp(fslot)[c];
+  pos = (lo + hi) >> 1;
+  if (hi - lo <= kFineMin) return true;
+  if (slot < 0) return false;
+  const unsigned short* fine = reinterpret_cast<const unsigned short*>(fslot + (1 << kDirBits));
+  const unsigned f = (unsigned)(key >> (63 - kDirBits - kFineBits)) & ((1u << kFineBits) - 1u);
+  pos = lo + (int)gp(fine)[((size_t)slot << kFineBits) + f];
+  return true;
+}
+
 // Wave-parallel lower_bound of a (uniform) key in the sorted key array:
 // 64 pivots per step, 4 dependent loads for 500k keys instead of 19.
 __device__ __forceinline__ int wave_lower_bound(const unsigned long long* keys, int n, unsigned long long key) {
