@@ -992,9 +992,8 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     bool seeded = false;
     bool large_step = false;   // previous match exists but the pose moved >= 2 cm since
     bool rewindow = false;     // mode 2: previous match's distance AND the Morton window at the new position
-    // coordinates of the point behind vis.bestj when it is already in registers
+    // coordinates of the point behind vis.bestj (every seed step carries them)
     float bpx = 0.f, bpy = 0.f, bpz = 0.f;
-    bool have_bp = true;
     if (have_prev && active) {
       const int j = jprev;
       if (j >= 0) {
@@ -1041,7 +1040,6 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       bpx = rp.x;
       bpy = rp.y;
       bpz = rp.z;
-      have_bp = true;
       seeded = true;
     }
     // Exact seeding for queries without a usable previous correspondence:
@@ -1071,20 +1069,32 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       float4 p[kSeedW];
 #pragma unroll
       for (int k = 0; k < kSeedW; ++k) p[k] = ldg4(tgt.pts, min(max(w0 + k, 0), tgt.n - 1));
+      // the winner's coordinates travel with its key (group sharing below needs no load)
+      float cx = bpx, cy = bpy, cz = bpz;
       if (use_window) {
 #pragma unroll
         for (int k = 0; k < kSeedW; ++k) {
           const int cand = min(max(w0 + k, 0), tgt.n - 1);
-          bk = umin64(bk, dkey(dist2(qx, qy, qz, p[k].x, p[k].y, p[k].z), cand));
+          const unsigned long long kk = dkey(dist2(qx, qy, qz, p[k].x, p[k].y, p[k].z), cand);
+          if (kk < bk) {
+            bk = kk;
+            cx = p[k].x;
+            cy = p[k].y;
+            cz = p[k].z;
+          }
         }
       }
-      vis.merge_slices(bk);
+      static_assert(Q == 16, "slice merge over lanes l ^ 16, l ^ 32");
+      xor_min64_xyz<16>(bk, cx, cy, cz);
+      xor_min64_xyz<32>(bk, cx, cy, cz);
       if (use_window) {
         const float bd = __uint_as_float((unsigned)(bk >> 32));
         if (bd < cap2) {
           vis.best = bd;
           vis.bestj = (int)(unsigned)bk;
-          have_bp = false;   // the winning window point may sit in another slice lane
+          bpx = cx;
+          bpy = cy;
+          bpz = cz;
         }
       }
     }
@@ -1117,18 +1127,28 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         CP[lane] = f4v{p.x, p.y, p.z, __int_as_float(cand)};
         __builtin_amdgcn_wave_barrier();
         unsigned long long bk = dkey(vis.best, vis.bestj);
+        float ux = bpx, uy = bpy, uz = bpz;
         const int s4 = lane / Q;
 #pragma unroll 4
         for (int k = 0; k < 64 / (64 / Q); ++k) {
           const f4v c = CP[s4 * (64 / (64 / Q)) + k];
-          bk = umin64(bk, dkey(dist2(qx, qy, qz, c.x, c.y, c.z), __float_as_int(c.w)));
+          const unsigned long long kk = dkey(dist2(qx, qy, qz, c.x, c.y, c.z), __float_as_int(c.w));
+          if (kk < bk) {
+            bk = kk;
+            ux = c.x;
+            uy = c.y;
+            uz = c.z;
+          }
         }
-        vis.merge_slices(bk);
+        xor_min64_xyz<16>(bk, ux, uy, uz);
+        xor_min64_xyz<32>(bk, ux, uy, uz);
         __builtin_amdgcn_wave_barrier();
         if (active && bk < dkey(vis.best, vis.bestj)) {
           vis.best = __uint_as_float((unsigned)(bk >> 32));
           vis.bestj = (int)(unsigned)bk;
-          have_bp = false;
+          bpx = ux;
+          bpy = uy;
+          bpz = uz;
           seeded = true;
         }
       }
@@ -1140,19 +1160,20 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     {
       const unsigned long long donors = __ballot(lane < Q && active && vis.bestj >= 0);
       if (donors && __any(active)) {
-        float4 bp = make_float4(bpx, bpy, bpz, 0.f);
-        if (__any(!have_bp && vis.bestj >= 0)) {
-          if (!have_bp) bp = ldg4(tgt.pts, max(vis.bestj, 0));
-        }
+        // lane (query qi, slice s) takes donors 4s .. 4s + 3 (read from their
+        // slice-0 lanes), then the four slices merge: 4 distance steps per
+        // lane instead of one per donor
         unsigned long long bk = dkey(vis.best, vis.bestj);
-        unsigned long long m = donors;
-        while (m) {
-          const int k = __builtin_ctzll(m);
-          m &= m - 1;
-          const float sx = readlane_f(bp.x, k), sy = readlane_f(bp.y, k), sz = readlane_f(bp.z, k);
-          const int sj = readlane_i(vis.bestj, k);
-          bk = umin64(bk, dkey(dist2(qx, qy, qz, sx, sy, sz), sj));
+        const int s = lane / Q;
+#pragma unroll 1
+        for (int t = 0; t < 4; ++t) {
+          const int d = s * 4 + t;
+          const float sx = __shfl(bpx, d), sy = __shfl(bpy, d), sz = __shfl(bpz, d);
+          const int sj = __shfl(vis.bestj, d);
+          if ((donors >> d) & 1ull) bk = umin64(bk, dkey(dist2(qx, qy, qz, sx, sy, sz), sj));
         }
+        bk = xor_min64<16>(bk);
+        bk = xor_min64<32>(bk);
         if (active) {
           vis.best = __uint_as_float((unsigned)(bk >> 32));
           vis.bestj = (int)(unsigned)bk;

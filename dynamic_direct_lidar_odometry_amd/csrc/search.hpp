@@ -519,6 +519,31 @@ __device__ __forceinline__ unsigned long long xor_min64(unsigned long long v) {
   return umin64(((unsigned long long)a1 << 32) | a0, ((unsigned long long)b1 << 32) | b0);
 }
 
+// xor_min64 carrying the winning key's point coordinates along (lanes l and
+// l ^ M; equal keys name the same point)
+template <int M>
+__device__ __forceinline__ void xor_min64_xyz(unsigned long long& v, float& x, float& y, float& z) {
+  static_assert(M == 16 || M == 32, "xor_min64_xyz: M = 16 or 32");
+  const unsigned in[5] = {(unsigned)v, (unsigned)(v >> 32), __float_as_uint(x), __float_as_uint(y), __float_as_uint(z)};
+  unsigned a[5], b[5];
+#pragma unroll
+  for (int e = 0; e < 5; ++e) {
+    if constexpr (M == 32) {
+      const auto r = __builtin_amdgcn_permlane32_swap(in[e], in[e], false, false);
+      a[e] = r[0]; b[e] = r[1];
+    } else {
+      const auto r = __builtin_amdgcn_permlane16_swap(in[e], in[e], false, false);
+      a[e] = r[0]; b[e] = r[1];
+    }
+  }
+  const unsigned long long ka = ((unsigned long long)a[1] << 32) | a[0], kb = ((unsigned long long)b[1] << 32) | b[0];
+  const bool ta = ka < kb;
+  v = ta ? ka : kb;
+  x = __uint_as_float(ta ? a[2] : b[2]);
+  y = __uint_as_float(ta ? a[3] : b[3]);
+  z = __uint_as_float(ta ? a[4] : b[4]);
+}
+
 // squared distance of a (distance, position) key
 __device__ __forceinline__ float key_dist(unsigned long long k) { return __uint_as_float((unsigned)(k >> 32)); }
 // a key names a real point (not a bound without one: position 0xffffffff)
