@@ -282,11 +282,18 @@ class Context:
 
     # ---- registration
     def align(self, guess=None):
-        out = np.zeros((4, 4), np.float32)
-        res = GicpResult()
-        g = None if guess is None else np.ascontiguousarray(guess, np.float32)
-        self._check(self.L.gicp_align(self.h, None if g is None else _ptr(g), _ptr(out), C.byref(res)))
-        return out, res
+        # Per-context guess / pose / result buffers with their addresses taken
+        # once: numpy's .ctypes accessors cost ~2-4 us per call, a few percent
+        # of a cfg 3 align.  The caller gets copies.
+        ab = self.__dict__.get("_abuf")
+        if ab is None:
+            gb, ob, rb = np.zeros((4, 4), np.float32), np.zeros((4, 4), np.float32), GicpResult()
+            ab = self._abuf = (gb, ob, rb, gb.ctypes.data, ob.ctypes.data, C.pointer(rb))
+        gb, ob, rb, gp, op, rp = ab
+        if guess is not None:
+            np.copyto(gb, np.reshape(guess, (4, 4)), casting="unsafe")
+        self._check(self.L.gicp_align(self.h, None if guess is None else gp, op, rp))
+        return ob.copy(), GicpResult.from_buffer_copy(rb)
 
     def residuals(self):
         n = self.size(SOURCE)

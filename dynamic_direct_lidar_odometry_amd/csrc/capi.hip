@@ -216,7 +216,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.reuse_rec0 = kn.reuse_rec0;
   j.reuse_rec_eps = kn.reuse_rec_eps;
   j.reuse_rec_conv = kn.reuse_rec_conv;
-  HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
+  // no copy here: k_align_init reads the pinned job and writes the device one
   return GICP_OK;
 }
 
@@ -268,7 +268,9 @@ constexpr int kMaxFirstChunk = 8;  // largest predicted first chunk (iterations)
 // this rank's reduced moments all-reduced across ranks (80 doubles over
 // RCCL: H, b, cost and the LM trial-cost moments in one collective), then
 // the LM/GN step, replicated bit-identically on every rank.
-gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks) {
+// publish: host-mapped state slot the LM step copies the new state to (the
+// last iteration of a chunk), or nullptr.
+gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks, AlignState* publish) {
   (void)nblocks;   // = geometry(c).mom_blocks (fill_job)
   const LinGeom g = geometry(c);
   launch_linearize(c->stream, jd, g);
@@ -276,22 +278,23 @@ gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks) {
     launch_mom_reduce(c->stream, jd);
     NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
   }
-  if (!g.fuse_lm) launch_lm_step(c->stream, jd);
+  if (!g.fuse_lm) launch_lm_step(c->stream, jd, publish);
+  else if (publish) HIP_TRY(hipMemcpyAsync(publish, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
   return GICP_OK;
 }
 
 gicp_status enqueue_chunk(gicp_ctx* c, bool with_init, int iters, int nblocks, int slot) {
-  const AlignJob* jd = c->job_dev.as<AlignJob>();
-  if (with_init) launch_align_init(c->stream, jd);
+  AlignJob* jd = c->job_dev.as<AlignJob>();
+  if (with_init) launch_align_init(c->stream, jd, c->job_host_dev);
+  // the chunk's last LM step publishes the whole state to pinned host
+  // memory: the host polls {iter, done} from it, and once done it already
+  // holds the final pose, so no read-back round trip (and no copy kernel)
+  // follows convergence (a speculative no-op chunk behind it rewrites the
+  // same bytes)
   for (int i = 0; i < iters; ++i) {
-    gicp_status s = enqueue_iteration(c, jd, nblocks);
+    gicp_status s = enqueue_iteration(c, jd, nblocks, i == iters - 1 ? c->state_host_dev + slot : nullptr);
     if (s) return s;
   }
-  // publish the whole state to pinned host memory at the end of the chunk:
-  // the host polls {iter, done} from it, and once done it already holds the
-  // final pose, so no separate read-back round trip follows convergence (a
-  // speculative no-op chunk behind it rewrites the same bytes)
-  HIP_TRY(hipMemcpyAsync(c->state_host + slot, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
   return GICP_OK;
 }
 
@@ -390,8 +393,21 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   // read, at most chunk k + 1 (the other slot) is queued behind it; chunk
   // k + 2 (same slot as k) is launched only after the read.
   int k = 0;
+  // the host polls the chunk's event (hipEventQuery) instead of blocking in
+  // hipEventSynchronize: 2 us less per align at cfg 3 (DDLO_SPIN_WAIT=0: block)
+  static const bool spin = [] {
+    const char* v = std::getenv("DDLO_SPIN_WAIT");
+    return !(v && *v == '0');
+  }();
   for (;;) {
-    HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
+    if (spin) {
+      hipError_t q;
+      while ((q = hipEventQuery(c->chunk_ev[k])) == hipErrorNotReady) {
+      }
+      HIP_TRY(q);
+    } else {
+      HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
+    }
     const volatile AlignState* st = c->state_host + (k & 1);
     if (st->done || k == nchunks - 1) break;
     while (launched < nchunks && launched <= k + 2) {  // keep one chunk queued ahead of k+1
@@ -415,14 +431,14 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
 }
 
 gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
-  const AlignJob* jd = c->job_dev.as<AlignJob>();
+  AlignJob* jd = c->job_dev.as<AlignJob>();
   const size_t need = 2 * (size_t)max_it;
   while (c->prof_ev.size() < need) {
     hipEvent_t e;
     HIP_TRY(hipEventCreate(&e));
     c->prof_ev.push_back(e);
   }
-  launch_align_init(c->stream, jd);
+  launch_align_init(c->stream, jd, c->job_host_dev);
   for (int i = 0; i < max_it; ++i) {
     HIP_TRY(hipEventRecord(c->prof_ev[2 * i], c->stream));
     LinGeom g = geometry(c);
@@ -433,7 +449,7 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
       launch_mom_reduce(c->stream, jd);
       NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
     }
-    launch_lm_step(c->stream, jd);
+    launch_lm_step(c->stream, jd, nullptr);
   }
   HIP_TRY(hipGetLastError());
   return GICP_OK;
@@ -484,8 +500,10 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming));
-  HIP_TRY(hipHostMalloc((void**)&c->job_host, sizeof(AlignJob), hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&c->state_host, 2 * sizeof(AlignState), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&c->job_host, sizeof(AlignJob), hipHostMallocMapped));
+  HIP_TRY(hipHostMalloc((void**)&c->state_host, 2 * sizeof(AlignState), hipHostMallocMapped));
+  HIP_TRY(hipHostGetDevicePointer((void**)&c->job_host_dev, c->job_host, 0));
+  HIP_TRY(hipHostGetDevicePointer((void**)&c->state_host_dev, c->state_host, 0));
   HIP_TRY(hipHostMalloc((void**)&c->flag_host, sizeof(int) * 4, hipHostMallocDefault));
   HIP_TRY(c->job_dev.ensure(sizeof(AlignJob)));
   HIP_TRY(c->state_dev.ensure(sizeof(AlignState)));
@@ -699,7 +717,7 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
   if (c->profiling || max_it <= 0) {
     s = max_it > 0 ? run_align_eager_profiled(c, max_it, nblocks) : GICP_OK;
     if (s) return s;
-    if (max_it <= 0) launch_align_init(c->stream, c->job_dev.as<AlignJob>());
+    if (max_it <= 0) launch_align_init(c->stream, c->job_dev.as<AlignJob>(), c->job_host_dev);
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -875,10 +893,9 @@ gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, doubl
   c->job_host->optimizer = GICP_OPT_GAUSS_NEWTON;
   c->job_host->max_iterations = 1;
   c->job_host->fixed_iterations = 1;
-  HIP_TRY(hipMemcpyAsync(c->job_dev.p, c->job_host, sizeof(AlignJob), hipMemcpyHostToDevice, c->stream));
-  const AlignJob* jd = c->job_dev.as<AlignJob>();
-  launch_align_init(c->stream, jd);
-  s = enqueue_iteration(c, jd, nblocks);
+  AlignJob* jd = c->job_dev.as<AlignJob>();
+  launch_align_init(c->stream, jd, c->job_host_dev);
+  s = enqueue_iteration(c, jd, nblocks, nullptr);
   if (s) return s;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));

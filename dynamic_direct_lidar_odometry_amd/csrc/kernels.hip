@@ -802,7 +802,26 @@ constexpr int kLinWaves = 4;      // waves per block (search and moment kernels)
 constexpr int kSearchQ = 16;        // queries per wavefront in the correspondence search
 constexpr int kSeedW = 8;           // Morton-window seed points per slice lane
 
-__global__ __launch_bounds__(256) void k_align_init(const AlignJob* __restrict__ job) {
+// job_src (optional): the host's pinned AlignJob.  The block copies it to the
+// device job (8-byte words) and initialises from its LDS copy, so an align
+// needs no separate host-to-device copy before its first kernel.
+__global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_dev,
+                                                    const AlignJob* __restrict__ job_src) {
+  static_assert(sizeof(AlignJob) % 8 == 0, "AlignJob is copied in 8-byte words");
+  __shared__ unsigned long long job_lds[sizeof(AlignJob) / 8];
+  const AlignJob* job = job_dev;
+  if (job_src) {
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(job_src);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(job_dev);
+    for (int w = threadIdx.x; w < (int)(sizeof(AlignJob) / 8); w += blockDim.x) {
+      // system scope: read past every GPU cache (the host rewrites this buffer per align)
+      const unsigned long long v = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      job_lds[w] = v;
+      dst[w] = v;
+    }
+    __syncthreads();
+    job = reinterpret_cast<const AlignJob*>(job_lds);
+  }
   AlignState* st = job->state;
   if (threadIdx.x <= kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;   // + the moment kernel's arrival counter
   if (threadIdx.x < 64) {   // source radius from the top-level boxes (<= 64 of them)
@@ -2467,9 +2486,20 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job) {
 #endif
 }
 
-__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job) {
-  if (__builtin_amdgcn_readfirstlane(job->state->done)) return;
-  lm_step_body(job);
+// publish (optional): a host-mapped AlignState the block copies the final
+// state of this step to (also after an early exit), so the host reads a
+// chunk's result from pinned memory without a device-to-host copy.
+__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job,
+                                                        AlignState* __restrict__ publish) {
+  if (!__builtin_amdgcn_readfirstlane(job->state->done)) lm_step_body(job);
+  if (publish) {
+    static_assert(sizeof(AlignState) % 16 == 0, "AlignState is copied in 16-byte words");
+    __threadfence();   // this block's state stores, then an L1 invalidate before they are read back
+    __syncthreads();
+    const int4* src = reinterpret_cast<const int4*>(job->state);
+    int4* dst = reinterpret_cast<int4*>(publish);
+    for (int w = threadIdx.x; w < (int)(sizeof(AlignState) / 16); w += blockDim.x) dst[w] = src[w];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2691,7 +2721,9 @@ void launch_cov_remap(hipStream_t s, const double* old_cov6, const int* old_inv_
                       double* cov6) {
   k_cov_remap<<<cdiv(n, 256), 256, 0, s>>>(old_cov6, old_inv_perm, new_perm, n, cov6);
 }
-void launch_align_init(hipStream_t s, const AlignJob* job) { k_align_init<<<1, 128, 0, s>>>(job); }
+void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src) {
+  k_align_init<<<1, 128, 0, s>>>(job, job_src);
+}
 size_t search_lds_bytes(int upper_count) {
   return (size_t)kLinWaves * kCollectLdsBytes + 2 * sizeof(f4v) * (size_t)upper_count;
 }
@@ -2766,7 +2798,9 @@ int moment_blocks(int nsrc) {
   const int groups = (nsrc + 63) / 64;
   return std::max(1, std::min((groups + kMomWaves - 1) / kMomWaves, kMomBlocksMax));
 }
-void launch_lm_step(hipStream_t s, const AlignJob* job) { k_lm_step<<<1, kLmThreads, 0, s>>>(job); }
+void launch_lm_step(hipStream_t s, const AlignJob* job, AlignState* publish) {
+  k_lm_step<<<1, kLmThreads, 0, s>>>(job, publish);
+}
 void launch_mom_reduce(hipStream_t s, const AlignJob* job) { k_mom_reduce<<<1, kLmThreads, 0, s>>>(job); }
 void launch_residual_image(hipStream_t s, const float4* pts, const int* perm, const int* inv_perm, int n,
                            const double* residual, double tmin, double tmax, int W, int H, int* winner, float* img,

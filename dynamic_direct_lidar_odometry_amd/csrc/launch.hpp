@@ -43,7 +43,7 @@ bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq,
                       TieList ties = TieList{nullptr, nullptr});
 void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6);
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);
-void launch_align_init(hipStream_t s, const AlignJob* job);
+void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src);
 // tgt_upper: number of upper-level (>= 1) boxes of the target (LDS cache size)
 // Launch geometry of one linearize (grids, upper-box LDS cache), bucketed by
 // cloud size; part of the chunk-graph key.
@@ -58,7 +58,7 @@ int search_queries_per_wave();
 bool search_uses_tasks();   // false under DDLO_SEARCH=collect (the single-kernel search)
 int task_cap_per_region(int nsrc);   // task-list slots per region for nsrc source points
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
-void launch_lm_step(hipStream_t s, const AlignJob* job);
+void launch_lm_step(hipStream_t s, const AlignJob* job, AlignState* publish);
 void launch_mom_reduce(hipStream_t s, const AlignJob* job);  // sharded align: slab -> job->mom
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out);
 void launch_residual_image(hipStream_t s, const float4* pts, const int* perm, const int* inv_perm, int n,
