@@ -629,6 +629,13 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
                           cv->cov6.as<double>(), side.cloud->nf->status.as<int>(), c->nf_err.as<int>());
     gicp_status st = publish_ties(c, c->stream);
     if (st) return st;
+    static const bool dbg = std::getenv("DDLO_TIE_DEBUG") != nullptr;   // development: tied queries per cloud
+    if (dbg) {
+      int cnt = 0;
+      HIP_TRY(hipMemcpyAsync(&cnt, tl.count, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      std::fprintf(stderr, "[ties] n %d k %d tied %d\n", side.cloud->n, k, cnt);
+    }
   }
   HIP_TRY(hipGetLastError());
   side.cov = cv;

@@ -31,6 +31,7 @@ c.compute_covariances(SOURCE)
 c.compute_covariances(TARGET)
 guess = prob["guess"].astype(np.float32)
 prev = None
+dump = {}
 for it in (1, 2, 3):
     c.set_params(default_params(k_correspondences=10, max_correspondence_distance=2.0, max_iterations=it,
                                 transformation_epsilon=1e-9))
@@ -47,6 +48,16 @@ for it in (1, 2, 3):
     print(f"iter {it - 1}: sub-groups {ng}, cycles mean {cyc.mean():.0f} p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} "
           f"p99.9 {q[3]:.0f} max {cyc.max():.0f}; sum/4096 slots {cyc.sum() / 4096:.0f}; block-max sum/1024 "
           f"{blk.sum() / 1024:.0f}; list-schedule makespan {ms:.0f}; tasks {tasks.sum():.0f}")
+    wav = makespan(cyc, 4096)
+    msg = f"   per-wave dynamic fetch, index order: {wav:.0f}"
+    if prev is not None:
+        lpt = makespan(cyc[np.argsort(-prev, kind="stable")], 4096)
+        msg += f"; heaviest-previous first: {lpt:.0f}"
+    msg += f"; oracle LPT: {makespan(np.sort(cyc)[::-1], 4096):.0f}"
+    print(msg)
+    dump[f"cyc{it - 1}"] = cyc
+    dump[f"tasks{it - 1}"] = tasks
+    dump[f"blocks{it - 1}"] = st[:, 0].astype(np.float64)
     order = np.argsort(-cyc)
     for H in (16, 64, 256):
         for P in (4, 8):
@@ -62,3 +73,5 @@ for it in (1, 2, 3):
         print(f"   top-64 overlap with the previous iteration: {len(a & b)}")
     prev = cyc
 c.debug_stats(False)
+os.makedirs("gpurun_out", exist_ok=True)
+np.savez("gpurun_out/tail_sim.npz", **dump)
