@@ -345,12 +345,16 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ b
   const NfTask& tk = v.tk;
   const int feat = tk.feat;
   const float cut = tk.cut;
-  int lim1, before1, lim2, before2;
+  int lim1, before1, lim2 = 0, before2;
   task_chunk_sums(b.cA, tk, v.blk, &lim1, &before1, sh);
   int before = before1;
   int zlo = 0, zhi = lim1;   // the "good" zone [zlo, zhi) of this pass
+  if (PASS == 2 || !TABLE) task_chunk_sums(b.cAE, tk, v.blk, &lim2, &before2, sh);
+  // no element equals the cut (most nodes): pass 2 swaps nothing, and pass
+  // 1's apply already finished the node (its children and record)
+  const bool pass2_empty = lim2 == lim1;
   if (PASS == 2) {
-    task_chunk_sums(b.cAE, tk, v.blk, &lim2, &before2, sh);
+    if (pass2_empty) return;
     task_chunk_sums(b.cE2, tk, v.blk, &before2, &before, sh);   // E after pass 1: none before lim1
     zlo = lim1;
     zhi = lim2;
@@ -406,7 +410,7 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ b
     ecount = block_sum(ecount, sh);
     if (threadIdx.x == 0) b.cE2[v.blk] = ecount;
   }
-  if (!TABLE && PASS == 2) {
+  if (!TABLE && (PASS == 2 || pass2_empty)) {
     // the split index, the children's point min / max, and (one thread per
     // task) the node record and the children's pending entries
     const int index = nf_index(tk.count, lim1, lim2);
@@ -616,7 +620,8 @@ __device__ int wave_split(const NfBuild& b, float4* Q, IT* ML, IT* MR, int cap, 
     lim2 += __popcll(__ballot(i < n && x <= cut));
   }
   if (!wave_pass(Q, ML, MR, cap, 0, lim1, n, feat, cut, false, ctl)) return -1;
-  if (!wave_pass(Q, ML, MR, cap, lim1, lim2, n, feat, cut, true, ctl)) return -1;
+  // pass 2 swaps nothing when no element equals the cut (most nodes)
+  if (lim2 > lim1 && !wave_pass(Q, ML, MR, cap, lim1, lim2, n, feat, cut, true, ctl)) return -1;
   const int index = nf_index(n, lim1, lim2);
   if (lane == 0) {
     b.nodes[nd.node].c1 = c1;
@@ -819,7 +824,20 @@ __device__ void group_depth(const NfBuild& b, SubLds& S, int cur, int nq, int ba
     }
   unsigned short* cnt = S.ML + 256 * (has ? j : 0);
   group_pass(Q, S.ML + nd.lb / 2, S.MR + nd.lb / 2, cnt, act, gw, G, 0, lim1, nd.n, feat, cut, false, b.ctl);
-  group_pass(Q, S.ML + nd.lb / 2, S.MR + nd.lb / 2, cnt, act, gw, G, lim1, lim2, nd.n, feat, cut, true, b.ctl);
+  // pass 2 (barriers inside: a workgroup-uniform decision) only if a node of
+  // this depth has elements equal to its cut
+  bool need2 = false;
+  for (int jj = 0; jj < nq; ++jj) {
+    int l1 = 0, l2 = 0;
+    for (int g = 0; g < G; ++g) {
+      l1 += S.gcnt[jj * G + g][0];
+      l2 += S.gcnt[jj * G + g][1];
+    }
+    need2 |= !S.gleaf[jj] && l2 > l1;
+  }
+  if (need2)
+    group_pass(Q, S.ML + nd.lb / 2, S.MR + nd.lb / 2, cnt, act && lim2 > lim1, gw, G, lim1, lim2, nd.n, feat, cut, true,
+               b.ctl);
   if (act && gw == 0 && lane == 0) {
     const int index = nf_index(nd.n, lim1, lim2);
     const int c1 = atomicAdd(&S.next_id, 2);
