@@ -544,6 +544,8 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   (void)hipStreamDestroy(c->stream);
   (void)hipStreamSynchronize(c->aux_stream);
   if (c->nf_graph) (void)hipGraphExecDestroy(c->nf_graph);
+  if (c->nf_ntask_host) (void)hipHostFree(c->nf_ntask_host);
+  if (c->nf_ntask_ev) (void)hipEventDestroy(c->nf_ntask_ev);
   (void)hipStreamDestroy(c->aux_stream);
   (void)hipEventDestroy(c->aux_ev);
   delete c;

@@ -193,6 +193,7 @@ struct NfTreeDev {
 };
 
 constexpr int kNfMaxLevels = 40;   // big levels of the device build (deeper: the build reports a failure)
+constexpr int kNfLevelSpare = 2;   // big levels a ctx's build carries beyond those its last build used
 
 struct NfCtl {
   int nnodes, nsmall, err;   // err bits: 1 node capacity, 4 depth, 8 list capacity, 16/32 pairing checks

@@ -258,8 +258,23 @@ struct gicp_ctx {
   hipStream_t aux_stream = nullptr;
   hipEvent_t aux_ev = nullptr;
   DevBuf nf_desc;                    // the build descriptor the tree kernels read
-  hipGraphExec_t nf_graph = nullptr;  // the build, captured for one size bucket
-  int nf_graph_key = -1;
+  hipGraphExec_t nf_graph = nullptr;  // the build, captured for one size bucket and level count
+  long long nf_graph_key = -1;
+  // Big levels the builds of this ctx need: the level counts of each build
+  // (ctl->ntask, copied to pinned memory after it) set later builds of the
+  // size bucket to the most levels any of them used + kNfLevelSpare, so
+  // that the graph does not carry ~6 kernels per level that finds no node to
+  // split.  A cloud that needs more levels is still exact (its larger nodes
+  // go to k_nf_small_global, slowly) and sends the next build back to the
+  // full margin.
+  int* nf_ntask_host = nullptr;       // pinned [kNfMaxLevels + 1]
+  hipEvent_t nf_ntask_ev = nullptr;   // the copy's completion
+  int nf_ntask_bucket = -1, nf_ntask_lmax = 0;   // the build the copy belongs to
+  int nf_hint_bucket = -1, nf_hint = 0, nf_used_max = 0;   // the next build's level count for that bucket
+  // a copied level count is ready to read (its build completed)
+  bool nf_ntask_pending_check() const {
+    return nf_ntask_bucket >= 0 && nf_ntask_ev && hipEventQuery(nf_ntask_ev) == hipSuccess;
+  }
   bool profiling = false;
   std::vector<hipEvent_t> prof_ev;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -409,6 +424,23 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   // device memory), so a build is one graph launch, not ~80 kernel launches
   const int nbucket = (int)(((long)n + 16383) / 16384 * 16384);
   const NfSizes z = nf_sizes(nbucket);
+  // the level count: the full margin for diagnostics builds, else from the
+  // last completed build of this bucket on this ctx
+  if (c->nf_ntask_pending_check()) {
+    int used = 0;
+    while (used < c->nf_ntask_lmax && c->nf_ntask_host[used] > 0) ++used;
+    if (c->nf_hint_bucket != c->nf_ntask_bucket) c->nf_used_max = 0;
+    c->nf_hint_bucket = c->nf_ntask_bucket;
+    if (used >= c->nf_ntask_lmax) {
+      c->nf_hint = 0;   // every level had nodes to split: measure again with the full margin
+    } else {
+      c->nf_used_max = std::max(c->nf_used_max, used);
+      c->nf_hint = c->nf_used_max + kNfLevelSpare;
+    }
+    c->nf_ntask_bucket = -1;
+  }
+  int Lmax = z.Lmax;
+  if (stop < 0 && !off && c->nf_hint_bucket == nbucket && c->nf_hint > 0) Lmax = std::min(z.Lmax, c->nf_hint);
   t->cap = z.big_ids + 2 * n;   // big-level ids, then 2 per point for the small subtrees' ranges
   HIP_TRY(t->vpts.ensure(sizeof(float4) * (size_t)n));
   HIP_TRY(t->nodes.ensure(sizeof(NfNode) * (size_t)t->cap));
@@ -446,14 +478,14 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   b.sorted = cd.pts.as<float4>();
   b.n = n;
   b.nbucket = nbucket;
-  b.Lmax = z.Lmax;
+  b.Lmax = Lmax;
   b.max_task = z.max_task;
   b.max_pend = z.max_pend;
   b.max_small = z.max_small;
   b.max_chunks = z.max_chunks;
   b.big_ids = z.big_ids;
   if (off) {
-    const long long v[16] = {z.Lmax, z.max_task, z.max_pend, z.max_small, z.max_chunks, (long long)o_tasks,
+    const long long v[16] = {Lmax, z.max_task, z.max_pend, z.max_small, z.max_chunks, (long long)o_tasks,
                              (long long)o_pend, (long long)o_small, (long long)o_cmap, (long long)o_cA,
                              (long long)o_cAE, (long long)o_cE2, (long long)o_tblL, (long long)total, n, t->cap};
     for (int i = 0; i < 16; ++i) off[i] = v[i];
@@ -466,7 +498,8 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
     launch_nf_build(s, b, db, stop);
     HIP_TRY(hipGetLastError());
   } else {
-    if (c->nf_graph_key != nbucket) {
+    const long long gkey = (long long)nbucket * 64 + Lmax;
+    if (c->nf_graph_key != gkey) {
       if (c->nf_graph) HIP_TRY(hipGraphExecDestroy(c->nf_graph));
       c->nf_graph = nullptr;
       c->nf_graph_key = -1;
@@ -480,9 +513,19 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
       const hipError_t e3 = hipGraphInstantiate(&c->nf_graph, g, nullptr, nullptr, 0);
       (void)hipGraphDestroy(g);
       HIP_TRY(e3);
-      c->nf_graph_key = nbucket;
+      c->nf_graph_key = gkey;
     }
     HIP_TRY(hipGraphLaunch(c->nf_graph, s));
+  }
+  if (stop < 0 && !off) {   // the level counts of this build, for the next one
+    if (!c->nf_ntask_host) {
+      HIP_TRY(hipHostMalloc((void**)&c->nf_ntask_host, sizeof(int) * (kNfMaxLevels + 1), hipHostMallocDefault));
+      HIP_TRY(hipEventCreateWithFlags(&c->nf_ntask_ev, hipEventDisableTiming));
+    }
+    HIP_TRY(hipMemcpyAsync(c->nf_ntask_host, b.ctl->ntask, sizeof(int) * (kNfMaxLevels + 1), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(c->nf_ntask_ev, s));
+    c->nf_ntask_bucket = nbucket;
+    c->nf_ntask_lmax = Lmax;
   }
   HIP_TRY(hipMemcpyAsync(t->status.p, &b.ctl->err, sizeof(int), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(t->status.as<int>() + 1, &b.ctl->nnodes, sizeof(int), hipMemcpyDeviceToDevice, s));
