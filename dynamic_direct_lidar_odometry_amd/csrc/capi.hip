@@ -575,12 +575,15 @@ gicp_status gicp_get_params(const gicp_ctx* c, gicp_params* out) {
   return GICP_OK;
 }
 
-gicp_status gicp_set_source(gicp_ctx* c, const float* xyz, size_t n, size_t stride, int build_index) {
+namespace {
+// nf_early: the caller computes the source covariances next (gicp_s2s_batch),
+// so nanoflann's tree starts with the index build
+gicp_status set_source_impl(gicp_ctx* c, const float* xyz, size_t n, size_t stride, int build_index, bool nf_early) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
   gicp_status s = set_device(c);
   if (s) return s;
   std::shared_ptr<CloudData> cd;
-  s = build_cloud(c, xyz, n, stride, &cd);   // the device cloud is always sorted + indexed (cheap)
+  s = build_cloud(c, xyz, n, stride, &cd, false, true, nf_early);   // the device cloud is always sorted + indexed (cheap)
   if (s) return s;
   const Side old = c->src;
   c->src.cloud = cd;
@@ -600,6 +603,11 @@ gicp_status gicp_set_source(gicp_ctx* c, const float* xyz, size_t n, size_t stri
   }
   invalidate_align(c);
   return GICP_OK;
+}
+}  // namespace
+
+gicp_status gicp_set_source(gicp_ctx* c, const float* xyz, size_t n, size_t stride, int build_index) {
+  return set_source_impl(c, xyz, n, stride, build_index, false);
 }
 
 gicp_status gicp_set_target(gicp_ctx* c, const float* xyz, size_t n, size_t stride) {
@@ -1170,7 +1178,7 @@ gicp_status gicp_s2s_batch(int device, const gicp_params* p, const float* const*
     gicp_ctx* c = ctxs[w];
     gicp_status s = gicp_set_target(c, clouds[t0 - 1], sizes[t0 - 1], stride_bytes);
     for (int t = t0; t < t1 && !s; ++t) {
-      s = gicp_set_source(c, clouds[t], sizes[t], stride_bytes, 1);
+      s = set_source_impl(c, clouds[t], sizes[t], stride_bytes, 1, true);
       if (!s) s = gicp_align(c, nullptr, out16 + 16 * (size_t)t, res ? &res[t] : nullptr);
       if (!s) s = gicp_swap_source_target(c);  // scan t becomes the next target (odom.cc:768)
     }

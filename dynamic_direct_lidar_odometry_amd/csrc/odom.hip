@@ -536,10 +536,13 @@ gicp_status preprocess(ddlo_odom* o, int n, bool crop, double crop_size, bool vo
 
 // device cloud from float4 points; `finite`: the points are known finite (a
 // voxel filter's output, keyframes, the submap), no read-back of the check
+// with_cov: covariances follow (the scan, a keyframe), so nanoflann's tree
+// for their tie order starts with the index build (not for the submap,
+// whose covariances are the keyframes')
 gicp_status cloud_from(ddlo_odom* o, gicp_ctx* c, const float4* pts, int n, std::shared_ptr<CloudData>* out,
-                       bool finite) {
+                       bool finite, bool with_cov) {
   (void)o;
-  return build_cloud(c, reinterpret_cast<const float*>(pts), (size_t)n, sizeof(float4), out, true, !finite);
+  return build_cloud(c, reinterpret_cast<const float*>(pts), (size_t)n, sizeof(float4), out, true, !finite, with_cov);
 }
 
 // keyframe = world-frame copy of the (preprocessed) scan cloud, submap voxel
@@ -561,7 +564,7 @@ gicp_status make_keyframe(ddlo_odom* o, const std::shared_ptr<CloudData>& scan) 
   HIP_TRY(kf->pts.ensure(sizeof(float4) * (size_t)m));
   HIP_TRY(hipMemcpyAsync(kf->pts.p, o->a.p, sizeof(float4) * (size_t)m, hipMemcpyDeviceToDevice, o->s));
   Side side;
-  st = cloud_from(o, o->s2s, kf->pts.as<float4>(), m, &side.cloud, true);
+  st = cloud_from(o, o->s2s, kf->pts.as<float4>(), m, &side.cloud, true, true);
   if (st) return st;
   // s2s->params: the S2S k (gicp_s2s_.calculateSourceCovariances); a
   // keyframe smaller than k uses all of its points (the reference reads
@@ -623,7 +626,7 @@ gicp_status submap_keyframes(ddlo_odom* o, bool* changed) {
     off += kf.n;
   }
   Side tgt;
-  gicp_status st = cloud_from(o, o->s2m, o->cat_pts.as<float4>(), (int)total, &tgt.cloud, true);
+  gicp_status st = cloud_from(o, o->s2m, o->cat_pts.as<float4>(), (int)total, &tgt.cloud, true, false);
   if (st) return st;
   auto cv = std::make_shared<CovData>();
   cv->n = (int)total;
@@ -813,7 +816,7 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
   }
   // the preprocessed scan as a device cloud (finite after the voxel filter)
   std::shared_ptr<CloudData> scan;
-  st = cloud_from(o, o->s2s, o->a.as<float4>(), m, &scan, o->p.vf_scan_use != 0);
+  st = cloud_from(o, o->s2s, o->a.as<float4>(), m, &scan, o->p.vf_scan_use != 0, true);
   if (st) return st;
   mark(2);
 

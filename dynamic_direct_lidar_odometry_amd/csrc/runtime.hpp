@@ -334,8 +334,13 @@ inline hipError_t grow(DevBuf& b, size_t bytes, hipStream_t s) {
 // on_device (e.g. a preprocessed scan or a keyframe of the odometry driver).
 // check_finite = false (device clouds known finite): no read-back, and the
 // call returns without waiting for the build.
+inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s);
+
+// nf_early: start nanoflann's tree of the cloud (ctx's aux stream) as soon
+// as its sorted points exist, beside the rest of the index build -- for a
+// cloud whose covariances follow (the odometry driver's scans and keyframes)
 inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t stride, std::shared_ptr<CloudData>* out,
-                               bool on_device = false, bool check_finite = true) {
+                               bool on_device = false, bool check_finite = true, bool nf_early = false) {
   if (!xyz || n == 0 || stride < 12 || (stride % 4) != 0) return fail(GICP_EINVAL, "invalid cloud (null, empty or bad stride)");
   if (n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "cloud too large");
   auto cd = std::make_shared<CloudData>();
@@ -382,6 +387,10 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(cd->pts.ensure(sizeof(float4) * npad));
   HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
   launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
+  if (nf_early && c->tie_exact) {
+    gicp_status st = ensure_nftree(c, *cd, s);
+    if (st) return st;
+  }
   HIP_TRY(cd->dir.ensure(sizeof(int) * (size_t)fine_dir_ints(N)));
   launch_key_dir(s, cd->keys.as<unsigned long long>(), N, cd->dir.as<int>());
   HIP_TRY(cd->soa.ensure(sizeof(float) * 3 * (size_t)npad));
