@@ -223,6 +223,7 @@ struct NfBuild {
   NfTask* pend;            // [(Lmax + 1) * max_pend] children produced by the level above
   NfTask* small;           // [max_small]
   int* chunk_task;         // [2 * max_chunks]
+  NfTask* ctask;           // [2 * max_chunks] per chunk: a copy of its task (pad = the task index), one load
   int *cA, *cAE, *cE2;     // [max_chunks] per-chunk counts
   float4 *tblL, *tblR;     // [n] rank tables of the Hoare pairing
   const float* quant;      // the cloud's bbox: min [0..2], max [4..6]

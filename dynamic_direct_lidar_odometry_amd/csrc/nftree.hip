@@ -159,13 +159,16 @@ struct TaskView {   // a big-level block's task and chunk
   int t, c, blk;
   NfTask tk;
 };
+// The block's chunk and task: the map kernel's per-chunk task copy and the
+// chunk count are independent loads (one round trip).  The copy's feat /
+// cut are not the count kernel's: the pass kernels recompute the cut.
 __device__ __forceinline__ bool task_of_block(const NfBuild& b, int L, TaskView* v) {
   const int par = L & 1;
   const int blk = blockIdx.x;
+  v->tk = b.ctask[par * b.max_chunks + blk];   // grid = max_chunks: in bounds
   if (blk >= b.ctl->nchunks[par]) return false;
   v->blk = blk;
-  v->t = b.chunk_task[par * b.max_chunks + blk];
-  v->tk = b.tasks[(size_t)L * b.max_task + v->t];
+  v->t = v->tk.pad;
   v->c = blk - v->tk.chunk0;
   return true;
 }
@@ -280,6 +283,7 @@ __global__ __launch_bounds__(1024) void k_nf_map(const NfBuild* __restrict__ bp,
   // chunk -> task map (tasks are in chunk0 order)
   const int nchunks = min(s_ch, b.max_chunks);
   int* cmap = b.chunk_task + (L & 1) * b.max_chunks;
+  NfTask* ct = b.ctask + (L & 1) * b.max_chunks;
   for (int c = threadIdx.x; c < nchunks; c += blockDim.x) {
     int lo = 0, hi = nbig - 1;
     while (lo < hi) {   // last task with chunk0 <= c
@@ -288,6 +292,9 @@ __global__ __launch_bounds__(1024) void k_nf_map(const NfBuild* __restrict__ bp,
       else hi = mid - 1;
     }
     cmap[c] = lo;
+    NfTask e = T[lo];
+    e.pad = lo;
+    ct[c] = e;
   }
   // the children this level will produce: their min / max start empty
   NfTask* C = b.pend + (size_t)(L + 1) * b.max_pend;
@@ -343,8 +350,20 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ b
   TaskView v;
   if (!task_of_block(b, L, &v)) return;
   const NfTask& tk = v.tk;
-  const int feat = tk.feat;
-  const float cut = tk.cut;
+  int feat;
+  float cut;
+  nf_cut(tk, &feat, &cut);   // the count kernel's cut (a pure function of the task)
+  // pass 1: the chunk's points first, their loads overlap the count sums'
+  // (pass 2 loads them after its early exit: most nodes skip it)
+  const int p0 = v.c * kNfCH + threadIdx.x * kNfPer;
+  float4 e[kNfPer];
+  if constexpr (PASS == 1) {
+#pragma unroll
+    for (int j = 0; j < kNfPer; ++j) {
+      const int p = p0 + j;
+      if (p < tk.count) e[j] = b.vpts[tk.begin + p];
+    }
+  }
   int lim1, before1, lim2 = 0, before2;
   task_chunk_sums(b.cA, tk, v.blk, &lim1, &before1, sh);
   int before = before1;
@@ -360,14 +379,12 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ b
     zhi = lim2;
   }
   const int ngood = zhi - zlo;
-  const int p0 = v.c * kNfCH + threadIdx.x * kNfPer;
-  float4 e[kNfPer];
   int cnt = 0;
 #pragma unroll
   for (int j = 0; j < kNfPer; ++j) {
     const int p = p0 + j;
     if (p < tk.count) {
-      e[j] = b.vpts[tk.begin + p];
+      if constexpr (PASS == 2) e[j] = b.vpts[tk.begin + p];
       const float x = coord(e[j], feat);
       cnt += PASS == 1 ? (x < cut) : (x == cut);
     }

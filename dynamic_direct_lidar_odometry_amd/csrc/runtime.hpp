@@ -465,7 +465,8 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
                o_cE2 = o_cAE + al(sizeof(int) * (size_t)z.max_chunks),
                o_tblL = o_cE2 + al(sizeof(int) * (size_t)z.max_chunks),
                o_tblR = o_tblL + al(sizeof(float4) * (size_t)nbucket),
-               total = o_tblR + al(sizeof(float4) * (size_t)nbucket);
+               o_ctask = o_tblR + al(sizeof(float4) * (size_t)nbucket),
+               total = o_ctask + al(sizeof(NfTask) * 2 * (size_t)z.max_chunks);
   HIP_TRY(grow(c->nf_scratch, total, s));
   char* u = c->nf_scratch.as<char>();
   NfBuild b;
@@ -478,6 +479,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   b.pend = reinterpret_cast<NfTask*>(u + o_pend);
   b.small = reinterpret_cast<NfTask*>(u + o_small);
   b.chunk_task = reinterpret_cast<int*>(u + o_cmap);
+  b.ctask = reinterpret_cast<NfTask*>(u + o_ctask);
   b.cA = reinterpret_cast<int*>(u + o_cA);
   b.cAE = reinterpret_cast<int*>(u + o_cAE);
   b.cE2 = reinterpret_cast<int*>(u + o_cE2);

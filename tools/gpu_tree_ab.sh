@@ -15,3 +15,7 @@ for S in; do
   DDLO_GICP_LIB=ab/libC.so timeout -k 10 300 python -u bench.py --no-cpu --no-sharded --no-gn --no-seg --no-odom --steps 20 --batch-frames 300 --batch-streams $S > gpurun_out/tree_s.json 2> gpurun_out/tree_s.err || { echo "BENCH_FAIL streams $S"; tail -5 gpurun_out/tree_s.err; exit 1; }
   python3 -c "import json; d=json.load(open('gpurun_out/tree_s.json')); b=d['batched_s2s']; print('C streams $S batch ms/pair', b['ms_per_pair'])"
 done
+if [ -n "$NFTRACE" ]; then
+  DDLO_GICP_LIB=ab/libC.so timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/nft -o run -- python3 tools/time_cov.py > gpurun_out/nft.log 2>&1 || { tail -5 gpurun_out/nft.log; exit 1; }
+  python3 tools/nf_trace.py gpurun_out/nft/run_kernel_trace.csv | tail -14
+fi
