@@ -430,8 +430,8 @@ def main():
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--cpu-runs", type=int, default=10, help="oracle align runs for cpu_baseline (median)")
     ap.add_argument("--cpu-warmup", type=int, default=2, help="untimed oracle aligns before them")
     ap.add_argument("--no-cpu", action="store_true")

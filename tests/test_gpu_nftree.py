@@ -147,3 +147,20 @@ def test_device_build_levels_match_emulator(name):
     v_full = nf_emu.build(pts, Lmax=Ldev)
     print("full same", np.array_equal(vind, v_full))
     assert first_bad is None and st[0] == 0 and np.array_equal(vind, v_full)
+
+
+def test_tree_level_count_across_clouds():
+    """A ctx's builds carry only the big levels its earlier builds of the size
+    bucket used (+2).  A later cloud of the same bucket that needs more
+    (log-uniform x: the box midpoint peels ~10 % of a node off per level)
+    goes through the global-memory fallback for its large nodes and must
+    still equal the oracle's tree; the cloud after it is exact too."""
+    rng = np.random.default_rng(11)
+    normal = (rng.standard_normal((45000, 3)) * [20, 20, 3]).astype(np.float32)
+    logu = np.stack([10.0 ** rng.uniform(0, 3, 44000), rng.standard_normal(44000), rng.standard_normal(44000)],
+                    1).astype(np.float32)
+    normal2 = (rng.standard_normal((46000, 3)) * [15, 25, 2]).astype(np.float32)
+    c = P.Context(0)
+    for pts in (normal, normal2, logu, normal, logu):
+        c.set_target(pts)
+        assert O.same_tree(c.nftree(TARGET), O.tree(pts)) is None
