@@ -1,7 +1,7 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 120 python3 tools/time_cfg3.py || exit 1
-DDLO_GICP_LIB=$PWD/dynamic_direct_lidar_odometry_amd/_lib/lmprof/libddlo_gicp.so timeout -k 10 120 python3 tools/time_cfg3.py > gpurun_out/lmprof.log 2>&1 || { tail gpurun_out/lmprof.log; exit 1; }
+DDLO_GICP_LIB=$PWD/ab/libL.so timeout -k 10 120 python3 tools/time_cfg3.py > gpurun_out/lmprof.log 2>&1 || { tail gpurun_out/lmprof.log; exit 1; }
 python3 - <<'PY'
 import numpy as np
 rows=[list(map(int,l.split()[1:])) for l in open('gpurun_out/lmprof.log') if l.startswith('lm_prof')]
