@@ -316,13 +316,24 @@ void drop_pair(hipExecGraphPair& p) {
   p.g = nullptr;
 }
 
-void drop_graphs(gicp_ctx* c) {
-  for (auto& p : c->g_first) drop_pair(p);
-  c->g_first.clear();
-  drop_pair(c->g_rest[0]);
-  drop_pair(c->g_rest[1]);
-  c->graph_key.fill(-1);
+void drop_set(GraphSet& gs) {
+  for (auto& p : gs.first) drop_pair(p);
+  gs.first.clear();
+  drop_pair(gs.rest[0]);
+  drop_pair(gs.rest[1]);
+  gs.key.fill(-1);
 }
+
+void drop_graphs(gicp_ctx* c) {
+  for (auto& gs : c->gsets) drop_set(gs);
+  c->gsets.clear();
+}
+
+// The graph set of a launch geometry: a cached one, else captured (its two
+// single-iteration graphs now, first chunks on demand), evicting the least
+// recently used set -- after the stream's queued chunk, which may be one of
+// its graphs, has run.
+gicp_status graph_set(gicp_ctx* c, const std::array<long long, 7>& key, int nblocks, GraphSet** out);
 
 // Launch the align as a first chunk of n outer iterations (n = the previous
 // align's iteration count on this ctx: aligns of consecutive scans converge
@@ -341,11 +352,9 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
                                       g.scan_blocks, g.mom_blocks, g.lds_boxes}};
   const bool use_graph = !c->comm || c->comm_graphs;
   const int first = std::max(1, std::min({c->predicted_iters, max_it, kMaxFirstChunk}));
-  if (use_graph && c->graph_key != key) {
-    drop_graphs(c);
-    c->g_first.resize(kMaxFirstChunk);
-    gicp_status s = capture_chunk(c, false, 1, nblocks, 0, &c->g_rest[0]);
-    if (!s) s = capture_chunk(c, false, 1, nblocks, 1, &c->g_rest[1]);
+  GraphSet* gs = nullptr;
+  if (use_graph) {
+    gicp_status s = graph_set(c, key, nblocks, &gs);
     if (s) {
       drop_graphs(c);
       (void)hipGetLastError();
@@ -353,10 +362,9 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
       c->comm_graphs = false;  // RCCL refused stream capture: launch chunks eagerly
       return run_align_graph(c, max_it, nblocks, final_chunk);
     }
-    c->graph_key = key;
   }
-  if (use_graph && !c->g_first[first - 1].ge) {
-    gicp_status s = capture_chunk(c, true, first, nblocks, 0, &c->g_first[first - 1]);
+  if (use_graph && !gs->first[first - 1].ge) {
+    gicp_status s = capture_chunk(c, true, first, nblocks, 0, &gs->first[first - 1]);
     if (s) {
       drop_graphs(c);
       return s;
@@ -366,7 +374,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   auto launch_chunk = [&](int k) -> gicp_status {
     const bool is_first = k == 0;
     if (use_graph) {
-      HIP_TRY(hipGraphLaunch(is_first ? c->g_first[first - 1].ge : c->g_rest[k & 1].ge, c->stream));
+      HIP_TRY(hipGraphLaunch(is_first ? gs->first[first - 1].ge : gs->rest[k & 1].ge, c->stream));
       return GICP_OK;
     }
     return enqueue_chunk(c, is_first, is_first ? first : 1, nblocks, k & 1);
@@ -427,6 +435,37 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   // align (A/B at cfg 3: 0.466 -> 0.459 ms/scan without it).
   c->speculate = k > 0;
   c->predicted_iters = std::max(1, (int)((const volatile AlignState*)(c->state_host + (k & 1)))->iter);
+  return GICP_OK;
+}
+
+gicp_status graph_set(gicp_ctx* c, const std::array<long long, 7>& key, int nblocks, GraphSet** out) {
+  ++c->graph_clock;
+  for (auto& gs : c->gsets)
+    if (gs.key == key) {
+      gs.last_use = c->graph_clock;
+      *out = &gs;
+      return GICP_OK;
+    }
+  GraphSet* slot = nullptr;
+  if ((int)c->gsets.size() < kGraphSets) {
+    c->gsets.reserve(kGraphSets);   // no reallocation: the sets stay where their pointers point
+    c->gsets.emplace_back();
+    slot = &c->gsets.back();
+  } else {
+    slot = &c->gsets[0];
+    for (auto& gs : c->gsets)
+      if (gs.last_use < slot->last_use) slot = &gs;
+    gicp_status s = drain_tail(c);   // the queued speculative chunk may be one of its graphs
+    if (s) return s;
+    drop_set(*slot);
+  }
+  slot->first.resize(kMaxFirstChunk);
+  gicp_status s = capture_chunk(c, false, 1, nblocks, 0, &slot->rest[0]);
+  if (!s) s = capture_chunk(c, false, 1, nblocks, 1, &slot->rest[1]);
+  if (s) return s;
+  slot->key = key;
+  slot->last_use = c->graph_clock;
+  *out = slot;
   return GICP_OK;
 }
 
@@ -543,7 +582,8 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   c->tgt = Side();
   (void)hipStreamDestroy(c->stream);
   (void)hipStreamSynchronize(c->aux_stream);
-  if (c->nf_graph) (void)hipGraphExecDestroy(c->nf_graph);
+  for (auto& e : c->nf_graphs)
+    if (e.ge) (void)hipGraphExecDestroy(e.ge);
   if (c->nf_ntask_host) (void)hipHostFree(c->nf_ntask_host);
   if (c->nf_ntask_ev) (void)hipEventDestroy(c->nf_ntask_ev);
   (void)hipStreamDestroy(c->aux_stream);

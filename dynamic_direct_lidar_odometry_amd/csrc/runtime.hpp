@@ -219,6 +219,19 @@ struct hipExecGraphPair {
   hipGraphExec_t ge = nullptr;
 };
 
+// The chunk graphs of one launch geometry: [init + n iterations] for the
+// predicted iteration count n (one per n, index n - 1) and [1 iteration]
+// publishing to state slot s = 0, 1; captured for: RCCL in the chunk, job
+// buffer, launch geometry (LinGeom).
+struct GraphSet {
+  std::array<long long, 7> key{{-1, -1, -1, -1, -1, -1, -1}};
+  std::vector<hipExecGraphPair> first;
+  hipExecGraphPair rest[2];
+  long long last_use = 0;
+};
+constexpr int kGraphSets = 4;   // geometries a ctx keeps captured (scans straddling a size bucket alternate)
+constexpr int kNfGraphs = 4;    // tree-build graphs a ctx keeps captured
+
 constexpr int kDefaultPredictedIters = 4;
 
 struct gicp_ctx {
@@ -244,13 +257,10 @@ struct gicp_ctx {
   int* flag_host = nullptr;       // pinned
   bool have_align = false;        // a linearize ran against the current src/tgt
   int last_nsrc = 0;
-  // chunk graphs: [init + n iterations + state copy to slot 0] for the
-  // predicted iteration count n (one per n, index n - 1) and [1 iteration +
-  // state copy to slot s] for s = 0, 1
-  std::vector<hipExecGraphPair> g_first;
-  hipExecGraphPair g_rest[2];
-  // captured for: RCCL in the chunk, job buffer, launch geometry (LinGeom)
-  std::array<long long, 7> graph_key{{-1, -1, -1, -1, -1, -1, -1}};
+  // chunk graphs of the last kGraphSets launch geometries (least recently
+  // used evicted)
+  std::vector<GraphSet> gsets;
+  long long graph_clock = 0;
   int predicted_iters = kDefaultPredictedIters;   // iterations of the previous align on this ctx
   std::vector<hipEvent_t> chunk_ev;
   // second stream: nanoflann's tree (tie order) is built here while the
@@ -258,8 +268,15 @@ struct gicp_ctx {
   hipStream_t aux_stream = nullptr;
   hipEvent_t aux_ev = nullptr;
   DevBuf nf_desc;                    // the build descriptor the tree kernels read
-  hipGraphExec_t nf_graph = nullptr;  // the build, captured for one size bucket and level count
-  long long nf_graph_key = -1;
+  // the build, captured per (size bucket, level count); the last kNfGraphs
+  // kept (a scan size straddling a bucket boundary alternates two)
+  struct NfGraph {
+    long long key = -1;
+    hipGraphExec_t ge = nullptr;
+    long long last_use = 0;
+  };
+  std::vector<NfGraph> nf_graphs;
+  long long nf_clock = 0;
   // Big levels the builds of this ctx need: the level counts of each build
   // (ctl->ntask, copied to pinned memory after it) set later builds of the
   // size bucket to the most levels any of them used + kNfLevelSpare, so
@@ -270,7 +287,10 @@ struct gicp_ctx {
   int* nf_ntask_host = nullptr;       // pinned [kNfMaxLevels + 1]
   hipEvent_t nf_ntask_ev = nullptr;   // the copy's completion
   int nf_ntask_bucket = -1, nf_ntask_lmax = 0;   // the build the copy belongs to
-  int nf_hint_bucket = -1, nf_hint = 0, nf_used_max = 0;   // the next build's level count for that bucket
+  struct NfHint {
+    int used_max = 0, hint = 0;   // hint 0: the full margin
+  };
+  std::map<int, NfHint> nf_hints;   // per size bucket: the next build's level count
   // a copied level count is ready to read (its build completed)
   bool nf_ntask_pending_check() const {
     return nf_ntask_bucket >= 0 && nf_ntask_ev && hipEventQuery(nf_ntask_ev) == hipSuccess;
@@ -438,18 +458,20 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   if (c->nf_ntask_pending_check()) {
     int used = 0;
     while (used < c->nf_ntask_lmax && c->nf_ntask_host[used] > 0) ++used;
-    if (c->nf_hint_bucket != c->nf_ntask_bucket) c->nf_used_max = 0;
-    c->nf_hint_bucket = c->nf_ntask_bucket;
+    auto& h = c->nf_hints[c->nf_ntask_bucket];
     if (used >= c->nf_ntask_lmax) {
-      c->nf_hint = 0;   // every level had nodes to split: measure again with the full margin
+      h.hint = 0;   // every level had nodes to split: measure again with the full margin
     } else {
-      c->nf_used_max = std::max(c->nf_used_max, used);
-      c->nf_hint = c->nf_used_max + kNfLevelSpare;
+      h.used_max = std::max(h.used_max, used);
+      h.hint = h.used_max + kNfLevelSpare;
     }
     c->nf_ntask_bucket = -1;
   }
   int Lmax = z.Lmax;
-  if (stop < 0 && !off && c->nf_hint_bucket == nbucket && c->nf_hint > 0) Lmax = std::min(z.Lmax, c->nf_hint);
+  if (stop < 0 && !off) {
+    const auto it = c->nf_hints.find(nbucket);
+    if (it != c->nf_hints.end() && it->second.hint > 0) Lmax = std::min(z.Lmax, it->second.hint);
+  }
   t->cap = z.big_ids + 2 * n;   // big-level ids, then 2 per point for the small subtrees' ranges
   HIP_TRY(t->vpts.ensure(sizeof(float4) * (size_t)n));
   HIP_TRY(t->nodes.ensure(sizeof(NfNode) * (size_t)t->cap));
@@ -510,10 +532,24 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
     HIP_TRY(hipGetLastError());
   } else {
     const long long gkey = (long long)nbucket * 64 + Lmax;
-    if (c->nf_graph_key != gkey) {
-      if (c->nf_graph) HIP_TRY(hipGraphExecDestroy(c->nf_graph));
-      c->nf_graph = nullptr;
-      c->nf_graph_key = -1;
+    ++c->nf_clock;
+    gicp_ctx::NfGraph* ng = nullptr;
+    for (auto& e : c->nf_graphs)
+      if (e.key == gkey) ng = &e;
+    if (!ng) {
+      if ((int)c->nf_graphs.size() < kNfGraphs) {
+        c->nf_graphs.reserve(kNfGraphs);
+        c->nf_graphs.emplace_back();
+        ng = &c->nf_graphs.back();
+      } else {   // evict the least recently used, after the builds queued on the stream
+        ng = &c->nf_graphs[0];
+        for (auto& e : c->nf_graphs)
+          if (e.last_use < ng->last_use) ng = &e;
+        HIP_TRY(hipStreamSynchronize(s));
+        if (ng->ge) HIP_TRY(hipGraphExecDestroy(ng->ge));
+        ng->ge = nullptr;
+        ng->key = -1;
+      }
       hipGraph_t g = nullptr;
       HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
       launch_nf_build(s, b, db, -1);
@@ -521,12 +557,13 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
       const hipError_t e2 = hipStreamEndCapture(s, &g);
       HIP_TRY(e1);
       HIP_TRY(e2);
-      const hipError_t e3 = hipGraphInstantiate(&c->nf_graph, g, nullptr, nullptr, 0);
+      const hipError_t e3 = hipGraphInstantiate(&ng->ge, g, nullptr, nullptr, 0);
       (void)hipGraphDestroy(g);
       HIP_TRY(e3);
-      c->nf_graph_key = gkey;
+      ng->key = gkey;
     }
-    HIP_TRY(hipGraphLaunch(c->nf_graph, s));
+    ng->last_use = c->nf_clock;
+    HIP_TRY(hipGraphLaunch(ng->ge, s));
   }
   if (stop < 0 && !off) {   // the level counts of this build, for the next one
     if (!c->nf_ntask_host) {
