@@ -5,3 +5,4 @@ mkdir -p gpurun_out/r03
 bash tools/gpu_r3_profiles.sh || exit 1
 DDLO_TRAFFIC_JSON=gpurun_out/r03/traffic.json timeout -k 10 900 python -u bench.py > gpurun_out/r03/bench.json 2> gpurun_out/r03/bench.err || { echo BENCH_FAIL; tail -20 gpurun_out/r03/bench.err; exit 1; }
 cat gpurun_out/r03/bench.json
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
