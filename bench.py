@@ -115,7 +115,15 @@ def host_info(threads):
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = None
-    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_threads": threads}
+    quota = None   # the job's CPU share (cgroup v2 cpu.max: quota period)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "omp_threads": threads}
 
 
 def varied_guesses(prob):
@@ -567,9 +575,17 @@ def main():
 
     if rank == 0 and not args.no_cpu:
         from oracle import oracle as O
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+        # The reference runs num_threads_ = omp_get_max_threads() (nano_gicp_impl.hpp:52-56), i.e. every
+        # host core.  A GPU box's job is cgroup-limited (cpu.max) to a share of a large host, so "all cores"
+        # is not the fastest setting there: the oracle is timed at 8, 16, 32, 64, 128 threads and at the
+        # affinity count, and the headline baseline is the FASTEST median (the most favourable CPU figure).
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            affinity = os.cpu_count() or 1
+        thread_set = sorted({t for t in (8, 16, 32, 64, 128) if t <= affinity} | {affinity})
 
-        def cpu_ms_at(nthreads):
+        def cpu_ms_at(nthreads, runs):
             g = O.Gicp(src, sub, O.as_params(params), threads=nthreads)
             g.set_covariances(0, scov)
             g.set_covariances(1, tcov)
@@ -577,24 +593,39 @@ def main():
                 g.align(guess)
             times = []
             oo = ro = None
-            for _ in range(args.cpu_runs):
+            for _ in range(runs):
                 c0 = time.perf_counter()
                 oo, ro = g.align(guess)
                 times.append(time.perf_counter() - c0)
             return 1e3 * float(np.median(times)), oo, ro
 
-        cpu_ms, oout, ores = cpu_ms_at(threads)
-        cpu8_ms = cpu_ms_at(8)[0] if threads != 8 else cpu_ms
-        result["cpu_baseline"] = {"value": round(cpu_ms, 3), "unit": "ms/scan", "cores": threads, "kind": "port",
+        by_threads = {}
+        oout = ores = None
+        for t in thread_set:
+            # a throttled setting (far above the cgroup share) takes seconds per align: 3 runs are enough to
+            # show it is not the fastest
+            runs = args.cpu_runs if t <= 128 else min(args.cpu_runs, 3)
+            ms_t, oo, ro = cpu_ms_at(t, runs)
+            by_threads[t] = round(ms_t, 3)
+            if oout is None:
+                oout, ores = oo, ro
+        best_t = min(by_threads, key=by_threads.get)
+        cpu_ms = by_threads[best_t]
+        result["cpu_baseline"] = {"value": round(cpu_ms, 3), "unit": "ms/scan", "cores": best_t, "kind": "port",
                                   "sample": f"median of {args.cpu_runs} full S2M aligns of the same cfg3 problem after "
                                             f"{args.cpu_warmup} warm-ups ({ores.iterations_run} iters each), OpenMP "
-                                            f"oracle oracle/cpu_ref.cpp at -O2, {threads} threads",
-                                  "value_8_threads": round(cpu8_ms, 3),
-                                  "host": host_info(threads),
+                                            f"oracle oracle/cpu_ref.cpp at -O2; fastest of the thread sweep "
+                                            f"{thread_set} ({best_t} threads)",
+                                  "ms_by_threads": {str(k): v for k, v in by_threads.items()},
+                                  "value_all_cores": by_threads[affinity], "threads_all_cores": affinity,
+                                  "value_16_threads": by_threads.get(16), "value_8_threads": by_threads.get(8),
+                                  "host": host_info(best_t),
                                   "validation": "profiles/r03_cpu_validation.json (cpu_ref search stages vs the "
                                                 "reference's own nanoflann, same inputs)",
                                   "speedup_gpu_vs_cpu": round(cpu_ms / ms_per_step, 2),
-                                  "speedup_gpu_vs_cpu_8_threads": round(cpu8_ms / ms_per_step, 2)}
+                                  "speedup_gpu_vs_cpu_all_cores": round(by_threads[affinity] / ms_per_step, 2),
+                                  "speedup_gpu_vs_cpu_16_threads": (round(by_threads[16] / ms_per_step, 2)
+                                                                   if 16 in by_threads else None)}
         result["pose_delta_vs_cpu"] = {"trans_m": float(np.abs(out[:3, 3] - oout[:3, 3]).max()),
                                        "rot_rad": rot_err(out, oout)}
     ctx.close()

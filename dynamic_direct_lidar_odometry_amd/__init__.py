@@ -74,6 +74,8 @@ class GicpResult(C.Structure):
         ("lm_lambda", C.c_double),
         ("device_ms", C.c_double),
         ("linearize_ms", C.c_double),
+        ("ties_resolved", C.c_int32),
+        ("tie_reruns", C.c_int32),
     ]
 
 
@@ -124,6 +126,7 @@ def load():
         "gicp_synchronize": (I, [P]),
         "gicp_set_shard": (I, [P, I, C.c_float, C.c_float]),
         "gicp_set_shard_groups": (I, [P, I, I]),
+        "gicp_set_tie_target": (I, [P, P, C.c_size_t, C.c_size_t, P, C.c_size_t]),
         "gicp_comm_unique_id": (I, [P, S]),
         "gicp_set_comm": (I, [P, P, S, I, I]),
         "gicp_get_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
@@ -394,6 +397,16 @@ class Context:
     def set_shard_groups(self, nparts: int, part: int):
         """Interleaved ownership: this ctx searches the 16-point groups = part (mod nparts)."""
         self._check(self.L.gicp_set_shard_groups(self.h, int(nparts), int(part)))
+
+    def set_tie_target(self, points, local_index):
+        """Slab shard: the whole target its local target was cut from and each local point's index in it
+        (exact ties resolve in the whole target's nanoflann order).  points=None removes it."""
+        if points is None:
+            self._check(self.L.gicp_set_tie_target(self.h, None, 0, 12, None, 0))
+            return
+        a, stride = _xyz(points)
+        li = np.ascontiguousarray(local_index, np.int32)
+        self._check(self.L.gicp_set_tie_target(self.h, _ptr(a), len(a), stride, _ptr(li), len(li)))
 
     def set_comm(self, unique_id: bytes | None, nranks: int, rank: int):
         buf = None

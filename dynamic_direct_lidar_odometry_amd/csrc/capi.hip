@@ -7,6 +7,9 @@
 // failed.  The host synchronises once per align, to read back the pose.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <thread>
+
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>  // types only: RCCL is dlopen'ed on first gicp_set_comm
 
@@ -216,6 +219,22 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.reuse_rec0 = kn.reuse_rec0;
   j.reuse_rec_eps = kn.reuse_rec_eps;
   j.reuse_rec_conv = kn.reuse_rec_conv;
+  // exact correspondence ties in nanoflann's order (k_moments): the task
+  // search tracks the examined points' second distance; the target's tree,
+  // when it exists, re-runs the tied queries.  Slab shards hold a subset of
+  // the target, whose tree orders ties differently: Morton order there.
+  j.tie_detect = (c->tie_exact && search_uses_tasks() && (c->own_axis < 0 || c->tie_ref)) ? 1 : 0;
+  j.tgt_nf = NfTreeDev{nullptr, nullptr, nullptr, 0};
+  j.tgt_nf_status = nullptr;
+  j.tie_map = nullptr;
+  if (j.tie_detect) {
+    const CloudData* tc = c->tie_ref ? c->tie_ref.get() : c->tgt.cloud.get();
+    if (tc->nf) {
+      j.tgt_nf = tc->nf->dev();
+      j.tgt_nf_status = tc->nf->status.as<int>();
+    }
+    if (c->tie_ref) j.tie_map = c->tie_map.as<int>();
+  }
   // no copy here: k_align_init reads the pinned job and writes the device one
   return GICP_OK;
 }
@@ -255,10 +274,38 @@ gicp_status prepare_align(gicp_ctx* c) {
   HIP_TRY(c->slab.ensure(sizeof(double) * kSlabStride * linearize_blocks(ns)));
   HIP_TRY(c->mom.ensure(sizeof(double) * kSlabStride));
   HIP_TRY(c->search.ensure(need_search));
+  // the target's nanoflann tree (tie order): a sharded align builds it up
+  // front (every rank the same tree, so no rank ever re-runs alone and the
+  // collectives stay matched); otherwise it is built only when an align
+  // meets a tie (gicp_align).  The stream waits once for a tree's build.
+  if (c->tie_exact && (c->own_axis < 0 || c->tie_ref) && search_uses_tasks()) {
+    CloudData& tc = c->tie_ref ? *c->tie_ref : *c->tgt.cloud;
+    if ((c->comm || c->tie_ref) && !tc.nf) {
+      gicp_status s = ensure_nftree(c, tc, c->stream);
+      if (s) return s;
+    }
+    const auto& nf = tc.nf;
+    if (nf && c->nf_joined.lock() != nf) {
+      HIP_TRY(nftree_join(*nf, c->stream));
+      c->nf_joined = nf;
+    }
+  }
   if (c->stats_on) {
     HIP_TRY(c->stats.ensure(sizeof(unsigned int) * kStatFields * (ns + 15)));
     HIP_TRY(hipMemsetAsync(c->stats.p, 0, c->stats.bytes, c->stream));
   }
+  return GICP_OK;
+}
+
+// Build the target's nanoflann tree (the tie order of the correspondences)
+// and make the ctx stream wait for it.
+gicp_status ensure_tie_tree(gicp_ctx* c) {
+  gicp_status s = drain_tail(c);
+  if (s) return s;
+  s = ensure_nftree(c, *c->tgt.cloud, c->stream);
+  if (s) return s;
+  HIP_TRY(nftree_join(*c->tgt.cloud->nf, c->stream));
+  c->nf_joined = c->tgt.cloud->nf;
   return GICP_OK;
 }
 
@@ -409,9 +456,16 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   }();
   for (;;) {
     if (spin) {
+      // several host threads waiting at once (gicp_s2s_batch's workers):
+      // they yield the core between polls, so the pollers do not starve the
+      // HIP runtime's own threads
+      static std::atomic<int> waiters{0};
+      waiters.fetch_add(1, std::memory_order_relaxed);
       hipError_t q;
       while ((q = hipEventQuery(c->chunk_ev[k])) == hipErrorNotReady) {
+        if (waiters.load(std::memory_order_relaxed) > 1) std::this_thread::yield();
       }
+      waiters.fetch_sub(1, std::memory_order_relaxed);
       HIP_TRY(q);
     } else {
       HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
@@ -659,6 +713,7 @@ gicp_status gicp_set_target(gicp_ctx* c, const float* xyz, size_t n, size_t stri
   if (s) return s;
   c->tgt.cloud = cd;
   c->tgt.cov.reset();  // (:154)
+  c->tie_ref.reset();  // a slab's whole-target tie order belongs to the previous target
   invalidate_align(c);
   return GICP_OK;
 }
@@ -685,6 +740,7 @@ gicp_status gicp_get_size(const gicp_ctx* c, int side, size_t* n) {
 
 gicp_status gicp_compute_covariances(gicp_ctx* c, int side) {
   if (!c || (side != 0 && side != 1)) return fail(GICP_EINVAL, "invalid argument");
+  begin_ties(c);
   gicp_status s = set_device(c);
   if (s) return s;
   s = compute_cov(c, side == GICP_SIDE_SOURCE ? c->src : c->tgt);
@@ -753,34 +809,46 @@ gicp_status gicp_share_source(gicp_ctx* dst, const gicp_ctx* src) {
 
 gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_result* res) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
+  begin_ties(c);
   gicp_status s = set_device(c);
   if (s) return s;
   s = prepare_align(c);
   if (s) return s;
   const int ns = c->src.cloud->n;
   const int nblocks = linearize_blocks(ns);
-  s = fill_job(c, guess16, nblocks);
-  if (s) return s;
-  const int max_it = c->job_host->max_iterations;
   hipEvent_t end_ev = c->ev1;
-  HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  if (c->profiling || max_it <= 0) {
-    s = max_it > 0 ? run_align_eager_profiled(c, max_it, nblocks) : GICP_OK;
+  int reruns = 0;
+  for (;;) {
+    s = fill_job(c, guess16, nblocks);
     if (s) return s;
-    if (max_it <= 0) launch_align_init(c->stream, c->job_dev.as<AlignJob>(), c->job_host_dev);
-    HIP_TRY(hipEventRecord(c->ev1, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    c->state_slot = 0;
-    c->tail_pending = false;
-  } else {
-    int fc = 0;
-    s = run_align_graph(c, max_it, nblocks, &fc);
+    const int max_it = c->job_host->max_iterations;
+    end_ev = c->ev1;
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    if (c->profiling || max_it <= 0) {
+      s = max_it > 0 ? run_align_eager_profiled(c, max_it, nblocks) : GICP_OK;
+      if (s) return s;
+      if (max_it <= 0) launch_align_init(c->stream, c->job_dev.as<AlignJob>(), c->job_host_dev);
+      HIP_TRY(hipEventRecord(c->ev1, c->stream));
+      HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      c->state_slot = 0;
+      c->tail_pending = false;
+    } else {
+      int fc = 0;
+      s = run_align_graph(c, max_it, nblocks, &fc);
+      if (s) return s;
+      // chunk fc's end-of-chunk copy already put the final state in its
+      // slot; the (at most one) speculative no-op chunk still queued writes
+      // the other slot and does not delay the return
+      end_ev = c->chunk_ev[fc];
+    }
+    // a correspondence met an exact tie before the target had nanoflann's
+    // tree: build it and run the align again, so every correspondence is
+    // nanoflann's (the tree stays with the target cloud for later aligns)
+    if (!final_state(c).tie_pending || reruns > 0) break;
+    s = ensure_tie_tree(c);
     if (s) return s;
-    // chunk fc's end-of-chunk copy already put the final state in its
-    // slot; the (at most one) speculative no-op chunk still queued writes
-    // the other slot and does not delay the return
-    end_ev = c->chunk_ev[fc];
+    ++reruns;
   }
   const AlignState& st = final_state(c);
   c->have_align = st.iter > 0;
@@ -804,6 +872,8 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
     res->final_cost = st.final_cost;
     std::memcpy(res->final_hessian, st.final_hessian, sizeof(res->final_hessian));
     res->lm_lambda = st.lambda;
+    res->ties_resolved = st.ties_resolved;
+    res->tie_reruns = reruns;
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, end_ev));
     res->device_ms = ms;
@@ -819,6 +889,9 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
   }
   s = check_ties(c);
   if (s) return s;
+  if (st.tie_err || st.tie_pending)
+    return fail(GICP_EHIP, "nanoflann tie order: a tied correspondence could not be re-run (bits " +
+                               std::to_string(st.tie_err) + (st.tie_pending ? ", no tree" : "") + ")");
   if (st.lm_failed) g_last_error = "lm not converged!!";
   return GICP_OK;
 }
@@ -925,34 +998,43 @@ gicp_status gicp_transform_source(gicp_ctx* c, float* out_xyz, size_t n, size_t 
 
 gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, double* b6, double* cost, int32_t* ncorr) {
   if (!c || !pose16) return fail(GICP_EINVAL, "null argument");
+  begin_ties(c);
   gicp_status s = set_device(c);
   if (s) return s;
   s = prepare_align(c);
   if (s) return s;
   const int ns = c->src.cloud->n;
   const int nblocks = linearize_blocks(ns);
-  float g[16];
-  for (int i = 0; i < 16; ++i) g[i] = 0.f;
-  s = fill_job(c, g, nblocks);
-  if (s) return s;
-  // exact double pose (not the float guess path)
-  for (int r = 0; r < 3; ++r) {
-    for (int cc = 0; cc < 3; ++cc) c->job_host->guess_R[3 * r + cc] = pose16[4 * r + cc];
-    c->job_host->guess_t[r] = pose16[4 * r + 3];
+  for (int rerun = 0;; ++rerun) {
+    float g[16];
+    for (int i = 0; i < 16; ++i) g[i] = 0.f;
+    s = fill_job(c, g, nblocks);
+    if (s) return s;
+    // exact double pose (not the float guess path)
+    for (int r = 0; r < 3; ++r) {
+      for (int cc = 0; cc < 3; ++cc) c->job_host->guess_R[3 * r + cc] = pose16[4 * r + cc];
+      c->job_host->guess_t[r] = pose16[4 * r + 3];
+    }
+    c->job_host->optimizer = GICP_OPT_GAUSS_NEWTON;
+    c->job_host->max_iterations = 1;
+    c->job_host->fixed_iterations = 1;
+    AlignJob* jd = c->job_dev.as<AlignJob>();
+    launch_align_init(c->stream, jd, c->job_host_dev);
+    s = enqueue_iteration(c, jd, nblocks, nullptr);
+    if (s) return s;
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->state_slot = 0;
+    c->tail_pending = false;
+    if (!final_state(c).tie_pending || rerun > 0) break;
+    s = ensure_tie_tree(c);   // a tie met before the target had its nanoflann tree (see gicp_align)
+    if (s) return s;
   }
-  c->job_host->optimizer = GICP_OPT_GAUSS_NEWTON;
-  c->job_host->max_iterations = 1;
-  c->job_host->fixed_iterations = 1;
-  AlignJob* jd = c->job_dev.as<AlignJob>();
-  launch_align_init(c->stream, jd, c->job_host_dev);
-  s = enqueue_iteration(c, jd, nblocks, nullptr);
-  if (s) return s;
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  c->state_slot = 0;
-  c->tail_pending = false;
   const AlignState& st = final_state(c);
+  if (st.tie_err || st.tie_pending)
+    return fail(GICP_EHIP, "nanoflann tie order: a tied correspondence could not be re-run (bits " +
+                               std::to_string(st.tie_err) + ")");
   if (H36) std::memcpy(H36, st.final_hessian, sizeof(double) * 36);
   if (cost) *cost = st.final_cost;
   if (ncorr) *ncorr = st.num_corr;
@@ -967,6 +1049,7 @@ gicp_status gicp_knn_target(gicp_ctx* c, const float* q, size_t nq, size_t strid
   if (!c->tgt.cloud) return fail(GICP_ENOTARGET, "no target");
   if (k < 1 || k > 64) return fail(GICP_EINVAL, "k must be in [1, 64]");
   if (c->tgt.cloud->n < k) return fail(GICP_ETOOFEW, "target has fewer than k points");
+  begin_ties(c);
   gicp_status s = set_device(c);
   if (s) return s;
   const size_t raw = (nq - 1) * stride + 12;
@@ -1112,6 +1195,36 @@ gicp_status gicp_set_shard(gicp_ctx* c, int axis, float lo, float hi) {
   c->own_axis = axis;
   c->own_lo = axis >= 0 ? lo : -INFINITY;
   c->own_hi = axis >= 0 ? hi : INFINITY;
+  invalidate_align(c);
+  return GICP_OK;
+}
+
+gicp_status gicp_set_tie_target(gicp_ctx* c, const float* xyz, size_t n, size_t stride, const int32_t* local_index,
+                                size_t n_local) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  if (n == 0) {
+    c->tie_ref.reset();
+    return GICP_OK;
+  }
+  if (!xyz || !local_index) return fail(GICP_EINVAL, "null argument");
+  if (!c->tgt.cloud || (int)n_local != c->tgt.cloud->n) return fail(GICP_ESTATE, "set the local target first (n_local = its size)");
+  for (size_t i = 0; i < n_local; ++i)
+    if (local_index[i] < 0 || (size_t)local_index[i] >= n) return fail(GICP_EINVAL, "local_index out of range");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  std::shared_ptr<CloudData> cd;
+  s = build_cloud(c, xyz, n, stride, &cd);
+  if (s) return s;
+  s = ensure_nftree(c, *cd, c->stream);
+  if (s) return s;
+  HIP_TRY(c->tie_map.ensure(sizeof(int) * (n + n_local)));
+  int* map = c->tie_map.as<int>();
+  int* lidx = map + n;
+  HIP_TRY(hipMemcpyAsync(lidx, local_index, sizeof(int) * n_local, hipMemcpyHostToDevice, c->stream));
+  launch_tie_map(c->stream, lidx, c->tgt.cloud->inv_perm.as<int>(), (int)n_local, (int)n, map);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->tie_ref = cd;
   invalidate_align(c);
   return GICP_OK;
 }

@@ -67,6 +67,26 @@ __host__ __device__ inline int lvl_cnt(const CloudDev& c, int l) {
   return l == 0 ? c.cnt0 : l == 1 ? c.cnt1 : l == 2 ? c.cnt2 : l == 3 ? c.cnt3 : c.cnt4;
 }
 
+// ---------------------------------------------------------------------------
+// nanoflann's kd-tree on the device (nftree.hpp / nftree.hip): only used to
+// resolve exact distance ties in nanoflann's traversal order.
+// nanoflann Node (reference impl/nanoflann_impl.hpp:876-894): a leaf holds the
+// vind range [c1, c2); an inner node its children and divfeat / divlow / divhigh.
+struct NfNode {
+  int c1, c2;
+  int feat;            // divfeat; -1 = leaf
+  float divlow, divhigh;
+  int parent;          // -1 at the root (build bookkeeping)
+  int pad0, pad1;
+};
+
+struct NfTreeDev {
+  const float4* vpts;  // [n] points in vind order: x, y, z, original index (int bits)
+  const NfNode* nodes; // node 0 = root
+  const float4* box;   // [2]: root_bbox (lo, hi), computeInitialDistances
+  int n;
+};
+
 // Per-align device state (one per ctx, lives in device memory).
 struct AlignState {
   double R[9];           // x0 (current estimate), row-major
@@ -89,7 +109,12 @@ struct AlignState {
   int rec;               // the next search records reuse references (AlignJob::ref)
   float src_radius;      // max |p| over the source cloud's root boxes (reuse step bound)
   int any_rec;           // an iteration of this align recorded references
-  int pad[1];
+  // exact distance ties in the correspondences (nanoflann's order, k_moments):
+  int tie_pending;       // a matched query's nearest distance is tied and the target has no nanoflann tree yet
+                         // (the host builds it and runs the align again)
+  int ties_resolved;     // tied queries re-run through the target's nanoflann tree (this align)
+  int tie_err;           // a re-run failed (bits as k_nf_resolve_*: 1 depth, 2 tree build, 16 distance mismatch)
+  int pad[2];            // 16-byte multiple (copied in 16-byte words)
 };
 
 // Everything a kernel needs for one align, written by the host before launch.
@@ -170,26 +195,17 @@ struct AlignJob {
   float4* ref;                   // [n_src] q_ref (x, y, z) + B^2 (< 0: no reference)
   float4* ref_p;                 // [n_src] p1 (x, y, z) + its sorted target position as int bits (-1: none within the bound)
   unsigned* sec;                 // [n_src] fp32 bits: smallest squared distance of an examined non-best point
-};
-
-// ---------------------------------------------------------------------------
-// nanoflann's kd-tree on the device (nftree.hpp / nftree.hip): only used to
-// resolve exact distance ties in nanoflann's traversal order.
-// nanoflann Node (reference impl/nanoflann_impl.hpp:876-894): a leaf holds the
-// vind range [c1, c2); an inner node its children and divfeat / divlow / divhigh.
-struct NfNode {
-  int c1, c2;
-  int feat;            // divfeat; -1 = leaf
-  float divlow, divhigh;
-  int parent;          // -1 at the root (build bookkeeping)
-  int pad0, pad1;
-};
-
-struct NfTreeDev {
-  const float4* vpts;  // [n] points in vind order: x, y, z, original index (int bits)
-  const NfNode* nodes; // node 0 = root
-  const float4* box;   // [2]: root_bbox (lo, hi), computeInitialDistances
-  int n;
+  // Exact ties of update_correspondences' 1-NN (nano_gicp_impl.hpp:255 ->
+  // nanoflann_impl.hpp:205-237,1509: the first equidistant point of
+  // nanoflann's walk wins).  tie_detect: k_moments flags a matched query whose
+  // examined points hold another one at its nearest distance (sec == the
+  // key's distance) and re-runs it through the target's nanoflann tree
+  // (tgt_nf.nodes != nullptr), else sets AlignState::tie_pending.
+  int tie_detect;
+  const int* tgt_nf_status;      // the tree build's error bits (device int; 0 = usable)
+  NfTreeDev tgt_nf;              // nodes == nullptr: no tree (yet)
+  const int* tie_map;            // tgt_nf is a whole cloud the target was cut from (slab shard): its original
+                                 // index -> the target's sorted position (-1: not in it); nullptr: tgt.inv_perm
 };
 
 constexpr int kNfMaxLevels = 40;   // big levels of the device build (deeper: the build reports a failure)

@@ -23,6 +23,7 @@
 #include "gicp_types.hpp"
 #include "search.hpp"
 #include "nn_tasks.hpp"
+#include "nftree.hpp"
 #include "cov_math.hpp"
 #include "launch.hpp"
 
@@ -855,7 +856,9 @@ __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_d
     st->num_corr = 0;
     st->have_prev = 0;
     st->final_cost = 0.0;
-
+    st->tie_pending = 0;
+    st->ties_resolved = 0;
+    st->tie_err = 0;
   }
 }
 
@@ -983,6 +986,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       if (inrange && lane < Q) {
         keyout[i] = passed ? pass_key : dkey(INFINITY, -1);
         qstate[i] = make_float4(qx, qy, qz, -1.f);
+        if (job->tie_detect) job->sec[i] = __float_as_uint(INFINITY);   // proven strict: no tie
       }
       if (lane == 0) {
         job->hard_flag[g] = 2;   // nothing to search: k_nn_collect skips the sub-group
@@ -1239,7 +1243,9 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         qstate[i] = make_float4(qx, qy, qz, active ? wr : -1.f);
         keyout[i] = active ? col.bk : passed ? pass_key : dkey(INFINITY, -1);   // col.bk: the seed, lowered by inline scans
       }
-      if (rec && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further
+      // the examined points' second distance: the reuse bound (rec) and the
+      // tie test of k_moments (sec == the key's distance); k_nn_scan lowers it
+      if ((rec || job->tie_detect) && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);
       if (stats) {
         const unsigned npass = (unsigned)__popcll(__ballot(passed && lane < Q));
         if (lane == 0) {
@@ -1351,7 +1357,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __rest
   col.pf_ratio = job->pf_ratio;
   col.run(tgt, tl, skey, job->split_extent);
   if (inrange && lane < Q && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
-  if (st->rec && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further
+  if ((st->rec || job->tie_detect) && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further
   if (lane == 0) job->grp_blocks[g] = (unsigned short)min(col.st_blocks, 65535u);
   if (stats && lane == 0) {
     const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
@@ -1423,7 +1429,12 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   const int lo = c * chunk, hi = min(n, lo + chunk);
   const unsigned long long* rt = job->tasks + (size_t)r * cap_r;
   unsigned* const sec = job->sec;
-  const bool reuse = st->rec != 0;   // this search records reuse references
+  const bool rec = st->rec != 0;     // this search records reuse references
+  // the second distance of the examined points is tracked for the reuse
+  // bound (rec) and for k_moments' tie test (tie_detect): every point at the
+  // final nearest distance is examined (its leaf is within the walk radius),
+  // so the query is tied iff another examined point has that distance
+  const bool reuse = rec || job->tie_detect;
   int run_sg = -1;
   unsigned long long acc = ~0ull;   // lane's query minimum over the current run
   float acc2 = INFINITY;            // smallest distance of the run's other points (reuse)
@@ -1444,7 +1455,11 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
         const unsigned long long lost = pend_old < pend_acc ? pend_acc : pend_old;
         if (key_real(lost)) push = fminf(push, key_dist(lost));
       }
-      if (push < pend_bound) atomicMin(sec + pend_q, __float_as_uint(push));
+      // rec: everything below the walk radius (B^2 = min(sec, radius));
+      // tie test only: a push can matter only if it equals the query's
+      // current minimum (the final one is <= it), so almost none is issued
+      if (rec ? push <= pend_bound : push == key_dist(umin64(pend_old, pend_acc)))
+        atomicMin(sec + pend_q, __float_as_uint(push));
       pend = false;
     }
   };
@@ -1785,6 +1800,54 @@ constexpr int kMomWaves = 8;    // waves per moment block (512 threads: 256 bloc
 // back its XCD's L2 before the completion counter.)
 __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job);
 
+// Exact ties of update_correspondences' 1-NN (nano_gicp_impl.hpp:255): the
+// reference keeps the equidistant point nanoflann's walk meets first
+// (KNNResultSet adds only below the worst distance, nanoflann_impl.hpp:1509),
+// the search here the lower Morton position.  The lanes in `tied` are re-run,
+// one at a time by the whole wavefront, through the target's nanoflann tree
+// (nf_search_wave, k = 1), from the same fp32 query; the result must have the
+// same distance.  Without a tree the align is flagged (tie_pending): the host
+// builds it and runs the align again.  Not inlined: the rare path keeps its
+// registers out of the moment loop.
+__device__ __noinline__ void resolve_tied_corr(const AlignJob* __restrict__ job, AlignState* st, const CloudDev& tgt,
+                                               bool tied, int i, float kd, int& j, NfWaveStack* S) {
+  unsigned long long tm = __ballot(tied);
+  const int lane = lane_id();
+  const NfTreeDev t = job->tgt_nf;
+  if (t.nodes == nullptr) {
+    if (lane == __builtin_ctzll(tm)) st->tie_pending = 1;
+    return;
+  }
+  if (*job->tgt_nf_status) {   // the tree build failed: keep the Morton-order answers, report
+    if (lane == __builtin_ctzll(tm)) atomicOr(&st->tie_err, 2);
+    return;
+  }
+  int nres = 0;
+  while (tm) {
+    const int l = __builtin_ctzll(tm);
+    tm &= tm - 1;
+    const int il = __builtin_amdgcn_readlane(i, l);
+    const float dl = __uint_as_float((unsigned)__builtin_amdgcn_readlane((int)__float_as_uint(kd), l));
+    const float4 q = ldg4(job->qstate, il);   // the search's fp32 query (trans_f * a_i, :240,253)
+    float rd;
+    int rix;
+    int err = 0, jn = -1;
+    const bool ok = nf_search_wave(t, q.x, q.y, q.z, 1, S, &rd, &rix);
+    // lane 0 holds the (k = 1) result
+    rd = __uint_as_float((unsigned)__builtin_amdgcn_readfirstlane((int)__float_as_uint(rd)));
+    rix = __builtin_amdgcn_readfirstlane(rix);
+    if (!ok) err = 1;
+    else if (__float_as_uint(rd) != __float_as_uint(dl) || rix < 0 || rix >= t.n) err = 16;
+    else if ((jn = job->tie_map ? job->tie_map[rix] : tgt.inv_perm[rix]) < 0) err = 32;   // outside the slab + halo
+    if (lane == l) {
+      if (jn >= 0) j = jn;
+      else atomicOr(&st->tie_err, err);
+    }
+    ++nres;
+  }
+  if (lane == 0) atomicAdd(&st->ties_resolved, nres);
+}
+
 // FUSE_LM: the LM step runs in the last block to finish (one block per CU:
 // 256 blocks), handed off without a release fence -- each block stores its
 // slab row write-through (sc1), drains it (vmcnt(0)), and one lane adds to
@@ -1806,6 +1869,8 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
   const double max_corr2 = job->max_corr2;
   const int rec = st->rec;   // this iteration records reuse references
   const int first_rec_done = st->any_rec;   // an earlier iteration of this align recorded
+  const int tie_detect = job->tie_detect;
+  __shared__ NfWaveStack tie_stk[kMomWaves];   // nanoflann search frames of a tied query (per wave)
   double R[9], t[3];
   for (int e = 0; e < 9; ++e) R[e] = st->R[e];
   for (int e = 0; e < 3; ++e) t[e] = st->t[e];
@@ -1824,11 +1889,23 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     // (nano_gicp_impl.hpp:257-258): a match iff a point was found and its
     // squared distance, promoted to double, is below max_corr^2
     int j = -1;
+    unsigned kj = 0xffffffffu;
+    float kd = INFINITY;
+    bool tied = false;
     if (active) {
       const unsigned long long k = key[i];
-      const unsigned kj = (unsigned)k;
-      const float kd = __uint_as_float((unsigned)(k >> 32));
+      kj = (unsigned)k;
+      kd = __uint_as_float((unsigned)(k >> 32));
       j = (kj != 0xffffffffu && (double)kd < max_corr2) ? (int)kj : -1;
+      // another examined point at the nearest distance: an exact tie
+      if (tie_detect && j >= 0) tied = job->sec[i] == (unsigned)(k >> 32);
+    }
+    // nanoflann's choice among the tied points (wave-uniform, rare)
+    if (tie_detect && __any(tied)) {
+      resolve_tied_corr(job, st, tgt, tied, i, kd, j, &tie_stk[wib]);
+      if (tied) kj = (unsigned)j;
+    }
+    if (active) {
       corr[i] = j;
       sqd[i] = kj != 0xffffffffu ? kd : INFINITY;
       // reuse reference of a query searched in a recording iteration: its
@@ -2720,6 +2797,21 @@ void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, con
 void launch_cov_remap(hipStream_t s, const double* old_cov6, const int* old_inv_perm, const int* new_perm, int n,
                       double* cov6) {
   k_cov_remap<<<cdiv(n, 256), 256, 0, s>>>(old_cov6, old_inv_perm, new_perm, n, cov6);
+}
+// slab shard tie order: whole-target original index -> local sorted position
+__global__ __launch_bounds__(256) void k_tie_map_clear(int n_full, int* __restrict__ map) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_full) map[i] = -1;
+}
+__global__ __launch_bounds__(256) void k_tie_map_scatter(const int* __restrict__ local_index,
+                                                         const int* __restrict__ inv_perm, int n_local,
+                                                         int* __restrict__ map) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_local) map[local_index[i]] = inv_perm[i];
+}
+void launch_tie_map(hipStream_t s, const int* local_index, const int* inv_perm, int n_local, int n_full, int* map) {
+  k_tie_map_clear<<<cdiv(n_full, 256), 256, 0, s>>>(n_full, map);
+  k_tie_map_scatter<<<cdiv(n_local, 256), 256, 0, s>>>(local_index, inv_perm, n_local, map);
 }
 void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src) {
   k_align_init<<<1, 128, 0, s>>>(job, job_src);

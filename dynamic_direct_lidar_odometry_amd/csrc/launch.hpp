@@ -43,6 +43,7 @@ bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq,
                       TieList ties = TieList{nullptr, nullptr});
 void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6);
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);
+void launch_tie_map(hipStream_t s, const int* local_index, const int* inv_perm, int n_local, int n_full, int* map);
 void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src);
 // tgt_upper: number of upper-level (>= 1) boxes of the target (LDS cache size)
 // Launch geometry of one linearize (grids, upper-box LDS cache), bucketed by

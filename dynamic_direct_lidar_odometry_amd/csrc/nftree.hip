@@ -53,8 +53,10 @@ __device__ __forceinline__ float o2f(unsigned o) {
 __device__ __forceinline__ float coord(const float4& p, int f) { return f == 0 ? p.x : (f == 1 ? p.y : p.z); }
 // Coordinate f of a point in memory: one load at a computed address.  (The
 // select form on a memory operand was lowered by ROCm 7.2's hipcc into a
-// per-lane branch that left the f == 2 lanes loading from an unset address:
-// wrong z splits in LDS, a fault in global memory.)
+// per-lane branch whose z address is computed under the f <= 0 branch's exec
+// mask, so the f == 2 lanes loaded from the loop index taken as an address:
+// wrong z splits in LDS, a fault in global memory.  ISA of the pre-fix code:
+// profiles/r04_fc2aa78_isa.md, tools/isa_fc2aa78.sh.)
 __device__ __forceinline__ float coord_at(const float4* p, int f) { return reinterpret_cast<const float*>(p)[f]; }
 
 // middleSplit_ (:1045-1087): cut dimension and value from the passed-down

@@ -575,6 +575,8 @@ gicp_status make_keyframe(ddlo_odom* o, const std::shared_ptr<CloudData>& scan) 
   launch_gather_cov6(o->s, side.cov->cov6.as<double>(), side.cloud->perm.as<int>(), m, kf->cov.as<double>());
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(o->s));
+  st = check_ties(o->s2s);   // the keyframe's (and the first scan's) covariance tie resolution
+  if (st) return st;
   o->keyframes.push_back(std::move(kf));
   return GICP_OK;
 }
@@ -739,6 +741,8 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
   if (n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "scan too large");
   gicp_status st = set_device(o->s2s);
   if (st) return st;
+  begin_ties(o->s2s);
+  begin_ties(o->s2m);
   std::memset(res, 0, sizeof(*res));
   copy_pose(o->T, res->T);
   copy_pose(o->T_s2s, res->T_s2s);

@@ -316,6 +316,11 @@ struct gicp_ctx {
   int* nf_err_host = nullptr;   // pinned copy of nf_err, read after the entry point's final wait
   bool nf_err_pending = false;
   long ties_resolved = 0;       // diagnostics
+  std::weak_ptr<NfTreeData> nf_joined;   // the target tree c->stream last waited for
+  // slab shard: the whole target the slab was cut from (its nanoflann tree
+  // orders the ties) and its original index -> local sorted position
+  std::shared_ptr<CloudData> tie_ref;
+  DevBuf tie_map;
 };
 
 namespace ddlo {
@@ -364,6 +369,17 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   if (!xyz || n == 0 || stride < 12 || (stride % 4) != 0) return fail(GICP_EINVAL, "invalid cloud (null, empty or bad stride)");
   if (n > (size_t)INT32_MAX / 2) return fail(GICP_EINVAL, "cloud too large");
   auto cd = std::make_shared<CloudData>();
+  // nf_early starts nanoflann's tree of cd on the aux stream; if this call
+  // then fails (non-finite input, a HIP error), cd and its buffers go back
+  // to the device pool: wait for the build first, so that no other ctx gets
+  // a block the aux stream still writes (DevicePool: idle when released)
+  struct AuxDrain {
+    gicp_ctx* c;
+    bool armed = false;
+    ~AuxDrain() {
+      if (armed) (void)hipStreamSynchronize(c->aux_stream);
+    }
+  } drain{c};
   const int N = (int)n;
   cd->n = N;
   cd->nlevels = levels_for(N, cd->lvl_cnt, cd->lvl_off);
@@ -408,6 +424,7 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
   launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
   if (nf_early && c->tie_exact) {
+    drain.armed = true;
     gicp_status st = ensure_nftree(c, *cd, s);
     if (st) return st;
   }
@@ -429,6 +446,7 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
     if (*c->flag_host) return fail(GICP_ENONFINITE, "cloud contains non-finite coordinates");
   }
   *out = cd;
+  drain.armed = false;   // the tree's owner (cd) lives on: its users wait on nf->ready
   return GICP_OK;
 }
 
@@ -610,6 +628,11 @@ inline gicp_status tie_scratch(gicp_ctx* c, int n, hipStream_t s, TieList* tl) {
   tl->cap = 2 * n;
   return GICP_OK;
 }
+
+// at the start of an entry point: a tie error word left pending by an
+// earlier call that failed before its check belongs to that call (already
+// reported as its failure), not to this one
+inline void begin_ties(gicp_ctx* c) { c->nf_err_pending = false; }
 
 // after the entry point's final wait: a failed tie resolution is an error
 // (the answers would silently carry the Morton tie order instead of nanoflann's)

@@ -157,8 +157,11 @@ class ShardedGicp:
         if len(idx) == 0:  # an empty rank still needs a valid cloud; it owns no queries
             idx = np.zeros(1, np.int64)
         self.local_index = idx
-        self.ctx.set_target(np.ascontiguousarray(np.asarray(points, np.float32)[idx, :3]))
+        whole = np.ascontiguousarray(np.asarray(points, np.float32)[:, :3])
+        self.ctx.set_target(np.ascontiguousarray(whole[idx]))
         self.ctx.set_covariances(TARGET, np.ascontiguousarray(covs[idx]))
+        # exact ties in the whole submap's nanoflann order (its tree, built once per submap)
+        self.ctx.set_tie_target(whole, idx)
         self.ctx.set_shard_groups(0, 0)
         self.ctx.set_shard(self.slab.axis, self.slab.lo, self.slab.hi)
         return self.slab

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DDLO_GICP_ABI_VERSION 1
+#define DDLO_GICP_ABI_VERSION 2
 
 typedef enum gicp_status {
   GICP_OK = 0,
@@ -101,6 +101,11 @@ typedef struct gicp_result {
   double device_ms;           /* device time of the align (HIP events)           */
   double linearize_ms;        /* summed device time of the linearize kernels
                                  (only when profiling is enabled, else 0)       */
+  int32_t ties_resolved;      /* correspondences whose nearest distance was an
+                                 exact tie, re-run in nanoflann's order          */
+  int32_t tie_reruns;         /* 1 if a tie appeared before the target had its
+                                 nanoflann tree: the tree was built and the
+                                 align run again (the result is the second run) */
 } gicp_result;
 
 /* ---- library / context --------------------------------------------------- */
@@ -248,6 +253,17 @@ gicp_status gicp_get_stream(const struct gicp_ctx* ctx, void** stream);
  * max_corr of an owned query lies in the slab + halo. */
 /* Ownership slab of this ctx; axis -1 removes it. */
 gicp_status gicp_set_shard(struct gicp_ctx* ctx, int axis, float lo, float hi);
+/* Exact ties for a slab shard: a slab's target is a subset of the submap, and
+ * nanoflann orders equidistant points by ITS tree, which differs from the
+ * whole submap's (nanoflann_impl.hpp:1045-1143 cut the subset's boxes).
+ * Give the ctx the whole target it was cut from and, for every local target
+ * point i (the cloud of the last gicp_set_target), its index local_index[i]
+ * in that whole cloud: tied correspondences are then re-run through the WHOLE
+ * target's nanoflann tree, as the unsharded reference resolves them.  The
+ * tree is built here, once per submap; gicp_set_target drops it.  n = 0
+ * removes it. */
+gicp_status gicp_set_tie_target(struct gicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes,
+                                const int32_t* local_index, size_t n_local);
 /* Interleaved sharding, for a target that fits every GPU (it is replicated):
  * rank `part` of `nparts` owns the source points whose 16-point group in the
  * device's spatial (Morton) order is congruent to part mod nparts, so every

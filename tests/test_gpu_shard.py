@@ -6,7 +6,8 @@ plumbing are checked separately:
     moments add up to the unsharded moments (fp64, rel 1e-10: only the
     summation order differs), matched counts exactly, and every owned
     query's correspondence equals the unsharded one (same squared distance,
-    bit-exact; same target point up to exact-distance ties);
+    bit-exact, and the same target point: exact ties resolve in the whole
+    submap's nanoflann order through gicp_set_tie_target);
   * a one-rank RCCL communicator: the align graph with the all-reduce
     inside returns the bit-identical pose, iteration count and residuals
     of the plain align.
@@ -56,19 +57,16 @@ def test_shard_moments_add_up(world):
         c.set_covariances(SOURCE, g["cov_src"])
         c.set_covariances(TARGET, g["cov_sub"][idx])
         c.set_shard(s.axis, s.lo, s.hi)
+        c.set_tie_target(g["sub"], idx)   # ties in the whole submap's nanoflann order
         _, _, _, n_r = c.linearize(pose)
         tot += c.moments()
         ntot += n_r
         corr, sqd = c.correspondences()
         mine = own == r
-        # owned queries: same exact distance; same point unless an exact tie
+        # owned queries: the unsharded correspondence, exact (ties included)
         np.testing.assert_array_equal(sqd[mine], fsqd[mine])
         gc = np.where(corr >= 0, idx[np.maximum(corr, 0)], -1)
-        diff = mine & (gc != fcorr)
-        if diff.any():
-            q = NP.transform_f32(pose, g["src"][diff])
-            d_alt = NP.nanoflann_sqd(q, g["sub"][gc[diff]])
-            np.testing.assert_array_equal(d_alt, fsqd[diff])
+        np.testing.assert_array_equal(gc[mine], fcorr[mine])
         c.close()
     assert ntot == nc
     np.testing.assert_allclose(tot[:74], mom[:74], rtol=1e-10, atol=1e-10 * np.abs(mom[:74]).max())
@@ -155,3 +153,41 @@ def test_shard_arguments_rejected():
     with pytest.raises(P.GicpError):
         c.set_comm(b"\0" * 128, 2, 5)
     c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_slab_shards_tied_target(knn_golden, world):
+    """Slab shards of a target full of exact ties (the reference-nanoflann
+    lattice fixture): every owned correspondence equals the unsharded one,
+    which equals the reference's own 1-NN."""
+    tgt = np.ascontiguousarray(knn_golden["lat_pts"])
+    src = np.ascontiguousarray(knn_golden["lat_q"])
+    rng = np.random.default_rng(3)
+    A = rng.normal(0, 0.05, (len(tgt), 3, 3))
+    tcov = NP.mat_to_sym6(A @ np.transpose(A, (0, 2, 1)) + 1e-3 * np.eye(3))
+    A = rng.normal(0, 0.05, (len(src), 3, 3))
+    scov = NP.mat_to_sym6(A @ np.transpose(A, (0, 2, 1)) + 1e-3 * np.eye(3))
+    par = dict(S2M, k_correspondences=10)
+    pose = np.eye(4)
+    ref = knn_golden["lat_k1_idx"][:, 0]
+    slabs = plan_slabs(tgt, world)
+    own = owner_of(NP.transform_f32(pose, src), slabs)
+    seen = np.zeros(len(src), bool)
+    for r, s in enumerate(slabs):
+        idx = halo_indices(tgt, s, par["max_correspondence_distance"])
+        c = P.Context(0)
+        c.set_params(P.default_params(**par))
+        c.set_target(np.ascontiguousarray(tgt[idx]))
+        c.set_covariances(TARGET, np.ascontiguousarray(tcov[idx]))
+        c.set_source(src)
+        c.set_covariances(SOURCE, np.ascontiguousarray(scov))
+        c.set_shard(s.axis, s.lo, s.hi)
+        c.set_tie_target(tgt, idx)
+        c.linearize(pose)
+        corr, _ = c.correspondences()
+        mine = own == r
+        gc = np.where(corr >= 0, idx[np.maximum(corr, 0)], -1)
+        np.testing.assert_array_equal(gc[mine], ref[mine])
+        seen |= mine
+        c.close()
+    assert seen.all()
