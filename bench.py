@@ -141,6 +141,29 @@ def varied_guesses(prob):
     return out
 
 
+def roofline_block(bytes_per_launch, launch_s, kernel, unit_bytes):
+    """roofline dict for a kernel (group): SURVEY.md §8(d) algorithmic bytes per launch / average launch time."""
+    ach = bytes_per_launch / launch_s / 1e9 if launch_s > 0 else 0.0
+    return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 6), "kernel": kernel, "avg_launch_us": round(launch_s * 1e6, 2),
+            "algorithmic_bytes_per_launch": int(bytes_per_launch), "bytes_rule": unit_bytes}
+
+
+def lin_roofline(ctx, guess, n_owned, reps=5):
+    """Linearize roofline of a ctx's align (HIP events on the library stream, gicp_set_profiling)."""
+    ctx.set_profiling(True)
+    ms, launches = 0.0, 0
+    for _ in range(reps):
+        _, r = ctx.align(guess)
+        ms += r.linearize_ms
+        launches += r.iterations_run
+    ctx.set_profiling(False)
+    ctx.synchronize()
+    return roofline_block(76.0 * n_owned, ms * 1e-3 / max(launches, 1),
+                          "linearize = k_nn_seed + k_nn_scan + k_moments (per outer iteration)",
+                          "B_lin = 76 B x owned source points")
+
+
 def rot_err(A, B):
     """Rotation angle between A and B: 2*asin(|RA - RB|_F / sqrt(8)) (well conditioned at 0)."""
     f = float(np.linalg.norm(A[:3, :3].astype(np.float64) - B[:3, :3].astype(np.float64)))
@@ -204,6 +227,8 @@ def sharded_leg(dist, rank, world, local_rank, args):
         elapsed = float(t[0])
     local_pts = len(sh.local_index)
     graphs = sh.ctx.comm_info()[2]
+    # per-rank linearize roofline (eager profiled aligns: the all-reduce sits outside the timed kernels)
+    roof = lin_roofline(sh.ctx, guess, len(src) / world, reps=3)
     sh.close()
     out_leg = {"workload": "cfg4 S2M: 262,144-pt 128x2048 scan -> 2,000,000-pt 8-keyframe submap, LM, maxCorr 2.0 m",
                "n_gpus": world, "ms_per_scan": round(1e3 * elapsed / args.sharded_steps, 4),
@@ -213,7 +238,7 @@ def sharded_leg(dist, rank, world, local_rank, args):
                "iters_per_s": round(iters / elapsed, 2), "iterations_per_scan": res.iterations_run,
                "converged": bool(res.converged), "target_points_per_rank_max": None,
                "collective": "RCCL all-reduce, 80 fp64 per outer iteration" + (" (in graph)" if graphs else " (eager)"),
-               "scaling": "strong"}
+               "scaling": "strong", "roofline_rank0": roof}
     if dist is not None:
         import torch
         t = torch.tensor([local_pts], dtype=torch.int64, device=f"cuda:{local_rank}")
@@ -285,7 +310,9 @@ def batched_leg(dist, rank, world, local_rank, args):
         P.s2s_batch(mine, params, device=local_rank, nstreams=args.batch_streams)
         el_m = time.perf_counter() - c0
     el_m, _ = reduce_over_ranks(dist, el_m, 0, f"cuda:{local_rank}")
-    return {"workload": f"cfg5 frame-parallel S2S: {npairs} pairs of {args.batch_frames} unique 64x2048 scans "
+    stages = cfg5_stage_rooflines(mine, params, local_rank) if rank == 0 else None
+    return {"cfg5_stages_rank0": stages,
+            "workload": f"cfg5 frame-parallel S2S: {npairs} pairs of {args.batch_frames} unique 64x2048 scans "
                         f"(closed plaza loop, moving pedestrians), k=10, maxCorr 1.0 m",
             "n_gpus": world, "streams_per_gpu": args.batch_streams, "pairs": npairs,
             "pairs_per_s": round(npairs / elapsed, 2), "ms_per_pair": round(1e3 * elapsed / npairs, 4),
@@ -293,6 +320,50 @@ def batched_leg(dist, rank, world, local_rank, args):
             "ms_per_pair_morton_tie_order": round(1e3 * el_m / npairs, 4),
             "per_pair_work": "H2D + index build + covariances (+ nanoflann's tree for the tie order) + align",
             "collective": "none (frames split by rank)"}
+
+
+def cfg5_stage_rooflines(frames, params, device, nframes=24):
+    """The per-scan stages of the cfg5 S2S leg, device-timed (HIP events) on one ctx over consecutive frames:
+    k=10 covariances (B_cov = 36 B x N), nanoflann's tree (tie order; B_idx = 32 B x N, SURVEY.md §8(d)'s
+    index-build figure), the S2S align's linearize (B_lin = 76 B x N_s)."""
+    import dynamic_direct_lidar_odometry_amd as P
+    from dynamic_direct_lidar_odometry_amd import SOURCE
+    c = P.Context(device)
+    c.set_params(params)
+    cov_s = tree_s = res_s = lin_s = 0.0
+    n_pts = lin_launch = tree_n = 0
+    fr = frames[:nframes + 1]
+    c.set_target(fr[0])
+    c.compute_covariances(1)
+    for t in range(1, len(fr)):
+        c.set_source(fr[t])
+        c.set_profiling(True)
+        c.compute_covariances(SOURCE)
+        cm, tm, rm = c.stage_times()
+        _, r = c.align()
+        c.set_profiling(False)
+        if t > 2:   # first frames: allocations and graph captures
+            cov_s += cm * 1e-3
+            res_s += rm * 1e-3
+            if tm > 0:
+                tree_s += tm * 1e-3
+                tree_n += len(fr[t])
+            n_pts += len(fr[t])
+            lin_s += r.linearize_ms * 1e-3
+            lin_launch += r.iterations_run
+        c.swap_source_target()
+    c.close()
+    k = max(len(fr) - 3, 1)
+    mean_n = n_pts / k
+    return {"frames": k, "mean_points": round(mean_n, 1),
+            "covariances": roofline_block(36.0 * mean_n, cov_s / k, "k_covariances2<10> (k-NN k=10 + PLANE)",
+                                          "B_cov = 36 B x N"),
+            "nanoflann_tree": roofline_block(32.0 * tree_n / k, tree_s / k,
+                                             "nanoflann tree build (k_nf_* graph, aux stream)",
+                                             "B_idx = 32 B x N (index-build figure)"),
+            "tie_resolvers_us": round(1e6 * res_s / k, 2),
+            "s2s_linearize": roofline_block(76.0 * mean_n, lin_s / max(lin_launch, 1),
+                                            "linearize = k_nn_seed + k_nn_scan + k_moments", "B_lin = 76 B x N_s")}
 
 
 class tie_order_env:
@@ -337,10 +408,12 @@ def s2s_gn_leg(local_rank, args):
         iters += r.iterations_run
     c.synchronize()
     el = time.perf_counter() - t0
+    roof = lin_roofline(c, None, len(src), reps=2)
     c.close()
     return {"workload": f"cfg2 S2S GICP: {len(src)}-pt -> {len(tgt)}-pt 64x2048 scans, 20 fixed GN iterations, "
                         "k=10, maxCorr 1.0 m", "iters_per_s": round(iters / el, 2),
-            "ms_per_align": round(1e3 * el / args.gn_steps, 4), "iterations_per_align": iters // args.gn_steps}
+            "ms_per_align": round(1e3 * el / args.gn_steps, 4), "iterations_per_align": iters // args.gn_steps,
+            "roofline": roof}
 
 
 def segmentation_leg(local_rank, args):

@@ -127,6 +127,7 @@ def load():
         "gicp_set_shard": (I, [P, I, C.c_float, C.c_float]),
         "gicp_set_shard_groups": (I, [P, I, I]),
         "gicp_set_tie_target": (I, [P, P, C.c_size_t, C.c_size_t, P, C.c_size_t]),
+        "gicp_get_stage_times": (I, [P, P]),
         "gicp_comm_unique_id": (I, [P, S]),
         "gicp_set_comm": (I, [P, P, S, I, I]),
         "gicp_get_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
@@ -386,6 +387,12 @@ class Context:
 
     def set_profiling(self, on=True):
         self._check(self.L.gicp_set_profiling(self.h, int(on)))
+
+    def stage_times(self):
+        """(covariance kernel, tree build, tie resolvers) device ms of the last profiled compute_covariances."""
+        t = (C.c_double * 3)()
+        self._check(self.L.gicp_get_stage_times(self.h, C.cast(t, C.c_void_p)))
+        return float(t[0]), float(t[1]), float(t[2])
 
     def synchronize(self):
         self._check(self.L.gicp_synchronize(self.h))

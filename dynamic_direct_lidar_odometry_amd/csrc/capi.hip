@@ -100,7 +100,7 @@ int env_int(const char* name, int dflt) {
 // process, not on every align (host time between aligns).
 struct SearchKnobs {
   float split_extent, hard_extent, probe, probe_d, tri_mv, reuse_gap, reuse_gap0, reuse_rec_eps, reuse_rec_conv;
-  int list_flush, xcd_scan, pf_ratio, hard_blocks, prev_window, reuse, reuse_rec0;
+  int list_flush, xcd_scan, pf_ratio, hard_blocks, prev_window, reuse, reuse_rec0, tie_scan;
 };
 const SearchKnobs& search_knobs() {
   static const SearchKnobs k = [] {
@@ -121,6 +121,7 @@ const SearchKnobs& search_knobs() {
     v.reuse_rec0 = env_int("DDLO_REUSE_REC0", 0);
     v.reuse_rec_eps = env_float("DDLO_REUSE_REC_EPS", 0.05f);
     v.reuse_rec_conv = env_float("DDLO_REUSE_REC_CONV", 10.f);
+    v.tie_scan = env_int("DDLO_TIE_SCAN", 2);   // 1 full second distance, 2 slice bests + winner-slice check; 0 = A/B only
     return v;
   }();
   return k;
@@ -227,6 +228,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.tgt_nf = NfTreeDev{nullptr, nullptr, nullptr, 0};
   j.tgt_nf_status = nullptr;
   j.tie_map = nullptr;
+  j.tie_scan = j.tie_detect ? kn.tie_scan : 0;
   if (j.tie_detect) {
     const CloudData* tc = c->tie_ref ? c->tie_ref.get() : c->tgt.cloud.get();
     if (tc->nf) {
@@ -625,6 +627,8 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   drop_graphs(c);
   if (c->comm) (void)rccl().comm_destroy(c->comm);
   for (auto e : c->prof_ev) (void)hipEventDestroy(e);
+  for (auto e : c->st_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto e : c->chunk_ev) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1176,6 +1180,28 @@ gicp_status gicp_debug_stats(gicp_ctx* c, int enable, unsigned int* out, size_t 
 gicp_status gicp_set_profiling(gicp_ctx* c, int enable) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
   c->profiling = enable != 0;
+  return GICP_OK;
+}
+
+gicp_status gicp_get_stage_times(gicp_ctx* c, gicp_stage_times* out) {
+  if (!c || !out) return fail(GICP_EINVAL, "null argument");
+  std::memset(out, 0, sizeof(*out));
+  if (!c->st_ev[0]) return fail(GICP_ESTATE, "no profiled compute_covariances on this ctx");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipStreamSynchronize(c->aux_stream));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, c->st_ev[0], c->st_ev[1]));
+  out->cov_ms = ms;
+  if (c->st_tree) {
+    HIP_TRY(hipEventElapsedTime(&ms, c->st_ev[2], c->st_ev[3]));
+    out->tree_ms = ms;
+  }
+  if (c->tie_exact) {
+    HIP_TRY(hipEventElapsedTime(&ms, c->st_ev[4], c->st_ev[5]));
+    out->resolve_ms = ms;
+  }
   return GICP_OK;
 }
 

@@ -202,6 +202,8 @@ struct AlignJob {
   // key's distance) and re-runs it through the target's nanoflann tree
   // (tgt_nf.nodes != nullptr), else sets AlignState::tie_pending.
   int tie_detect;
+  int tie_scan;                  // the scan's tie test: 1 second distance over every examined point, 2 the 8-point
+                                 // slices' losing bests + k_moments' check of the winner's slice, 0 none (A/B only)
   const int* tgt_nf_status;      // the tree build's error bits (device int; 0 = usable)
   NfTreeDev tgt_nf;              // nodes == nullptr: no tree (yet)
   const int* tie_map;            // tgt_nf is a whole cloud the target was cut from (slab shard): its original

@@ -1434,7 +1434,8 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   // bound (rec) and for k_moments' tie test (tie_detect): every point at the
   // final nearest distance is examined (its leaf is within the walk radius),
   // so the query is tied iff another examined point has that distance
-  const bool reuse = rec || job->tie_detect;
+  const bool reuse = rec || job->tie_scan;
+  const bool lane_sd = rec || job->tie_scan == 1;   // second distance over every point of a slice
   int run_sg = -1;
   unsigned long long acc = ~0ull;   // lane's query minimum over the current run
   float acc2 = INFINITY;            // smallest distance of the run's other points (reuse)
@@ -1542,13 +1543,22 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
         }
         const bool on = ((t >> qi) & 1ull) != 0ull;
         const int pos0 = (int)(t >> 40) * kLeafSize + s * 8;
-        if (reuse) {   // recording search: the leaf's best key and second distance (uniform branch)
+        if (reuse) {   // recording search / tie test: the leaf's best key and a second distance (uniform branch)
           float bd = INFINITY, sd = INFINITY;
           int bh = 0;
+          if (lane_sd) {   // every examined point: the reuse bound (and the full tie test)
 #pragma unroll
-          for (int h = 0; h < 8; ++h) {
-            const float dh = (h & 1) ? d[h / 2].y : d[h / 2].x;
-            if (dh < bd) { sd = bd; bd = dh; bh = h; } else { sd = fminf(sd, dh); }
+            for (int h = 0; h < 8; ++h) {
+              const float dh = (h & 1) ? d[h / 2].y : d[h / 2].x;
+              if (dh < bd) { sd = bd; bd = dh; bh = h; } else { sd = fminf(sd, dh); }
+            }
+          } else {   // tie test only: the slices' losing bests; a tie inside the winner's 8-point slice is
+                     // k_moments' own check
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+              const float dh = (h & 1) ? d[h / 2].y : d[h / 2].x;
+              if (dh < bd) { bd = dh; bh = h; }
+            }
           }
           unsigned long long bk = dkey(bd, pos0 + bh);
           xor_top2<16>(bk, sd);
@@ -1809,7 +1819,7 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job);
 // same distance.  Without a tree the align is flagged (tie_pending): the host
 // builds it and runs the align again.  Not inlined: the rare path keeps its
 // registers out of the moment loop.
-__device__ __noinline__ void resolve_tied_corr(const AlignJob* __restrict__ job, AlignState* st, const CloudDev& tgt,
+__device__ __forceinline__ void resolve_tied_corr(const AlignJob* __restrict__ job, AlignState* st, const CloudDev& tgt,
                                                bool tied, int i, float kd, int& j, NfWaveStack* S) {
   unsigned long long tm = __ballot(tied);
   const int lane = lane_id();
@@ -1870,6 +1880,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
   const int rec = st->rec;   // this iteration records reuse references
   const int first_rec_done = st->any_rec;   // an earlier iteration of this align recorded
   const int tie_detect = job->tie_detect;
+  const bool slice_check = tie_detect && job->tie_scan == 2;
   __shared__ NfWaveStack tie_stk[kMomWaves];   // nanoflann search frames of a tied query (per wave)
   double R[9], t[3];
   for (int e = 0; e < 9; ++e) R[e] = st->R[e];
@@ -1899,6 +1910,19 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       j = (kj != 0xffffffffu && (double)kd < max_corr2) ? (int)kj : -1;
       // another examined point at the nearest distance: an exact tie
       if (tie_detect && j >= 0) tied = job->sec[i] == (unsigned)(k >> 32);
+      // tie_scan 2: the scan compares only the 8-point slices' bests, so a
+      // second point at the distance inside the winner's own slice (the 8
+      // aligned sorted positions one lane scanned; the same 128-B line as the
+      // winner) is checked here, in the scan's fp32 arithmetic
+      if (slice_check && j >= 0 && !tied) {
+        const float4 qs = ldg4(job->qstate, i);
+        const int b0 = j & ~7;
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+          const float4 p = ldg4(tgt.pts, b0 + h);
+          tied = tied || (b0 + h != j && dist2(qs.x, qs.y, qs.z, p.x, p.y, p.z) == kd);
+        }
+      }
     }
     // nanoflann's choice among the tied points (wave-uniform, rare)
     if (tie_detect && __any(tied)) {

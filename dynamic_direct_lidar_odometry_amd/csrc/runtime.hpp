@@ -321,6 +321,9 @@ struct gicp_ctx {
   // orders the ties) and its original index -> local sorted position
   std::shared_ptr<CloudData> tie_ref;
   DevBuf tie_map;
+  // stage timing of compute_cov (profiling on): covariance kernel, tree build, resolvers
+  hipEvent_t st_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  bool st_tree = false;          // the last compute_cov built a tree (events 2, 3 recorded)
 };
 
 namespace ddlo {
@@ -466,6 +469,8 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   }
   if (!t->ready) HIP_TRY(hipEventCreateWithFlags(&t->ready, hipEventDisableTiming));
   t->n = n;
+  const bool timed = c->profiling && c->st_ev[2] && stop < 0 && !off;
+  if (timed) HIP_TRY(hipEventRecord(c->st_ev[2], s));
   // grids sized for a bucket of 16k points: one captured build graph serves
   // every cloud of the bucket (the kernels read the descriptor, and n, from
   // device memory), so a build is one graph launch, not ~80 kernel launches
@@ -595,6 +600,10 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   }
   HIP_TRY(hipMemcpyAsync(t->status.p, &b.ctl->err, sizeof(int), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(t->status.as<int>() + 1, &b.ctl->nnodes, sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (timed) {
+    HIP_TRY(hipEventRecord(c->st_ev[3], s));
+    c->st_tree = true;
+  }
   HIP_TRY(hipEventRecord(t->ready, s));
   return GICP_OK;
 }
@@ -661,6 +670,9 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   auto cv = std::make_shared<CovData>();
   cv->n = side.cloud->n;
   HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * (size_t)cv->n));
+  if (c->profiling && !c->st_ev[0])
+    for (auto& e : c->st_ev) HIP_TRY(hipEventCreate(&e));
+  c->st_tree = false;
   // DDLO_COV_TASKS=1: the task-based kNN (knn_tasks.hip) — exact, but not
   // faster than the lane-per-query kernel on the cfg 5 clouds
   const char* tv = std::getenv("DDLO_COV_TASKS");
@@ -674,6 +686,7 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     if (!st) st = tie_scratch(c, side.cloud->n, c->stream, &tl);
     if (st) return st;
   }
+  if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[0], c->stream));
   if (tasks && k <= 32) {
     // scratch of the task-based kNN; a queued covariance launch may still
     // read the old block, so growing it waits for the stream
@@ -737,10 +750,13 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   } else if (!launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), nullptr, tl)) {
     return fail(GICP_EINVAL, "unsupported k");
   }
+  if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[1], c->stream));
   if (c->tie_exact) {
     HIP_TRY(nftree_join(*side.cloud->nf, c->stream));
+    if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[4], c->stream));
     launch_nf_resolve_cov(c->stream, side.cloud->nf->dev(), cd, tl, k, c->params.regularization,
                           cv->cov6.as<double>(), side.cloud->nf->status.as<int>(), c->nf_err.as<int>());
+    if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[5], c->stream));
     gicp_status st = publish_ties(c, c->stream);
     if (st) return st;
     static const bool dbg = std::getenv("DDLO_TIE_DEBUG") != nullptr;   // development: tied queries per cloud

@@ -232,6 +232,16 @@ gicp_status gicp_get_moments(const struct gicp_ctx* ctx, double* out80);
 /* Device time accounting of the linearize kernel inside align (HIP events
  * captured in the align graph).  Off by default. */
 gicp_status gicp_set_profiling(struct gicp_ctx* ctx, int enable);
+/* With profiling on: device time (HIP events, on the streams the kernels run
+ * on) of the last gicp_compute_covariances on this ctx: the k-NN covariance
+ * kernel, nanoflann's tree build (tie order; 0 if the cloud already had its
+ * tree) and the tie resolvers.  Measurement entry (bench.py's roofline). */
+typedef struct gicp_stage_times {
+  double cov_ms;
+  double tree_ms;
+  double resolve_ms;
+} gicp_stage_times;
+gicp_status gicp_get_stage_times(struct gicp_ctx* ctx, gicp_stage_times* out);
 /* Diagnostics (development): enable per 64-query-group search counters for
  * subsequent linearize launches and/or read those of the last launch. */
 gicp_status gicp_debug_stats(struct gicp_ctx* ctx, int enable, unsigned int* out, size_t max_words, size_t* nwords);

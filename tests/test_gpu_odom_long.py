@@ -1,0 +1,96 @@
+"""cfg 5 at chain length: the odometry driver (include/ddlo_odom.h) against
+oracle/odom_ref.py over hundreds of consecutive 64x2048 frames of the
+1000-frame plaza loop (scene.loop_sequence, GPU ray caster: both sides get
+the same frames), long enough for the keyframe / submap logic of
+OdomNode::updateKeyframes and getSubmapKeyframes (odom.cc:1067-1154,
+993-1064, 1180-1315) to select among many keyframes.
+
+  * ddlo.yaml parameters, 210 frames: >= 5 keyframes, several submap
+    changes, the k-NN submap dropping early keyframes; every frame's status,
+    scan size, keyframe decision, keyframe count, submap index list and
+    change flag exact, S2S / S2M iteration counts exact, poses within the
+    north star's 1e-4.
+  * On this loop every keyframe is a vertex of the keyframes' convex hull and
+    the yaml's knn = kcv = 10, so the hull step never adds a keyframe the
+    k-NN step did not already take; a second chain with knn 2 / kcv 4 / kcc 4
+    (fixed 3 m keyframe distance) makes the convex-hull step drive submap
+    changes, and is held to the same bar.
+The concave hull (alpha = the keyframe distance) keeps no triangle of this
+near-planar trajectory; its GPU parity is tests/test_gpu_odom.py's
+32x512 sequence, its CPU restatement tests/test_odom_cpu.py.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from dynamic_direct_lidar_odometry_amd import odometry as OD
+from dynamic_direct_lidar_odometry_amd import scene
+from oracle import odom_ref as R
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16
+
+
+@pytest.fixture(scope="module")
+def frames210():
+    return scene.loop_sequence(64, 2048, 0, 210, device=0)[0]
+
+
+def knn_only(ref, nk, k):
+    c = ref.T_s2s[:3, 3]
+    ds = [math.sqrt(sum((float(c[j]) - float(kf[0][j])) ** 2 for j in range(3))) for kf in ref.keyframes[:nk]]
+    out = []
+    R.push_submap_indices(ds, k, list(range(nk)), out)
+    return set(out)
+
+
+def run_chain(frames, params):
+    gpu = OD.Odometry(0, params)
+    ref = R.OdomRef(params, threads=THREADS)
+    stats = dict(tracked=0, changes=0, hull_changes=0, dropped=0)
+    for i, f in enumerate(frames):
+        g = gpu.process(f)
+        o = ref.process(f)
+        assert g.status == o["status"], i
+        if g.status == OD.INIT:
+            continue
+        assert g.scan_points == o["scan_points"], i
+        assert g.keyframe_added == o["keyframe_added"], i
+        if g.status != OD.TRACKED:
+            continue
+        stats["tracked"] += 1
+        assert g.num_keyframes == o["num_keyframes"], i
+        sub = gpu.submap().tolist()
+        assert sub == o["submap"], i
+        assert g.submap_changed == o["submap_changed"], i
+        T = g.pose()
+        np.testing.assert_allclose(T[:3, 3], o["T"][:3, 3], atol=1e-4, err_msg=f"frame {i}")
+        np.testing.assert_allclose(T[:3, :3], o["T"][:3, :3], atol=1e-4, err_msg=f"frame {i}")
+        assert g.s2s.iterations_run == o["s2s"].iterations_run and g.s2m.iterations_run == o["s2m"].iterations_run, i
+        if o["submap_changed"]:
+            stats["changes"] += 1
+            nk = o["num_keyframes"] - o["keyframe_added"]   # the keyframes the submap was chosen from
+            if set(sub) - knn_only(ref, nk, params.submap_knn):
+                stats["hull_changes"] += 1
+            if len(sub) < nk:
+                stats["dropped"] += 1
+    gpu.close()
+    return stats, len(ref.keyframes)
+
+
+def test_cfg5_chain_210_frames_yaml(frames210):
+    p = OD.default_odom_params()
+    stats, nk = run_chain(frames210, p)
+    assert stats["tracked"] >= 200
+    assert nk >= 5, nk
+    assert stats["changes"] >= 4, stats
+
+
+def test_cfg5_chain_hull_driven_submaps(frames210):
+    p = OD.default_odom_params(submap_knn=2, submap_kcv=4, submap_kcc=4, adaptive=0, keyframe_thresh_dist=3.0)
+    stats, nk = run_chain(frames210[:150], p)
+    assert nk >= 5, nk
+    assert stats["hull_changes"] >= 1, stats
+    assert stats["dropped"] >= 1, stats
