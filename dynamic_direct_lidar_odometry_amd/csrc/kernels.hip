@@ -254,7 +254,23 @@ __global__ __launch_bounds__(256) void k_level_boxes(const float4* __restrict__ 
 // ============================================================================
 // K2: exact kNN-k (self queries) + covariance
 // ============================================================================
-template <int KCAP, bool EXACT>
+// Kept-neighbour list storage: registers, or (KLDS: k up to 64, where a
+// register list of 64 u64 keys spilled 213 VGPRs) a lane-interleaved LDS
+// array, slot s of a lane at p[64 s].
+template <int KCAP, bool KLDS>
+struct KeyList {
+  unsigned long long v[KCAP];
+  __device__ __forceinline__ unsigned long long& operator[](int s) { return v[s]; }
+  __device__ __forceinline__ const unsigned long long& operator[](int s) const { return v[s]; }
+};
+template <int KCAP>
+struct KeyList<KCAP, true> {
+  unsigned long long* p;   // the lane's slot 0 (LDS)
+  __device__ __forceinline__ unsigned long long& operator[](int s) { return p[64 * s]; }
+  __device__ __forceinline__ const unsigned long long& operator[](int s) const { return p[64 * s]; }
+};
+
+template <int KCAP, bool EXACT, bool KLDS = false>
 struct KnnVisitor : VisitStats {
   WaveBox box;
   float qx, qy, qz;
@@ -263,7 +279,7 @@ struct KnnVisitor : VisitStats {
   // kept neighbours as order-preserving (squared distance, sorted position)
   // keys, ascending: the exact rule (d < D) || (d == D && j < J) of
   // KNNResultSet + the position tie-break is one u64 compare per slot
-  unsigned long long K[KCAP];
+  KeyList<KCAP, KLDS> K;
   unsigned long long wk;   // worst kept key (bound)
   float wd;                // its distance
   float tight;             // min over the tested full leaves of the farthest-corner distance (squared)
@@ -324,13 +340,29 @@ struct KnnVisitor : VisitStats {
     wd = __uint_as_float((unsigned)(wk >> 32));
   }
   __device__ __forceinline__ void insert(unsigned long long key) {
+    if constexpr (KLDS) {   // sorted shift from the end (the list lives in LDS)
+      const unsigned long long out = K[KCAP - 1];
+      if (key >= out) {
+        td = fminf(td, key_dist(key));
+        return;
+      }
+      int s = KCAP - 1;
+      for (; s > 0; --s) {
+        const unsigned long long prev = K[s - 1];
+        if (prev <= key) break;
+        K[s] = prev;
+      }
+      K[s] = key;
+      td = fminf(td, key_dist(out));   // the key pushed out of the list
+    } else {
 #pragma unroll
-    for (int s = 0; s < KCAP; ++s) {
-      const unsigned long long lo = umin64(key, K[s]);
-      key = key < K[s] ? K[s] : key;
-      K[s] = lo;
+      for (int s = 0; s < KCAP; ++s) {
+        const unsigned long long lo = umin64(key, K[s]);
+        key = key < K[s] ? K[s] : key;
+        K[s] = lo;
+      }
+      td = fminf(td, key_dist(key));   // the key pushed out of the list
     }
-    td = fminf(td, key_dist(key));   // the key pushed out of the list
     update_worst();
   }
   // the k-th neighbour is no farther than the kept k-th key, nor than the
@@ -363,9 +395,8 @@ struct KnnVisitor : VisitStats {
 // (nano_gicp_impl.hpp:392-399), regularised, stored as sym6.  The neighbour
 // points are loaded four at a time (compiler barriers between the groups):
 // with all KCAP loads hoisted, k = 20 held 20 float4s live and spilled.
-template <int KCAP>
-__device__ __forceinline__ void cov_from_keys(const CloudDev& c, const unsigned long long (&K)[KCAP], int k, int method,
-                                              double* o) {
+template <int KCAP, class KL>
+__device__ __forceinline__ void cov_from_keys(const CloudDev& c, const KL& K, int k, int method, double* o) {
   double mx = 0, my = 0, mz = 0;
 #pragma unroll
   for (int s = 0; s < KCAP; ++s) {
@@ -399,8 +430,8 @@ __device__ __forceinline__ void cov_from_keys(const CloudDev& c, const unsigned 
 }
 
 // Seed a kNN visitor with the leaves [s0, s1] and then run the full traversal.
-template <int KCAP, bool EXACT>
-__device__ __forceinline__ void knn_search(const CloudDev& c, KnnVisitor<KCAP, EXACT>& vis, int s0, int s1,
+template <int KCAP, bool EXACT, bool KLDS>
+__device__ __forceinline__ void knn_search(const CloudDev& c, KnnVisitor<KCAP, EXACT, KLDS>& vis, int s0, int s1,
                                            WaveLds* L) {
   s0 = max(s0, 0);
   s1 = min(s1, c.cnt0 - 1);
@@ -413,8 +444,8 @@ __device__ __forceinline__ void knn_search(const CloudDev& c, KnnVisitor<KCAP, E
 
 // kNN-k of the cloud's own points: seed with the group's own leaves, then a
 // split search (keys = the cloud's sorted Morton keys)
-template <int KCAP, bool EXACT>
-__device__ __forceinline__ void knn_self_search(const CloudDev& c, KnnVisitor<KCAP, EXACT>& vis, int s0, int s1,
+template <int KCAP, bool EXACT, bool KLDS>
+__device__ __forceinline__ void knn_self_search(const CloudDev& c, KnnVisitor<KCAP, EXACT, KLDS>& vis, int s0, int s1,
                                                 unsigned long long key, WaveLds* L) {
   s0 = max(s0, 0);
   s1 = min(s1, c.cnt0 - 1);
@@ -432,7 +463,9 @@ __device__ __forceinline__ void knn_self_search(const CloudDev& c, KnnVisitor<KC
 template <int KCAP, bool EXACT>
 __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int method, double* __restrict__ cov6,
                                                      const unsigned char* __restrict__ redo, TieList ties) {
+  constexpr bool KLDS = KCAP > 32;
   __shared__ WaveLds lds[4];
+  __shared__ unsigned long long klist[KLDS ? 4 * 64 * KCAP : 1];   // KLDS: the kept lists (128 KB at k <= 64)
   WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
@@ -440,7 +473,8 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
   for (int g = wave; g < ngroups; g += nwaves_total) {
     if (redo && !redo[g]) continue;   // only the groups the task path could not finish
     const int i = g * 64 + lane_id();
-    KnnVisitor<KCAP, EXACT> vis;
+    KnnVisitor<KCAP, EXACT, KLDS> vis;
+    if constexpr (KLDS) vis.K.p = klist + (size_t)(threadIdx.x >> 6) * 64 * KCAP + lane_id();
     vis.init(k);
     vis.nfull = k <= kLeafSize ? c.n / kLeafSize : 0;   // a full leaf holds >= k points only if k <= 32
     vis.active = i < c.n;
@@ -577,14 +611,17 @@ template __global__ void k_covariances2<20, true, 2>(CloudDev, int, int, double*
 template <int KCAP, bool EXACT>
 __global__ __launch_bounds__(256) void k_knn_query(CloudDev c, const float4* __restrict__ q, int nq, int k,
                                                    int* __restrict__ out_idx, float* __restrict__ out_d, TieList ties) {
+  constexpr bool KLDS = KCAP >= 32;   // a register list of 32 keys spilled here (156 VGPRs)
   __shared__ WaveLds lds[4];
+  __shared__ unsigned long long klist[KLDS ? 4 * 64 * KCAP : 1];
   WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
   const int ngroups = (nq + 63) >> 6;
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const int i = g * 64 + lane_id();
-    KnnVisitor<KCAP, EXACT> vis;
+    KnnVisitor<KCAP, EXACT, KLDS> vis;
+    if constexpr (KLDS) vis.K.p = klist + (size_t)(threadIdx.x >> 6) * 64 * KCAP + lane_id();
     vis.init(k);
     vis.nfull = k <= kLeafSize ? c.n / kLeafSize : 0;   // a full leaf holds >= k points only if k <= 32
     vis.active = i < nq;

@@ -80,6 +80,54 @@ def test_cfg4_group_shards_add_up(cfg4, world):
     np.testing.assert_allclose(tot[:74], mom[:74], rtol=1e-10, atol=1e-10 * np.abs(mom[:74]).max())
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_cfg4_slab_shards_add_up(cfg4, world):
+    """Slab mode at cfg 4 size (the spatial tiling of north_star / SURVEY.md §8(e)): N contexts on one device,
+    each with its slab + 2 m halo of the 2M-point submap (slabs cut on the source at the guess) and the
+    whole submap as its tie order (gicp_set_tie_target).  Moments add up (rel 1e-10), matched counts add
+    up, every owned correspondence equals the unsharded one exactly (ties included).  Prints the per-rank
+    linearize time (ranks run one after another here) for DESIGN.md's critical-path table."""
+    from dynamic_direct_lidar_odometry_amd.shard import halo_indices, owner_of, plan_slabs_by_source, transform_f32
+    pose = cfg4["guess"].astype(np.float64)
+    full = _ctx(cfg4)
+    _, _, _, nc = full.linearize(pose)
+    mom = full.moments()
+    fcorr, fsqd = full.correspondences()
+    full.close()
+    slabs = plan_slabs_by_source(cfg4["src"], pose, world)
+    own = owner_of(transform_f32(cfg4["src"], pose), slabs)
+    tot = np.zeros(80)
+    ntot = 0
+    rows = []
+    for r, sl in enumerate(slabs):
+        idx = halo_indices(cfg4["sub"], sl, S2M["max_correspondence_distance"])
+        c = P.Context(0)
+        c.set_params(P.default_params(**S2M))
+        c.set_target(np.ascontiguousarray(cfg4["sub"][idx]))
+        c.set_covariances(TARGET, np.ascontiguousarray(cfg4["tcov"][idx]))
+        c.set_source(cfg4["src"])
+        c.set_covariances(SOURCE, cfg4["scov"])
+        c.set_shard(sl.axis, sl.lo, sl.hi)
+        c.set_tie_target(cfg4["sub"], idx)
+        _, _, _, n_r = c.linearize(pose)
+        tot += c.moments()
+        ntot += n_r
+        corr, sqd = c.correspondences()
+        mine = own == r
+        gc = np.where(corr >= 0, idx[np.maximum(corr, 0)], -1)
+        np.testing.assert_array_equal(gc[mine], fcorr[mine])
+        np.testing.assert_array_equal(sqd[mine], fsqd[mine])
+        c.set_profiling(True)
+        _, res = c.align(cfg4["guess"])
+        c.set_profiling(False)
+        rows.append((r, int(mine.sum()), len(idx), res.linearize_ms / max(res.iterations_run, 1) * 1e3))
+        c.close()
+    assert ntot == nc
+    np.testing.assert_allclose(tot[:74], mom[:74], rtol=1e-10, atol=1e-10 * np.abs(mom[:74]).max())
+    for r, nq, nt, us in rows:
+        print(f"slab world {world} rank {r}: owned queries {nq}, target points {nt}, linearize {us:.1f} us")
+
+
 def test_cfg4_comm1_pose_vs_oracle(cfg4):
     sh = ShardedGicp(0, 0, 1, P.comm_unique_id(), P.default_params(**S2M))
     sh.set_target(cfg4["sub"], cfg4["tcov"])
