@@ -50,7 +50,14 @@ __device__ __forceinline__ float o2f(unsigned o) {
   const unsigned u = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
   return __uint_as_float(u);
 }
-__device__ __forceinline__ float coord(const float4& p, int f) { return f == 0 ? p.x : (f == 1 ? p.y : p.z); }
+// Coordinate f of a point in registers, as a bit-mask blend: LLVM folds a
+// select chain on f (either form) into an element extract at a runtime
+// index, i.e. a store of the float4 to scratch and an indexed load
+// (k_nf_pass<2, false> had 144 B of scratch).
+__device__ __forceinline__ float coord(const float4& p, int f) {
+  const unsigned mx = 0u - (unsigned)(f == 0), my = 0u - (unsigned)(f == 1), mz = 0u - (unsigned)(f == 2);
+  return __uint_as_float((__float_as_uint(p.x) & mx) | (__float_as_uint(p.y) & my) | (__float_as_uint(p.z) & mz));
+}
 // Coordinate f of a point in memory: one load at a computed address.  (The
 // select form on a memory operand was lowered by ROCm 7.2's hipcc into a
 // per-lane branch whose z address is computed under the f <= 0 branch's exec
@@ -131,7 +138,7 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 // exclusive prefix of v over the block (thread order); *total = sum
-__device__ int block_excl_scan(int v, int* total, int* sh /* >= 17 ints */) {
+__device__ __forceinline__ int block_excl_scan(int v, int* total, int* sh /* >= 17 ints */) {
   const int lane = __lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int inc = wave_incl_scan(v);
   if (lane == 63) sh[w] = inc;
@@ -151,7 +158,7 @@ __device__ int block_excl_scan(int v, int* total, int* sh /* >= 17 ints */) {
   __syncthreads();
   return r;
 }
-__device__ int block_sum(int v, int* sh) {
+__device__ __forceinline__ int block_sum(int v, int* sh) {
   int tot;
   (void)block_excl_scan(v, &tot, sh);
   return tot;
@@ -176,7 +183,7 @@ __device__ __forceinline__ bool task_of_block(const NfBuild& b, int L, TaskView*
 }
 
 // sums of a per-chunk count over the task's chunks: all of them, and those before blk
-__device__ void task_chunk_sums(const int* cnt, const NfTask& tk, int blk, int* total, int* before, int* sh) {
+__device__ __forceinline__ void task_chunk_sums(const int* cnt, const NfTask& tk, int blk, int* total, int* before, int* sh) {
   int a = 0, p = 0;
   for (int c = tk.chunk0 + (int)threadIdx.x; c < tk.chunk0 + tk.nch; c += blockDim.x) {
     const int v = cnt[c];
@@ -397,7 +404,7 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ b
 #pragma unroll
   for (int j = 0; j < kNfPer; ++j) {
     const int p = p0 + j;
-    if (p >= tk.count) break;
+    if (p >= tk.count) continue;   // (p grows with j: the rest are past the task too; continue keeps e[] in registers)
     const float x = coord(e[j], feat);
     const bool good = PASS == 1 ? (x < cut) : (x == cut);
     float4 out = e[j];
@@ -433,8 +440,12 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ b
     // the split index, the children's point min / max, and (one thread per
     // task) the node record and the children's pending entries
     const int index = nf_index(tk.count, lim1, lim2);
+    // the two children's min / max, constant indices only (registers, no
+    // private-memory array: a runtime child index put m[][] on the stack)
     float m[2][6];
+#pragma unroll
     for (int s = 0; s < 2; ++s)
+#pragma unroll
       for (int a = 0; a < 3; ++a) {
         m[s][a] = INFINITY;
         m[s][3 + a] = -INFINITY;
@@ -442,22 +453,23 @@ __global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ b
 #pragma unroll
     for (int j = 0; j < kNfPer; ++j) {
       const int p = p0 + j;
-      if (p >= tk.count) break;
-      const int s = p < index ? 0 : 1;
+      const bool in = p < tk.count;
+      const bool left = p < index;
       const float cc[3] = {e[j].x, e[j].y, e[j].z};
+#pragma unroll
       for (int a = 0; a < 3; ++a) {
-        if (s == 0) {
-          m[0][a] = fminf(m[0][a], cc[a]);
-          m[0][3 + a] = fmaxf(m[0][3 + a], cc[a]);
-        } else {
-          m[1][a] = fminf(m[1][a], cc[a]);
-          m[1][3 + a] = fmaxf(m[1][3 + a], cc[a]);
-        }
+        const float lo_c = in ? cc[a] : INFINITY, hi_c = in ? cc[a] : -INFINITY;
+        m[0][a] = fminf(m[0][a], left ? lo_c : INFINITY);
+        m[0][3 + a] = fmaxf(m[0][3 + a], left ? hi_c : -INFINITY);
+        m[1][a] = fminf(m[1][a], left ? INFINITY : lo_c);
+        m[1][3 + a] = fmaxf(m[1][3 + a], left ? -INFINITY : hi_c);
       }
     }
     NfTask* C = b.pend + (size_t)(L + 1) * b.max_pend;
     __shared__ unsigned smm[kNfBT / 64][12];
+#pragma unroll
     for (int s = 0; s < 2; ++s)
+#pragma unroll
       for (int a = 0; a < 6; ++a) {
         float x = m[s][a];
         for (int d = 32; d >= 1; d >>= 1) {
