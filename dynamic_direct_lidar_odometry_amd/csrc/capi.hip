@@ -121,7 +121,7 @@ const SearchKnobs& search_knobs() {
     v.reuse_rec0 = env_int("DDLO_REUSE_REC0", 0);
     v.reuse_rec_eps = env_float("DDLO_REUSE_REC_EPS", 0.05f);
     v.reuse_rec_conv = env_float("DDLO_REUSE_REC_CONV", 10.f);
-    v.tie_scan = env_int("DDLO_TIE_SCAN", 2);   // 1 full second distance, 2 slice bests + winner-slice check; 0 = A/B only
+    v.tie_scan = env_int("DDLO_TIE_SCAN", 3);   // 1 / 2 / 3 (see AlignJob::tie_scan); 0 = A/B only
     return v;
   }();
   return k;
@@ -129,7 +129,7 @@ const SearchKnobs& search_knobs() {
 
 // byte layout of ctx->search for ns source points
 struct SearchLayout {
-  size_t qstate, key, ctr, hard_list, hard_flag, grp_blocks, ref, ref_p, sec, tasks, total;
+  size_t qstate, key, ctr, hard_list, hard_flag, grp_blocks, ref, ref_p, sec, key2, tasks, total;
   int cap_r;
   explicit SearchLayout(int ns) {
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -143,7 +143,8 @@ struct SearchLayout {
     ref = grp_blocks + al(sizeof(unsigned short) * ((size_t)ns / 16 + 16));
     ref_p = ref + al(sizeof(float4) * (size_t)ns);
     sec = ref_p + al(sizeof(float4) * (size_t)ns);
-    tasks = sec + al(sizeof(unsigned) * (size_t)ns);
+    key2 = sec + al(sizeof(unsigned) * (size_t)ns);
+    tasks = key2 + al(sizeof(unsigned long long) * (size_t)ns);
     total = tasks + sizeof(unsigned long long) * (size_t)kTaskRegions * cap_r;
   }
 };
@@ -200,6 +201,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
     j.ref = reinterpret_cast<float4*>(u + sl.ref);
     j.ref_p = reinterpret_cast<float4*>(u + sl.ref_p);
     j.sec = reinterpret_cast<unsigned*>(u + sl.sec);
+    j.key2 = reinterpret_cast<unsigned long long*>(u + sl.key2);
   }
   j.list_flush = kn.list_flush;
   j.xcd_scan = kn.xcd_scan;
@@ -1198,7 +1200,7 @@ gicp_status gicp_get_stage_times(gicp_ctx* c, gicp_stage_times* out) {
     HIP_TRY(hipEventElapsedTime(&ms, c->st_ev[2], c->st_ev[3]));
     out->tree_ms = ms;
   }
-  if (c->tie_exact) {
+  if (c->st_resolve) {
     HIP_TRY(hipEventElapsedTime(&ms, c->st_ev[4], c->st_ev[5]));
     out->resolve_ms = ms;
   }

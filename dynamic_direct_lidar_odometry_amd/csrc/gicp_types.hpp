@@ -195,6 +195,9 @@ struct AlignJob {
   float4* ref;                   // [n_src] q_ref (x, y, z) + B^2 (< 0: no reference)
   float4* ref_p;                 // [n_src] p1 (x, y, z) + its sorted target position as int bits (-1: none within the bound)
   unsigned* sec;                 // [n_src] fp32 bits: smallest squared distance of an examined non-best point
+                                 // (tie_scan 3: 0 = an equal-distance merge flagged the query)
+  unsigned long long* key2;      // [n_src] tie_scan 3: the search's minimum of (squared distance, ~position), the
+                                 // mirror of `key`: the same distance with a different point = a tie across runs
   // Exact ties of update_correspondences' 1-NN (nano_gicp_impl.hpp:255 ->
   // nanoflann_impl.hpp:205-237,1509: the first equidistant point of
   // nanoflann's walk wins).  tie_detect: k_moments flags a matched query whose
@@ -203,7 +206,8 @@ struct AlignJob {
   // (tgt_nf.nodes != nullptr), else sets AlignState::tie_pending.
   int tie_detect;
   int tie_scan;                  // the scan's tie test: 1 second distance over every examined point, 2 the 8-point
-                                 // slices' losing bests + k_moments' check of the winner's slice, 0 none (A/B only)
+                                 // slices' losing bests + k_moments' check of the winner's slice, 3 equal-distance
+                                 // flags at the merges + the mirrored key + the winner's slice check, 0 none (A/B)
   const int* tgt_nf_status;      // the tree build's error bits (device int; 0 = usable)
   NfTreeDev tgt_nf;              // nodes == nullptr: no tree (yet)
   const int* tie_map;            // tgt_nf is a whole cloud the target was cut from (slab shard): its original

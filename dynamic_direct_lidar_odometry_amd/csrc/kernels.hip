@@ -1024,6 +1024,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
         keyout[i] = passed ? pass_key : dkey(INFINITY, -1);
         qstate[i] = make_float4(qx, qy, qz, -1.f);
         if (job->tie_detect) job->sec[i] = __float_as_uint(INFINITY);   // proven strict: no tie
+        if (job->tie_scan == 3) job->key2[i] = mirror_key(passed ? pass_key : dkey(INFINITY, -1));
       }
       if (lane == 0) {
         job->hard_flag[g] = 2;   // nothing to search: k_nn_collect skips the sub-group
@@ -1254,6 +1255,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     if (!FUSED && inrange && lane < Q) {
       qstate[i] = make_float4(qx, qy, qz, active ? wr : -1.f);
       keyout[i] = active ? dkey(vis.best, vis.bestj) : passed ? pass_key : dkey(INFINITY, -1);
+      if (job->tie_scan == 3) job->key2[i] = mirror_key(keyout[i]);
     }
     if constexpr (FUSED) {
       // the walk of k_nn_collect, from the seed in registers
@@ -1278,7 +1280,9 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       col.run(tgt, tl, gp(src.keys)[ic], job->split_extent);
       if (inrange && lane < Q) {
         qstate[i] = make_float4(qx, qy, qz, active ? wr : -1.f);
-        keyout[i] = active ? col.bk : passed ? pass_key : dkey(INFINITY, -1);   // col.bk: the seed, lowered by inline scans
+        const unsigned long long k_out = active ? col.bk : passed ? pass_key : dkey(INFINITY, -1);
+        keyout[i] = k_out;   // col.bk: the seed, lowered by inline scans
+        if (job->tie_scan == 3) job->key2[i] = mirror_key(k_out);
       }
       // the examined points' second distance: the reuse bound (rec) and the
       // tie test of k_moments (sec == the key's distance); k_nn_scan lowers it
@@ -1393,7 +1397,10 @@ __global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __rest
   col.sg = g;
   col.pf_ratio = job->pf_ratio;
   col.run(tgt, tl, skey, job->split_extent);
-  if (inrange && lane < Q && col.bk != k0) keyout[i] = col.bk;   // lowered by inline scans
+  if (inrange && lane < Q && col.bk != k0) {
+    keyout[i] = col.bk;   // lowered by inline scans
+    if (job->tie_scan == 3) job->key2[i] = mirror_key(col.bk);
+  }
   if ((st->rec || job->tie_detect) && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further
   if (lane == 0) job->grp_blocks[g] = (unsigned short)min(col.st_blocks, 65535u);
   if (stats && lane == 0) {
@@ -1471,8 +1478,14 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   // bound (rec) and for k_moments' tie test (tie_detect): every point at the
   // final nearest distance is examined (its leaf is within the walk radius),
   // so the query is tied iff another examined point has that distance
-  const bool reuse = rec || job->tie_scan;
+  const bool reuse = rec || (job->tie_scan == 1 || job->tie_scan == 2);
   const bool lane_sd = rec || job->tie_scan == 1;   // second distance over every point of a slice
+  // tie_scan 3 (not recording): the Morton-order scan plus equal-distance
+  // flags at its merges (slices, tasks of a run) and the mirrored key pushed
+  // beside the key (runs): no atomic return is waited for
+  const bool tie3 = !rec && job->tie_scan == 3;
+  unsigned long long* const key2 = job->key2;
+  unsigned td = 0xffffffffu;   // smallest distance (bits) met twice at a merge of this run's keys (any slice lane)
   int run_sg = -1;
   unsigned long long acc = ~0ull;   // lane's query minimum over the current run
   float acc2 = INFINITY;            // smallest distance of the run's other points (reuse)
@@ -1514,7 +1527,14 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
         pend_bound = run_bound;
       } else {
         atomicMin(key + qidx, acc);
+        if (tie3) atomicMin(key2 + qidx, mirror_key(acc));
       }
+    }
+    if (tie3 && run_sg >= 0) {   // the run's tie distances of the query's four slice lanes -> its lane qi
+      unsigned t = min(td, (unsigned)__shfl_xor((int)td, 16));
+      t = min(t, (unsigned)__shfl_xor((int)t, 32));
+      if (lane < 16 && t <= __float_as_uint(run_bound))   // rare: a real equal-distance pair
+        atomicMin(sec + (size_t)run_sg * kTaskQ + qi, t);   // k_moments: tied iff it is the final distance
     }
   };
   for (int wbase = lo; wbase < hi; wbase += 64) {
@@ -1557,6 +1577,7 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
           acc = ~0ull;
           acc2 = INFINITY;
           run_bound = -1.f;
+          td = 0xffffffffu;
         }
         const unsigned char* T = cur + k * kScanTaskBytes;
         const f4v x0 = *(const f4v*)(T + s * 32), x1 = *(const f4v*)(T + s * 32 + 16);
@@ -1610,9 +1631,22 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
             if (dh < bd) { bd = dh; bh = h; }
           }
           unsigned long long bk = dkey(bd, pos0 + bh);
-          bk = xor_min64<16>(bk);
-          bk = xor_min64<32>(bk);
-          if (on) acc = umin64(acc, bk);
+          if (tie3) {   // equal distances meeting at a merge: a tie (two points of one slice: k_moments' check)
+            unsigned tt = 0xffffffffu;
+            bk = xor_min64_eq<16>(bk, tt);
+            bk = xor_min64_eq<32>(bk, tt);
+            if (on) {
+              // a leaf met again in the same run (two walk entries) is the same key, not a tie
+              const unsigned hb = (unsigned)(bk >> 32);
+              if (hb == (unsigned)(acc >> 32) && bk != acc) tt = min(tt, hb);
+              td = min(td, tt);
+              acc = umin64(acc, bk);
+            }
+          } else {
+            bk = xor_min64<16>(bk);
+            bk = xor_min64<32>(bk);
+            if (on) acc = umin64(acc, bk);
+          }
         }
         if (on) run_bound = q.w;
       }
@@ -1917,7 +1951,8 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
   const int rec = st->rec;   // this iteration records reuse references
   const int first_rec_done = st->any_rec;   // an earlier iteration of this align recorded
   const int tie_detect = job->tie_detect;
-  const bool slice_check = tie_detect && job->tie_scan == 2;
+  const bool slice_check = tie_detect && job->tie_scan >= 2;
+  const bool tie3m = tie_detect && job->tie_scan == 3 && !rec;   // the mirrored key of a non-recording search
   __shared__ NfWaveStack tie_stk[kMomWaves];   // nanoflann search frames of a tied query (per wave)
   double R[9], t[3];
   for (int e = 0; e < 9; ++e) R[e] = st->R[e];
@@ -1945,19 +1980,28 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       kj = (unsigned)k;
       kd = __uint_as_float((unsigned)(k >> 32));
       j = (kj != 0xffffffffu && (double)kd < max_corr2) ? (int)kj : -1;
-      // another examined point at the nearest distance: an exact tie
-      if (tie_detect && j >= 0) tied = job->sec[i] == (unsigned)(k >> 32);
+      // another examined point at the nearest distance: an exact tie (tie_scan
+      // 3: sec 0 = flagged, or the mirrored key names another point)
+      if (tie_detect && j >= 0) {
+        const unsigned sv = job->sec[i];
+        tied = sv <= (unsigned)(k >> 32);
+        if (tie3m) tied = tied || (unsigned)job->key2[i] != ((unsigned)k ^ 0xffffffffu);
+      }
       // tie_scan 2: the scan compares only the 8-point slices' bests, so a
       // second point at the distance inside the winner's own slice (the 8
       // aligned sorted positions one lane scanned; the same 128-B line as the
       // winner) is checked here, in the scan's fp32 arithmetic
       if (slice_check && j >= 0 && !tied) {
-        const float4 qs = ldg4(job->qstate, i);
+        // the search's fp32 query, recomputed (k_nn_seed's transform, same operations)
+        const float4 a = ldg4(src.pts, i);
+        const float qx = ((float)R[0] * a.x + (float)R[1] * a.y) + ((float)R[2] * a.z + (float)t[0]);
+        const float qy = ((float)R[3] * a.x + (float)R[4] * a.y) + ((float)R[5] * a.z + (float)t[1]);
+        const float qz = ((float)R[6] * a.x + (float)R[7] * a.y) + ((float)R[8] * a.z + (float)t[2]);
         const int b0 = j & ~7;
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
           const float4 p = ldg4(tgt.pts, b0 + h);
-          tied = tied || (b0 + h != j && dist2(qs.x, qs.y, qs.z, p.x, p.y, p.z) == kd);
+          tied = tied || (b0 + h != j && dist2(qx, qy, qz, p.x, p.y, p.z) == kd);
         }
       }
     }

@@ -324,6 +324,7 @@ struct gicp_ctx {
   // stage timing of compute_cov (profiling on): covariance kernel, tree build, resolvers
   hipEvent_t st_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool st_tree = false;          // the last compute_cov built a tree (events 2, 3 recorded)
+  bool st_resolve = false;       // ... and ran the tie resolvers (events 4, 5)
 };
 
 namespace ddlo {
@@ -681,6 +682,8 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   // exact ties: the points whose k-th neighbour distance is tied get their
   // neighbourhood from nanoflann's own search (nftree.hip)
   TieList tl{nullptr, nullptr};
+  // (building the tree only after a covariance pass that met ties measured
+  // slower on cfg 5: every voxel-filtered scan has ~270 tied queries at k = 10)
   if (c->tie_exact) {
     gicp_status st = ensure_nftree(c, *side.cloud, c->stream);
     if (!st) st = tie_scratch(c, side.cloud->n, c->stream, &tl);
@@ -751,6 +754,7 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     return fail(GICP_EINVAL, "unsupported k");
   }
   if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[1], c->stream));
+  c->st_resolve = c->tie_exact;
   if (c->tie_exact) {
     HIP_TRY(nftree_join(*side.cloud->nf, c->stream));
     if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[4], c->stream));

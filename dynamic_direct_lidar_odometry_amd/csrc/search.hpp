@@ -519,6 +519,29 @@ __device__ __forceinline__ unsigned long long xor_min64(unsigned long long v) {
   return umin64(((unsigned long long)a1 << 32) | a0, ((unsigned long long)b1 << 32) | b0);
 }
 
+// the mirrored key of tie_scan 3: same distance, complemented position
+__device__ __forceinline__ unsigned long long mirror_key(unsigned long long k) { return k ^ 0xffffffffull; }
+
+// xor_min64 that also records in td the distance of two lanes' keys that are
+// equal in distance (two distinct points: a tie at that distance)
+template <int M>
+__device__ __forceinline__ unsigned long long xor_min64_eq(unsigned long long v, unsigned& td) {
+  static_assert(M == 16 || M == 32, "xor_min64_eq: M = 16 or 32");
+  const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+  unsigned a0, a1, b0, b1;
+  if constexpr (M == 32) {
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a0 = rl[0]; b0 = rl[1]; a1 = rh[0]; b1 = rh[1];
+  } else {
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a0 = rl[0]; b0 = rl[1]; a1 = rh[0]; b1 = rh[1];
+  }
+  td = a1 == b1 ? min(td, a1) : td;   // the lanes hold disjoint points: equal distances are two points
+  return umin64(((unsigned long long)a1 << 32) | a0, ((unsigned long long)b1 << 32) | b0);
+}
+
 // xor_min64 carrying the winning key's point coordinates along (lanes l and
 // l ^ M; equal keys name the same point)
 template <int M>
