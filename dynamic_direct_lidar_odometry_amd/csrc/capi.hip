@@ -100,7 +100,7 @@ int env_int(const char* name, int dflt) {
 // process, not on every align (host time between aligns).
 struct SearchKnobs {
   float split_extent, hard_extent, probe, probe_d, tri_mv, reuse_gap, reuse_gap0, reuse_rec_eps, reuse_rec_conv;
-  int list_flush, xcd_scan, pf_ratio, hard_blocks, prev_window, reuse, reuse_rec0, tie_scan;
+  int list_flush, xcd_scan, pf_ratio, hard_blocks, prev_window, reuse, reuse_rec0, tie_scan, tie_ab;
 };
 const SearchKnobs& search_knobs() {
   static const SearchKnobs k = [] {
@@ -121,6 +121,7 @@ const SearchKnobs& search_knobs() {
     v.reuse_rec0 = env_int("DDLO_REUSE_REC0", 0);
     v.reuse_rec_eps = env_float("DDLO_REUSE_REC_EPS", 0.05f);
     v.reuse_rec_conv = env_float("DDLO_REUSE_REC_CONV", 10.f);
+    v.tie_ab = env_int("DDLO_TIE_AB", 0);
     v.tie_scan = env_int("DDLO_TIE_SCAN", 3);   // 1 / 2 / 3 (see AlignJob::tie_scan); 0 = A/B only
     return v;
   }();
@@ -231,6 +232,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.tgt_nf_status = nullptr;
   j.tie_map = nullptr;
   j.tie_scan = j.tie_detect ? kn.tie_scan : 0;
+  j.tie_ab = kn.tie_ab;
   if (j.tie_detect) {
     const CloudData* tc = c->tie_ref ? c->tie_ref.get() : c->tgt.cloud.get();
     if (tc->nf) {

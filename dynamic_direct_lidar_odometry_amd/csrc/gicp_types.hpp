@@ -205,6 +205,8 @@ struct AlignJob {
   // key's distance) and re-runs it through the target's nanoflann tree
   // (tgt_nf.nodes != nullptr), else sets AlignState::tie_pending.
   int tie_detect;
+  int tie_ab;                    // A/B only (DDLO_TIE_AB bits, inexact): 1 no mirrored-key atomic, 2 no slice-merge
+                                 // records, 4 no winner-slice check
   int tie_scan;                  // the scan's tie test: 1 second distance over every examined point, 2 the 8-point
                                  // slices' losing bests + k_moments' check of the winner's slice, 3 equal-distance
                                  // flags at the merges + the mirrored key + the winner's slice check, 0 none (A/B)

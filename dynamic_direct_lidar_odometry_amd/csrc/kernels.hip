@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       if (inrange && lane < Q) {
         keyout[i] = passed ? pass_key : dkey(INFINITY, -1);
         qstate[i] = make_float4(qx, qy, qz, -1.f);
-        if (job->tie_detect) job->sec[i] = __float_as_uint(INFINITY);   // proven strict: no tie
+        if (job->tie_detect) job->sec[i] = 0xffffffffu;   // not searched (proven strict or not owned): no tie test
         if (job->tie_scan == 3) job->key2[i] = mirror_key(passed ? pass_key : dkey(INFINITY, -1));
       }
       if (lane == 0) {
@@ -1286,7 +1286,8 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       }
       // the examined points' second distance: the reuse bound (rec) and the
       // tie test of k_moments (sec == the key's distance); k_nn_scan lowers it
-      if ((rec || job->tie_detect) && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);
+      if ((rec || job->tie_detect) && inrange && lane < Q)
+        job->sec[i] = active ? __float_as_uint(col.sec) : 0xffffffffu;   // all ones: not searched, no tie test
       if (stats) {
         const unsigned npass = (unsigned)__popcll(__ballot(passed && lane < Q));
         if (lane == 0) {
@@ -1401,7 +1402,8 @@ __global__ __launch_bounds__(256, MINW) void k_nn_collect(const AlignJob* __rest
     keyout[i] = col.bk;   // lowered by inline scans
     if (job->tie_scan == 3) job->key2[i] = mirror_key(col.bk);
   }
-  if ((st->rec || job->tie_detect) && inrange && lane < Q) job->sec[i] = __float_as_uint(col.sec);   // k_nn_scan lowers it further
+  if ((st->rec || job->tie_detect) && inrange && lane < Q)   // k_nn_scan lowers it further; all ones: not searched
+    job->sec[i] = col.active ? __float_as_uint(col.sec) : 0xffffffffu;
   if (lane == 0) job->grp_blocks[g] = (unsigned short)min(col.st_blocks, 65535u);
   if (stats && lane == 0) {
     const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
@@ -1484,8 +1486,10 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   // flags at its merges (slices, tasks of a run) and the mirrored key pushed
   // beside the key (runs): no atomic return is waited for
   const bool tie3 = !rec && job->tie_scan == 3;
+  const bool tie_xor = !(job->tie_ab & 2);
   unsigned long long* const key2 = job->key2;
-  unsigned td = 0xffffffffu;   // smallest distance (bits) met twice at a merge of this run's keys (any slice lane)
+  unsigned td = 0xffffffffu;   // smallest distance (bits) met twice at a slice merge of this run (any slice lane)
+  unsigned long long accm = ~0ull;   // the run's minimum of mirrored keys (its tasks' bests, highest position first)
   int run_sg = -1;
   unsigned long long acc = ~0ull;   // lane's query minimum over the current run
   float acc2 = INFINITY;            // smallest distance of the run's other points (reuse)
@@ -1527,7 +1531,7 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
         pend_bound = run_bound;
       } else {
         atomicMin(key + qidx, acc);
-        if (tie3) atomicMin(key2 + qidx, mirror_key(acc));
+        if (tie3 && !(job->tie_ab & 1)) atomicMin(key2 + qidx, accm);   // with key: two of the run's tasks at the distance = a tie
       }
     }
     if (tie3 && run_sg >= 0) {   // the run's tie distances of the query's four slice lanes -> its lane qi
@@ -1578,6 +1582,7 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
           acc2 = INFINITY;
           run_bound = -1.f;
           td = 0xffffffffu;
+          accm = ~0ull;
         }
         const unsigned char* T = cur + k * kScanTaskBytes;
         const f4v x0 = *(const f4v*)(T + s * 32), x1 = *(const f4v*)(T + s * 32 + 16);
@@ -1633,14 +1638,17 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
           unsigned long long bk = dkey(bd, pos0 + bh);
           if (tie3) {   // equal distances meeting at a merge: a tie (two points of one slice: k_moments' check)
             unsigned tt = 0xffffffffu;
-            bk = xor_min64_eq<16>(bk, tt);
-            bk = xor_min64_eq<32>(bk, tt);
+            if (tie_xor) {
+              bk = xor_min64_eq<16>(bk, tt);
+              bk = xor_min64_eq<32>(bk, tt);
+            } else {
+              bk = xor_min64<16>(bk);
+              bk = xor_min64<32>(bk);
+            }
             if (on) {
-              // a leaf met again in the same run (two walk entries) is the same key, not a tie
-              const unsigned hb = (unsigned)(bk >> 32);
-              if (hb == (unsigned)(acc >> 32) && bk != acc) tt = min(tt, hb);
               td = min(td, tt);
               acc = umin64(acc, bk);
+              accm = umin64(accm, mirror_key(bk));   // (a leaf met twice in a run is one key: no false tie)
             }
           } else {
             bk = xor_min64<16>(bk);
@@ -1951,7 +1959,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
   const int rec = st->rec;   // this iteration records reuse references
   const int first_rec_done = st->any_rec;   // an earlier iteration of this align recorded
   const int tie_detect = job->tie_detect;
-  const bool slice_check = tie_detect && job->tie_scan >= 2;
+  const bool slice_check = tie_detect && job->tie_scan >= 2 && !(job->tie_ab & 4);
   const bool tie3m = tie_detect && job->tie_scan == 3 && !rec;   // the mirrored key of a non-recording search
   __shared__ NfWaveStack tie_stk[kMomWaves];   // nanoflann search frames of a tied query (per wave)
   double R[9], t[3];
@@ -1975,25 +1983,37 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     unsigned kj = 0xffffffffu;
     float kd = INFINITY;
     bool tied = false;
+    // the moment operands (a, b, their covariances) are loaded before the tie
+    // checks, so those loads overlap them; a re-run query reloads its b
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    double ca[6] = {0, 0, 0, 0, 0, 0}, cb[6] = {0, 0, 0, 0, 0, 0};
     if (active) {
       const unsigned long long k = key[i];
+      // independent of the key: issued with it
+      const unsigned sv = tie_detect ? job->sec[i] : 0xffffffffu;
+      const unsigned k2lo = tie3m ? (unsigned)job->key2[i] : 0u;
       kj = (unsigned)k;
       kd = __uint_as_float((unsigned)(k >> 32));
       j = (kj != 0xffffffffu && (double)kd < max_corr2) ? (int)kj : -1;
-      // another examined point at the nearest distance: an exact tie (tie_scan
-      // 3: sec 0 = flagged, or the mirrored key names another point)
-      if (tie_detect && j >= 0) {
-        const unsigned sv = job->sec[i];
-        tied = sv <= (unsigned)(k >> 32);
-        if (tie3m) tied = tied || (unsigned)job->key2[i] != ((unsigned)k ^ 0xffffffffu);
+      if (j >= 0) {
+        a = ldg4(src.pts, i);
+        b = ldg4(tgt.pts, j);
+        load_sym6(src_cov + 6 * (size_t)i, ca);
+        load_sym6(tgt_cov + 6 * (size_t)j, cb);
       }
-      // tie_scan 2: the scan compares only the 8-point slices' bests, so a
+      // another examined point at the nearest distance: an exact tie.  sec:
+      // all ones = not searched (a reuse reference proved the match), else
+      // the smallest distance met twice / of a non-best point (never below
+      // the key's); tie_scan 3 also: the mirrored key names another point
+      const bool searched = tie_detect && j >= 0 && sv != 0xffffffffu;
+      tied = searched && sv <= (unsigned)(k >> 32);
+      if (tie3m && searched) tied = tied || k2lo != ((unsigned)k ^ 0xffffffffu);
+      // tie_scan >= 2: the scan compares only the 8-point slices' bests, so a
       // second point at the distance inside the winner's own slice (the 8
       // aligned sorted positions one lane scanned; the same 128-B line as the
       // winner) is checked here, in the scan's fp32 arithmetic
-      if (slice_check && j >= 0 && !tied) {
+      if (slice_check && searched && !tied) {
         // the search's fp32 query, recomputed (k_nn_seed's transform, same operations)
-        const float4 a = ldg4(src.pts, i);
         const float qx = ((float)R[0] * a.x + (float)R[1] * a.y) + ((float)R[2] * a.z + (float)t[0]);
         const float qy = ((float)R[3] * a.x + (float)R[4] * a.y) + ((float)R[5] * a.z + (float)t[1]);
         const float qz = ((float)R[6] * a.x + (float)R[7] * a.y) + ((float)R[8] * a.z + (float)t[2]);
@@ -2007,8 +2027,13 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     }
     // nanoflann's choice among the tied points (wave-uniform, rare)
     if (tie_detect && __any(tied)) {
+      const int j0 = j;
       resolve_tied_corr(job, st, tgt, tied, i, kd, j, &tie_stk[wib]);
       if (tied) kj = (unsigned)j;
+      if (j != j0) {   // another point of the same distance: its coordinates and covariance
+        b = ldg4(tgt.pts, j);
+        load_sym6(tgt_cov + 6 * (size_t)j, cb);
+      }
     }
     if (active) {
       corr[i] = j;
@@ -2037,11 +2062,6 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     }
     Contrib C;
     if (j >= 0) {
-      const float4 a = ldg4(src.pts, i);
-      const float4 b = ldg4(tgt.pts, j);
-      double ca[6], cb[6];
-      load_sym6(src_cov + 6 * (size_t)i, ca);
-      load_sym6(tgt_cov + 6 * (size_t)j, cb);
       const double A[9] = {ca[0], ca[1], ca[2], ca[1], ca[3], ca[4], ca[2], ca[4], ca[5]};
       // RC = R * CA ; S = RC * R^T ; RCR = CB + S
       double RC[9];

@@ -316,12 +316,96 @@ __global__ __launch_bounds__(1024) void k_nf_map(const NfBuild* __restrict__ bp,
   }
 }
 
+// Level L's map, fused into its count kernel (one launch less per level):
+// every block scans the children its parent level produced (pend[L], a few
+// dozen entries) for the big task holding its chunk and writes that chunk's
+// task copy; block 0 also writes the task list, the small tasks and the
+// counters, and the blocks clear the next level's children entries.  The
+// same lists as k_nf_map (which still runs the final, all-small call).
+__device__ __forceinline__ bool map_level_block(const NfBuild& b, int L, TaskView* v, int* sh) {
+  __shared__ int s_big, s_small, s_ch, s_small0, s_t, s_found;
+  __shared__ NfTask s_task;
+  NfCtl* ctl = b.ctl;
+  const int np = L == 0 ? 1 : 2 * ctl->ntask[L - 1];
+  const NfTask* P = b.pend + (size_t)L * b.max_pend;
+  NfTask* T = b.tasks + (size_t)L * b.max_task;
+  const int blk = blockIdx.x;
+  const bool lead = blk == 0;
+  if (threadIdx.x == 0) {
+    s_big = s_small = s_ch = 0;
+    s_small0 = lead ? ctl->nsmall : 0;
+    s_found = 0;
+  }
+  __syncthreads();
+  for (int base = 0; base < np; base += blockDim.x) {
+    const int i = base + threadIdx.x;
+    NfTask e;
+    bool valid = false;
+    if (i < np) {
+      e = P[i];
+      valid = e.count > 0 && e.node > 0 && e.node < b.cap;
+      if (L == 0 && i == 0) valid = e.count > 0;
+    }
+    const bool big = valid && e.count > kNfT;
+    const bool sml = valid && !big;
+    const int nch = big ? (e.count + kNfCH - 1) / kNfCH : 0;
+    int tb, ts, tc;
+    const int xb = block_excl_scan(big ? 1 : 0, &tb, sh);
+    const int xs = block_excl_scan(sml ? 1 : 0, &ts, sh);
+    const int xc = block_excl_scan(nch, &tc, sh);
+    const int t = s_big + xb, c0 = s_ch + xc;
+    if (big && t < b.max_task) {
+      e.chunk0 = c0;
+      e.nch = nch;
+      if (lead) T[t] = e;
+      if (blk >= c0 && blk < c0 + nch) {   // this block's chunk
+        e.pad = t;
+        s_task = e;
+        s_t = t;
+        s_found = 1;
+      }
+    }
+    if (lead && sml && s_small0 + s_small + xs < b.max_small) b.small[s_small0 + s_small + xs] = e;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_big += tb;
+      s_small += ts;
+      s_ch += tc;
+    }
+    __syncthreads();
+  }
+  const int nbig = min(s_big, b.max_task);
+  const int nchunks = min(s_ch, b.max_chunks);
+  if (lead && threadIdx.x == 0) {
+    if (s_big > b.max_task || s_small0 + s_small > b.max_small || s_ch > b.max_chunks) atomicOr(&ctl->err, 8);
+    ctl->ntask[L] = nbig;
+    ctl->nsmall = min(s_small0 + s_small, b.max_small);
+    ctl->nchunks[L & 1] = nchunks;
+  }
+  // the children this level will produce: their min / max start empty
+  NfTask* C = b.pend + (size_t)(L + 1) * b.max_pend;
+  for (int i = blk * (int)blockDim.x + (int)threadIdx.x; i < 2 * nbig; i += (int)(gridDim.x * blockDim.x)) {
+    C[i].count = 0;
+    for (int a = 0; a < 3; ++a) {
+      C[i].mm[a] = 0xffffffffu;
+      C[i].mm[3 + a] = 0u;
+    }
+  }
+  if (!s_found || blk >= nchunks) return false;
+  if (threadIdx.x == 0) b.ctask[(L & 1) * b.max_chunks + blk] = s_task;   // the pass kernels' one-load copy
+  v->tk = s_task;
+  v->blk = blk;
+  v->t = s_t;
+  v->c = blk - s_task.chunk0;
+  return true;
+}
+
 // middleSplit_'s cut per task; #{v < cut} and #{v <= cut} per chunk
 __global__ __launch_bounds__(kNfBT) void k_nf_count(const NfBuild* __restrict__ bp, int L) {
   const NfBuild& b = *bp;
   __shared__ int sh[17];
   TaskView v;
-  if (!task_of_block(b, L, &v)) return;
+  if (!map_level_block(b, L, &v, sh)) return;
   int feat;
   float cut;
   nf_cut(v.tk, &feat, &cut);
@@ -337,10 +421,7 @@ __global__ __launch_bounds__(kNfBT) void k_nf_count(const NfBuild* __restrict__ 
   if (threadIdx.x == 0) {
     b.cA[v.blk] = a;
     b.cAE[v.blk] = ae;
-    if (v.c == 0) {
-      NfTask* T = b.tasks + (size_t)L * b.max_task;
-      T[v.t].feat = feat;
-      T[v.t].cut = cut;
+    if (v.c == 0) {   // (the task list's feat / cut stay unset: every pass kernel recomputes the cut)
       const float mn[3] = {o2f(v.tk.mm[0]), o2f(v.tk.mm[1]), o2f(v.tk.mm[2])};
       const float mx[3] = {o2f(v.tk.mm[3]), o2f(v.tk.mm[4]), o2f(v.tk.mm[5])};
       nf_set_div(b.nodes, v.tk.node, mn, mx);   // the children's min / max are final now
@@ -1182,8 +1263,7 @@ void launch_nf_build(hipStream_t s, const NfBuild& hb, const NfBuild* db, int st
   const int G = std::max(1, hb.max_chunks);
   for (int L = 0; L < hb.Lmax; ++L) {
     if (stop >= 0 && L >= stop) return;
-    k_nf_map<<<1, 1024, 0, s>>>(db, L);
-    k_nf_count<<<G, kNfBT, 0, s>>>(db, L);
+    k_nf_count<<<G, kNfBT, 0, s>>>(db, L);   // the level's map + its counts
     k_nf_pass<1, true><<<G, kNfBT, 0, s>>>(db, L);
     k_nf_pass<1, false><<<G, kNfBT, 0, s>>>(db, L);
     k_nf_pass<2, true><<<G, kNfBT, 0, s>>>(db, L);
