@@ -376,8 +376,11 @@ struct KnnVisitor : VisitStats {
     for (int j = 0; j < kLeafSize; ++j) {
       const float d = dist2(qx, qy, qz, L->px[j], L->py[j], L->pz[j]);
       const unsigned long long key = dkey(d, start + j);
-      if (active && key < wk && d <= tight) insert(key);   // d > tight: not among the k nearest
-      else td = fminf(td, d);
+      // d > tight: not among the k nearest.  Only an active lane's examined
+      // points count for td: an inactive lane (another sub-range of a split
+      // group) re-scans leaves whose points it may already keep.
+      if (active && key < wk && d <= tight) insert(key);
+      else if (active) td = fminf(td, d);
     }
   }
   __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
@@ -528,7 +531,7 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
       const float d = dist2(this->qx, this->qy, this->qz, L->px[h0 + j], L->py[h0 + j], L->pz[h0 + j]);
       const unsigned long long key = dkey(d, start + h0 + j);
       if (this->active && key < wk_both() && d <= this->tight) this->insert(key);
-      else this->td = fminf(this->td, d);
+      else if (this->active) this->td = fminf(this->td, d);   // active lanes only (see KnnVisitor::process)
     }
     exchange();
   }

@@ -769,6 +769,20 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
       HIP_TRY(hipMemcpyAsync(&cnt, tl.count, sizeof(int), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
       std::fprintf(stderr, "[ties] n %d k %d tied %d\n", side.cloud->n, k, cnt);
+      if (const char* path = std::getenv("DDLO_TIE_DUMP")) {   // the tied queries' original indices, one line per cloud
+        const int m = std::min(cnt, tl.cap);
+        std::vector<int> pos(m), perm(side.cloud->n);
+        HIP_TRY(hipMemcpyAsync(pos.data(), tl.list, sizeof(int) * m, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(perm.data(), side.cloud->perm.p, sizeof(int) * perm.size(), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (FILE* f = std::fopen(path, "a")) {
+          std::fprintf(f, "%d %d", side.cloud->n, k);
+          for (int p : pos) std::fprintf(f, " %d", p < side.cloud->n ? perm[p] : -1);
+          std::fprintf(f, "\n");
+          std::fclose(f);
+        }
+      }
     }
   }
   HIP_TRY(hipGetLastError());

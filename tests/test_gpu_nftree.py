@@ -47,12 +47,17 @@ def test_device_tree_raycast_scan():
     assert O.same_tree(c.nftree(SOURCE), O.tree(src)) is None
 
 
+@pytest.mark.parametrize("spacing", [0.25, 1.5])
 @pytest.mark.parametrize("k", [10, 20])
-def test_covariance_ties_lattice(k):
-    """An integer lattice: nearly every point's k-th neighbour distance is tied."""
+def test_covariance_ties_lattice(k, spacing):
+    """An integer lattice: nearly every point's k-th neighbour distance is tied.
+    At 1.5 m spacing a 64-point Morton group spans more than the 5 m split
+    extent, so the groups are searched as sub-ranges whose traversals re-scan
+    each other's leaves (a lane's tie record must ignore the leaves scanned
+    while it is inactive)."""
     lat = np.stack(np.meshgrid(np.arange(24), np.arange(24), np.arange(5), indexing="ij"), -1).reshape(-1, 3)
-    pts = (lat.astype(np.float32) * np.float32(0.25))
-    pts = pts + (np.arange(len(pts)) % 7 == 0)[:, None].astype(np.float32) * np.float32(0.01)   # some irregularity
+    pts = (lat.astype(np.float32) * np.float32(spacing))
+    pts = pts + (np.arange(len(pts)) % 7 == 0)[:, None].astype(np.float32) * np.float32(0.04 * spacing)   # some irregularity
     c = P.Context(0)
     c.set_params(P.default_params(k_correspondences=k))
     c.set_target(pts)
@@ -74,6 +79,21 @@ def test_knn_ties_random_duplicates():
     c = P.Context(0)
     c.set_target(pts)
     for k in (1, 5, 10, 20, 33):
+        idx, sqd = c.knn_target(q, k)
+        ri, rd = O.knn(pts, q, k)
+        np.testing.assert_array_equal(sqd, rd)
+        np.testing.assert_array_equal(idx, ri)
+
+
+def test_knn_ties_split_groups():
+    """A 1.5 m lattice queried at its points and cell centres in lattice order:
+    split sub-groups (5 m extent) with exact ties at the k-th distance."""
+    lat = np.stack(np.meshgrid(np.arange(20), np.arange(20), np.arange(6), indexing="ij"), -1).reshape(-1, 3)
+    pts = lat.astype(np.float32) * np.float32(1.5)
+    q = np.concatenate([pts, pts[::3] + np.float32(0.75)])
+    c = P.Context(0)
+    c.set_target(pts)
+    for k in (1, 6, 10, 20):
         idx, sqd = c.knn_target(q, k)
         ri, rd = O.knn(pts, q, k)
         np.testing.assert_array_equal(sqd, rd)
