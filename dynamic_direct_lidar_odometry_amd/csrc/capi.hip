@@ -617,6 +617,8 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   {
     const char* v = std::getenv("DDLO_TIE_EXACT");   // A/B of the tie resolution (default: nanoflann's order)
     c->tie_exact = !(v && *v == '0');
+    const char* lz = std::getenv("DDLO_TIE_LAZY");   // 1: covariance ties through per-query lazy searches (A/B)
+    c->tie_lazy = lz && *lz == '1';
   }
   *out = c.release();
   return GICP_OK;
@@ -640,6 +642,7 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   if (c->state_host) (void)hipHostFree(c->state_host);
   if (c->flag_host) (void)hipHostFree(c->flag_host);
   if (c->nf_err_host) (void)hipHostFree(c->nf_err_host);
+  if (c->tie_cnt_ev) (void)hipEventDestroy(c->tie_cnt_ev);
   c->src = Side();
   c->tgt = Side();
   (void)hipStreamDestroy(c->stream);

@@ -1111,6 +1111,36 @@ __global__ __launch_bounds__(64) void k_nf_small_global(const NfBuild* __restric
 // wavefront per query (nf_search_wave)
 constexpr int kNfResolveWaves = 4;
 
+// Lane j < k holds the j-th neighbour (original index rix): the mean and
+// biased covariance in neighbour order (nano_gicp_impl.hpp:392-399),
+// regularised, written by lane 0.  Whole wavefront.
+__device__ __forceinline__ void nf_cov_wave(const CloudDev& c, int rix, int k, int method, double* o) {
+  const int lane = __lane_id();
+  float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lane < k) p = c.pts[c.inv_perm[rix]];
+  double mx = 0, my = 0, mz = 0;
+  for (int j = 0; j < k; ++j) {
+    mx += (double)__shfl(p.x, j);
+    my += (double)__shfl(p.y, j);
+    mz += (double)__shfl(p.z, j);
+  }
+  mx /= k;
+  my /= k;
+  mz /= k;
+  double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < k; ++j) {
+    const double d0 = (double)__shfl(p.x, j) - mx, d1 = (double)__shfl(p.y, j) - my, d2 = (double)__shfl(p.z, j) - mz;
+    C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
+    C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
+    C[6] += d2 * d0; C[7] += d2 * d1; C[8] += d2 * d2;
+  }
+  for (int e = 0; e < 9; ++e) C[e] /= k;
+  double out[6];
+  regularize(C, method, out);
+  if (lane == 0)
+    for (int e = 0; e < 6; ++e) o[e] = out[e];
+}
+
 __global__ __launch_bounds__(64 * kNfResolveWaves) void k_nf_resolve_cov(NfTreeDev t, CloudDev c, TieList ties, int k,
                                                                         int method, double* __restrict__ cov6,
                                                                         const int* __restrict__ status,
@@ -1137,33 +1167,7 @@ __global__ __launch_bounds__(64 * kNfResolveWaves) void k_nf_resolve_cov(NfTreeD
       if (lane == 0) atomicOr(err, rix == -2 ? 1 : 4);
       continue;
     }
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane < k) p = c.pts[c.inv_perm[rix]];
-    // mean and biased covariance in neighbour order (nano_gicp_impl.hpp:392-399)
-    double mx = 0, my = 0, mz = 0;
-    for (int j = 0; j < k; ++j) {
-      mx += (double)__shfl(p.x, j);
-      my += (double)__shfl(p.y, j);
-      mz += (double)__shfl(p.z, j);
-    }
-    mx /= k;
-    my /= k;
-    mz /= k;
-    double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int j = 0; j < k; ++j) {
-      const double d0 = (double)__shfl(p.x, j) - mx, d1 = (double)__shfl(p.y, j) - my,
-                   d2 = (double)__shfl(p.z, j) - mz;
-      C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
-      C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
-      C[6] += d2 * d0; C[7] += d2 * d1; C[8] += d2 * d2;
-    }
-    for (int e = 0; e < 9; ++e) C[e] /= k;
-    double out[6];
-    regularize(C, method, out);
-    if (lane == 0) {
-      double* o = cov6 + 6 * (size_t)s;
-      for (int e = 0; e < 6; ++e) o[e] = out[e];
-    }
+    nf_cov_wave(c, rix, k, method, cov6 + 6 * (size_t)s);
   }
 }
 
@@ -1200,6 +1204,454 @@ __global__ __launch_bounds__(64 * kNfResolveWaves) void k_nf_resolve_knn(NfTreeD
       out_d[(size_t)i * k + lane] = rd;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Lazy tie resolution: nanoflann's search of one tied query with the tree
+// built only where that search walks.  divideTree (:987-1043) works in place
+// on vind, depth first, and a node's split reads and permutes only its own
+// range, so a node's split depends only on its ancestors' splits: a search
+// that splits each node the first time it enters it, on a private copy of
+// vind, meets exactly the nodes, cuts, divlow / divhigh and leaf orders of
+// the full tree.  One workgroup per tied query; every split is middleSplit_
+// + planeSplit as rank pairings (as the full build), whole-workgroup passes
+// over the node's range in global memory (L2).  A scan has ~1 tied query,
+// so this replaces the whole-cloud build (~0.5-0.8 ms) by one path.
+constexpr int kLzT = 512;            // threads per workgroup (256 VGPRs: the epilogue's fp64 regularisation spilled at 128)
+constexpr int kLzW = kLzT / 64;
+constexpr int kLzStack = 96;         // search frames (depth of the tree + 1)
+
+struct LzFrame {
+  int begin, count, state, feat;
+  float lx, ly, lz, hx, hy, hz;      // the box divideTree passes down (named fields: a runtime-indexed
+                                     // array member would put the frame copies in private memory)
+  float fm, fd, divlow, divhigh;     // mindistsq, the saved dists[feat], the split's divs
+  int index;                         // split position (relative to begin)
+  float cut;
+  int pad[2];
+};
+// left_bbox (.hi[feat] = cut) / right_bbox (.lo[feat] = cut) of divideTree (:1024-1030)
+// (value selects: a store through a feat-dependent field pointer keeps the frame in private memory)
+__device__ __forceinline__ void lz_set_hi(LzFrame& f, int feat, float v) {
+  f.hx = feat == 0 ? v : f.hx;
+  f.hy = feat == 1 ? v : f.hy;
+  f.hz = feat == 2 ? v : f.hz;
+}
+__device__ __forceinline__ void lz_set_lo(LzFrame& f, int feat, float v) {
+  f.lx = feat == 0 ? v : f.lx;
+  f.ly = feat == 1 ? v : f.ly;
+  f.lz = feat == 2 ? v : f.lz;
+}
+
+struct LzMem {                       // one workgroup's scratch: vind order as SoA + pairing tables
+  float *x, *y, *z;
+  int* id;
+  int *ml, *mr, *cz, *cr;
+};
+
+static __host__ __device__ inline size_t lz_al(size_t b) { return (b + 255) / 256 * 256; }
+static __host__ __device__ inline size_t lz_wg_bytes(int n) {
+  return 4 * lz_al(4 * (size_t)n) + 2 * lz_al(4 * ((size_t)n / 2 + 64)) + 2 * lz_al(4 * ((size_t)n / 64 + 4));
+}
+static __host__ __device__ inline size_t lz_shared_bytes(int n) { return 3 * lz_al(4 * (size_t)n); }
+
+__device__ __forceinline__ LzMem lz_mem(char* p, int n) {
+  LzMem m;
+  const size_t a = lz_al(4 * (size_t)n), t = lz_al(4 * ((size_t)n / 2 + 64)), q = lz_al(4 * ((size_t)n / 64 + 4));
+  m.x = reinterpret_cast<float*>(p);
+  m.y = reinterpret_cast<float*>(p + a);
+  m.z = reinterpret_cast<float*>(p + 2 * a);
+  m.id = reinterpret_cast<int*>(p + 3 * a);
+  m.ml = reinterpret_cast<int*>(p + 4 * a);
+  m.mr = reinterpret_cast<int*>(p + 4 * a + t);
+  m.cz = reinterpret_cast<int*>(p + 4 * a + 2 * t);
+  m.cr = reinterpret_cast<int*>(p + 4 * a + 2 * t + q);
+  return m;
+}
+
+struct LzShared {
+  LzFrame F[kLzStack];
+  float rf[kLzW][8];
+  int ri[kLzW][4];
+  int sh[17];
+  int sp, fail;
+  float worst;
+};
+
+__device__ __forceinline__ float* lz_axis(const LzMem& m, int f) { return f == 0 ? m.x : (f == 1 ? m.y : m.z); }
+
+// min (v[0..2]) and max (v[3..5]) over the workgroup; every thread gets the result
+__device__ __forceinline__ void lz_reduce6(float v[6], LzShared& S) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) v[a] = wred(v[a], a >= 3);
+  if (__lane_id() == 0)
+#pragma unroll
+    for (int a = 0; a < 6; ++a) S.rf[w][a] = v[a];
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    float r = S.rf[0][a];
+    for (int i = 1; i < kLzW; ++i) r = a >= 3 ? fmaxf(r, S.rf[i][a]) : fminf(r, S.rf[i][a]);
+    v[a] = r;
+  }
+  __syncthreads();
+}
+
+// exclusive prefix of a[0, cnt) in place (global memory), returns the total
+__device__ __forceinline__ int lz_scan(int* a, int cnt, LzShared& S) {
+  const int per = (cnt + kLzT - 1) / kLzT;
+  const int b0 = min((int)threadIdx.x * per, cnt), b1 = min(b0 + per, cnt);
+  int s = 0;
+  for (int i = b0; i < b1; ++i) s += a[i];
+  int tot;
+  int off = block_excl_scan(s, &tot, S.sh);
+  for (int i = b0; i < b1; ++i) {
+    const int t = a[i];
+    a[i] = off;
+    off += t;
+  }
+  return tot;
+}
+
+// One Hoare pass of the node at base b (count n) as a rank pairing: the r-th
+// bad element of the zone [zlo, zhi) (ascending) swaps with the r-th good
+// element of [zhi, n) (descending); good = v < cut (pass 1) or v == cut
+// (pass 2).  False on an (impossible) count mismatch.
+__device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi, int n, int feat, float cut, bool pass2, LzShared& S) {
+  const int lane = __lane_id(), w = threadIdx.x >> 6;
+  const float* V = lz_axis(m, feat) + b;
+  const int nz = (zhi - zlo + 63) / 64, nr = (n - zhi + 63) / 64;
+  for (int z = w; z < nz; z += kLzW) {
+    const int i = zlo + 64 * z + lane;
+    bool f = false;
+    if (i < zhi) {
+      const float x = V[i];
+      f = !(pass2 ? x == cut : x < cut);
+    }
+    const int c = __popcll(__ballot(f));
+    if (lane == 0) m.cz[z] = c;
+  }
+  for (int r = w; r < nr; r += kLzW) {
+    const int i = n - 1 - 64 * r - lane;
+    bool f = false;
+    if (i >= zhi) {
+      const float x = V[i];
+      f = pass2 ? x == cut : x < cut;
+    }
+    const int c = __popcll(__ballot(f));
+    if (lane == 0) m.cr[r] = c;
+  }
+  __syncthreads();
+  const int mz = lz_scan(m.cz, nz, S);
+  const int mr = lz_scan(m.cr, nr, S);
+  __syncthreads();
+  if (mz != mr) return false;
+  if (mz == 0) return true;
+  for (int z = w; z < nz; z += kLzW) {
+    const int i = zlo + 64 * z + lane;
+    bool f = false;
+    if (i < zhi) {
+      const float x = V[i];
+      f = !(pass2 ? x == cut : x < cut);
+    }
+    const unsigned long long mask = __ballot(f);
+    const int slot = m.cz[z] + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+    if (f) m.ml[slot] = i;
+  }
+  for (int r = w; r < nr; r += kLzW) {
+    const int i = n - 1 - 64 * r - lane;   // lane order = descending positions
+    bool f = false;
+    if (i >= zhi) {
+      const float x = V[i];
+      f = pass2 ? x == cut : x < cut;
+    }
+    const unsigned long long mask = __ballot(f);
+    const int slot = m.cr[r] + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+    if (f) m.mr[slot] = i;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < mz; r += kLzT) {
+    const int a = b + m.ml[r], c = b + m.mr[r];
+    const float ax = m.x[a], ay = m.y[a], az = m.z[a];
+    const int ai = m.id[a];
+    m.x[a] = m.x[c]; m.y[a] = m.y[c]; m.z[a] = m.z[c]; m.id[a] = m.id[c];
+    m.x[c] = ax; m.y[c] = ay; m.z[c] = az; m.id[c] = ai;
+  }
+  __syncthreads();
+  return true;
+}
+
+// middleSplit_ + planeSplit of the node f (whole workgroup), in place; the
+// split position and the children's faces along the cut dimension (divlow =
+// the left child's max, divhigh = the right child's min, :1032-1033)
+__device__ __forceinline__ bool lz_split(const LzMem& m, const LzFrame& f, int* feat_out, float* cut_out, int* index_out,
+                         float* dlo, float* dhi, LzShared& S) {
+  const int b = f.begin, n = f.count;
+  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int i = threadIdx.x; i < n; i += kLzT) {   // computeMinMax (:965-978)
+    const float x = m.x[b + i], y = m.y[b + i], z = m.z[b + i];
+    v[0] = fminf(v[0], x); v[1] = fminf(v[1], y); v[2] = fminf(v[2], z);
+    v[3] = fmaxf(v[3], x); v[4] = fmaxf(v[4], y); v[5] = fmaxf(v[5], z);
+  }
+  lz_reduce6(v, S);
+  const float mn[3] = {v[0], v[1], v[2]}, mx[3] = {v[3], v[4], v[5]};
+  int feat;
+  float cut;
+  const float lo[3] = {f.lx, f.ly, f.lz}, hi[3] = {f.hx, f.hy, f.hz};
+  nf_cut3(lo, hi, mn, mx, &feat, &cut);
+  // lim1 = #(v < cut), lim2 = #(v <= cut), and the max below / min above the cut
+  const float* V = lz_axis(m, feat) + b;
+  int lt = 0, le = 0;
+  float mlt = -INFINITY, mgt = INFINITY;
+  for (int i = threadIdx.x; i < n; i += kLzT) {
+    const float x = V[i];
+    lt += x < cut;
+    le += x <= cut;
+    if (x < cut) mlt = fmaxf(mlt, x);
+    if (x > cut) mgt = fminf(mgt, x);
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    lt += __shfl_xor(lt, d);
+    le += __shfl_xor(le, d);
+    mlt = fmaxf(mlt, __shfl_xor(mlt, d));
+    mgt = fminf(mgt, __shfl_xor(mgt, d));
+  }
+  const int w = threadIdx.x >> 6;
+  if (__lane_id() == 0) {
+    S.ri[w][0] = lt;
+    S.ri[w][1] = le;
+    S.rf[w][0] = mlt;
+    S.rf[w][1] = mgt;
+  }
+  __syncthreads();
+  int lim1 = 0, lim2 = 0;
+  float max_lt = -INFINITY, min_gt = INFINITY;
+  for (int i = 0; i < kLzW; ++i) {
+    lim1 += S.ri[i][0];
+    lim2 += S.ri[i][1];
+    max_lt = fmaxf(max_lt, S.rf[i][0]);
+    min_gt = fminf(min_gt, S.rf[i][1]);
+  }
+  __syncthreads();
+  bool ok = lz_hoare(m, b, 0, lim1, n, feat, cut, false, S);
+  if (ok && lim2 > lim1) ok = lz_hoare(m, b, lim1, lim2, n, feat, cut, true, S);   // pass 2 (:1128-1142)
+  const int index = nf_index(n, lim1, lim2);
+  *feat_out = feat;
+  *cut_out = cut;
+  *index_out = index;
+  *dlo = index > lim1 ? cut : max_lt;
+  *dhi = index < lim2 ? cut : min_gt;
+  return ok;
+}
+
+// COV: queries are the cloud's own points (sorted positions in the list),
+// the result is their covariance; else rows of q, the result (index, distance).
+template <bool COV>
+__global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __restrict__ X0, const float* __restrict__ Y0,
+                                                  const float* __restrict__ Z0, const float4* __restrict__ q, TieList ties,
+                                                  int k, int method, double* __restrict__ cov6, int* __restrict__ out_idx,
+                                                  float* __restrict__ out_d, char* __restrict__ scr, size_t wg_bytes,
+                                                  int* __restrict__ err) {
+  __shared__ LzShared S;
+  const int n = c.n;
+  const int lane = __lane_id();
+  const int nc = *ties.count;
+  const int nl = min(nc, ties.cap);
+  if (nc > ties.cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 8);
+  const LzMem m = lz_mem(scr + (size_t)blockIdx.x * wg_bytes, n);
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int qi = ties.list[li];
+    const float4 qp = COV ? c.pts[qi] : q[qi];
+    for (int j = threadIdx.x; j < n; j += kLzT) {   // vind = 0 .. n-1 (init_vind)
+      m.x[j] = X0[j];
+      m.y[j] = Y0[j];
+      m.z[j] = Z0[j];
+      m.id[j] = j;
+    }
+    // computeInitialDistances (:1145-1164) against root_bbox
+    const float rlo[3] = {c.quant[0], c.quant[1], c.quant[2]}, rhi[3] = {c.quant[4], c.quant[5], c.quant[6]};
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f, distsq = 0.f;
+    if (qp.x < rlo[0]) { d0 = (qp.x - rlo[0]) * (qp.x - rlo[0]); distsq += d0; }
+    if (qp.x > rhi[0]) { d0 = (qp.x - rhi[0]) * (qp.x - rhi[0]); distsq += d0; }
+    if (qp.y < rlo[1]) { d1 = (qp.y - rlo[1]) * (qp.y - rlo[1]); distsq += d1; }
+    if (qp.y > rhi[1]) { d1 = (qp.y - rhi[1]) * (qp.y - rhi[1]); distsq += d1; }
+    if (qp.z < rlo[2]) { d2 = (qp.z - rlo[2]) * (qp.z - rlo[2]); distsq += d2; }
+    if (qp.z > rhi[2]) { d2 = (qp.z - rhi[2]) * (qp.z - rhi[2]); distsq += d2; }
+    if (threadIdx.x == 0) {
+      LzFrame r;
+      r.begin = 0;
+      r.count = n;
+      r.state = 0;
+      r.feat = 0;
+      r.lx = rlo[0]; r.ly = rlo[1]; r.lz = rlo[2];
+      r.hx = rhi[0]; r.hy = rhi[1]; r.hz = rhi[2];
+      r.fm = distsq;
+      r.fd = 0.f;
+      S.F[0] = r;
+      S.sp = 1;
+      S.fail = 0;
+      S.worst = FLT_MAX;
+    }
+    float kd = FLT_MAX;   // wave 0: lane j's result slot (KNNResultSet)
+    int kx = -1, count = 0;
+    __syncthreads();
+    for (;;) {
+      const int sp = S.sp;
+      if (sp == 0 || S.fail) break;
+      const LzFrame f = S.F[sp - 1];
+      const float worst = S.worst;
+      __syncthreads();   // every thread has the frame before thread 0 rewrites it
+      if (f.count <= kNfLeafMax) {   // leaf: candidates below the worst distance read at the leaf (:1503-1516)
+        if (threadIdx.x < 64) {
+          for (int bb = f.begin; bb < f.begin + f.count; bb += 64) {
+            const int i = bb + lane;
+            float r = FLT_MAX;
+            int ip = -1;
+            bool cand = false;
+            if (i < f.begin + f.count) {
+              r = 0.f;
+              float diff = qp.x - m.x[i];
+              r += diff * diff;
+              diff = qp.y - m.y[i];
+              r += diff * diff;
+              diff = qp.z - m.z[i];
+              r += diff * diff;
+              ip = m.id[i];
+              cand = r < worst;
+            }
+            unsigned long long mk = __ballot(cand);
+            while (mk) {
+              const int bl = __ffsll((long long)mk) - 1;
+              mk &= mk - 1;
+              const float dn = __shfl(r, bl);
+              const int xn = __shfl(ip, bl);
+              const int pos = __popcll(__ballot(lane < count && kd <= dn));
+              const float ud = __shfl_up(kd, 1);
+              const int ux = __shfl_up(kx, 1);
+              if (pos < k && lane < k) {
+                if (lane == pos) {
+                  kd = dn;
+                  kx = xn;
+                } else if (lane > pos) {
+                  kd = ud;
+                  kx = ux;
+                }
+              }
+              if (count < k) ++count;
+            }
+          }
+          const float wk = __shfl(kd, k - 1);
+          if (lane == 0) {
+            S.worst = count < k ? FLT_MAX : wk;
+            S.sp = sp - 1;
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+      if (f.state == 0) {   // first visit: split the node (divideTree's recursion step)
+        int feat, index;
+        float cut, dlo, dhi;
+        const bool ok = lz_split(m, f, &feat, &cut, &index, &dlo, &dhi, S);
+        const float val = feat == 0 ? qp.x : (feat == 1 ? qp.y : qp.z);
+        const bool first1 = ((val - dlo) + (val - dhi)) < 0;   // searchLevel (:1525-1540)
+        if (threadIdx.x == 0) {
+          if (!ok || sp >= kLzStack) {
+            S.fail = ok ? 1 : 16;
+          } else {
+            LzFrame& F = S.F[sp - 1];
+            F.state = 1;
+            F.feat = feat;
+            F.cut = cut;
+            F.index = index;
+            F.divlow = dlo;
+            F.divhigh = dhi;
+            LzFrame ch = f;   // left_bbox / right_bbox (:1024-1030)
+            ch.state = 0;
+            if (first1) {
+              ch.count = index;
+              lz_set_hi(ch, feat, cut);
+            } else {
+              ch.begin = f.begin + index;
+              ch.count = f.count - index;
+              lz_set_lo(ch, feat, cut);
+            }
+            S.F[sp] = ch;
+            S.sp = sp + 1;
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+      const int feat = f.feat;
+      const float val = feat == 0 ? qp.x : (feat == 1 ? qp.y : qp.z);
+      const float diff1 = val - f.divlow, diff2 = val - f.divhigh;
+      const bool first1 = (diff1 + diff2) < 0;
+      if (f.state == 1) {   // the other child, if its box is within the worst distance (:1548-1560)
+        const float cut_dist = first1 ? (val - f.divhigh) * (val - f.divhigh) : (val - f.divlow) * (val - f.divlow);
+        const float dst = feat == 0 ? d0 : (feat == 1 ? d1 : d2);
+        const float mind = f.fm + cut_dist - dst;
+        if (feat == 0) d0 = cut_dist;
+        else if (feat == 1) d1 = cut_dist;
+        else d2 = cut_dist;
+        if (threadIdx.x == 0) {
+          S.F[sp - 1].fd = dst;
+          S.F[sp - 1].state = 2;
+          if (mind * 1.0f <= worst) {
+            if (sp >= kLzStack) {
+              S.fail = 1;
+            } else {
+              LzFrame ch = f;
+              ch.state = 0;
+              ch.fm = mind;
+              if (first1) {   // the right child
+                ch.begin = f.begin + f.index;
+                ch.count = f.count - f.index;
+                lz_set_lo(ch, feat, f.cut);
+              } else {
+                ch.count = f.index;
+                lz_set_hi(ch, feat, f.cut);
+              }
+              S.F[sp] = ch;
+              S.sp = sp + 1;
+            }
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+      if (feat == 0) d0 = f.fd;   // state 2: dists[idx] = dst, return
+      else if (feat == 1) d1 = f.fd;
+      else d2 = f.fd;
+      if (threadIdx.x == 0) S.sp = sp - 1;
+      __syncthreads();
+    }
+    const int fail = S.fail;
+    if (threadIdx.x < 64) {
+      if (fail || count < k) {
+        if (lane == 0) atomicOr(err, fail ? fail : 4);
+      } else if (COV) {
+        nf_cov_wave(c, kx, k, method, cov6 + 6 * (size_t)qi);
+      } else if (lane < k) {
+        out_idx[(size_t)qi * k + lane] = kx;
+        out_d[(size_t)qi * k + lane] = kd;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// the cloud's points in original order (nanoflann's dataset order), SoA
+__global__ __launch_bounds__(256) void k_lz_unsort(CloudDev c, float* __restrict__ X, float* __restrict__ Y,
+                                                   float* __restrict__ Z) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= c.n) return;
+  const float4 p = c.pts[s];
+  const int o = __float_as_int(p.w);
+  X[o] = p.x;
+  Y[o] = p.y;
+  Z[o] = p.z;
 }
 
 // vind starts as the identity (init_vind): the cloud's points in original order
@@ -1282,6 +1734,24 @@ bool launch_nf_resolve_cov(hipStream_t s, const NfTreeDev& t, const CloudDev& c,
                            double* cov6, const int* status, int* err) {
   if (k > 64) return false;
   k_nf_resolve_cov<<<256, 64 * kNfResolveWaves, 0, s>>>(t, c, ties, k, method, cov6, status, err);
+  return true;
+}
+
+size_t nf_lazy_bytes(int n, int wgs) { return lz_shared_bytes(n) + (size_t)wgs * lz_wg_bytes(n); }
+
+bool launch_nf_lazy(hipStream_t s, const CloudDev& c, const float4* q, TieList ties, int k, int method, double* cov6,
+                    int* out_idx, float* out_d, void* scratch, int wgs, int* err) {
+  if (k > 64 || wgs < 1) return false;
+  char* base = static_cast<char*>(scratch);
+  float* X = reinterpret_cast<float*>(base);
+  float* Y = reinterpret_cast<float*>(base + lz_al(4 * (size_t)c.n));
+  float* Z = reinterpret_cast<float*>(base + 2 * lz_al(4 * (size_t)c.n));
+  k_lz_unsort<<<cdivl(c.n, 256), 256, 0, s>>>(c, X, Y, Z);
+  char* wg = base + lz_shared_bytes(c.n);
+  if (cov6)
+    k_nf_lazy<true><<<wgs, kLzT, 0, s>>>(c, X, Y, Z, q, ties, k, method, cov6, out_idx, out_d, wg, lz_wg_bytes(c.n), err);
+  else
+    k_nf_lazy<false><<<wgs, kLzT, 0, s>>>(c, X, Y, Z, q, ties, k, method, cov6, out_idx, out_d, wg, lz_wg_bytes(c.n), err);
   return true;
 }
 

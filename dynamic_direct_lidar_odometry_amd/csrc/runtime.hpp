@@ -313,7 +313,18 @@ struct gicp_ctx {
   // build scratch, the tied-query list and the resolvers' error word
   bool tie_exact = true;
   DevBuf nf_scratch, tie_buf, nf_err;
-  int* nf_err_host = nullptr;   // pinned copy of nf_err, read after the entry point's final wait
+  int* nf_err_host = nullptr;   // pinned: [0] copy of nf_err, read after the entry point's final wait;
+                                // [1] the last covariance pass's tied-query count
+  // covariance ties without a tree (k_nf_lazy): each tied query's search
+  // splits only the nodes it walks; a cloud with many ties gets the whole
+  // tree instead (lazy_heavy: the previous pass listed more than 2 x the
+  // lazy kernel's workgroups)
+  bool tie_lazy = false;   // DDLO_TIE_LAZY=1 (measured slower than the whole tree so far)
+  bool lazy_heavy = false;
+  DevBuf lazy_buf;
+  hipEvent_t tie_cnt_ev = nullptr;   // recorded after the count's copy
+  bool tie_cnt_pending = false;
+  int lazy_wgs_last = 0;
   bool nf_err_pending = false;
   long ties_resolved = 0;       // diagnostics
   std::weak_ptr<NfTreeData> nf_joined;   // the target tree c->stream last waited for
@@ -427,7 +438,7 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(cd->pts.ensure(sizeof(float4) * npad));
   HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
   launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
-  if (nf_early && c->tie_exact) {
+  if (nf_early && c->tie_exact && !(c->tie_lazy && !c->lazy_heavy)) {
     drain.armed = true;
     gicp_status st = ensure_nftree(c, *cd, s);
     if (st) return st;
@@ -627,7 +638,7 @@ inline gicp_status tie_scratch(gicp_ctx* c, int n, hipStream_t s, TieList* tl) {
   // a point is listed at most twice (the task-based kNN, then the lane-per-query kernel for its group)
   HIP_TRY(grow(c->tie_buf, sizeof(int) * (2 * (size_t)n + 64), s));
   HIP_TRY(c->nf_err.ensure(sizeof(int)));
-  if (!c->nf_err_host) HIP_TRY(hipHostMalloc((void**)&c->nf_err_host, sizeof(int), hipHostMallocDefault));
+  if (!c->nf_err_host) HIP_TRY(hipHostMalloc((void**)&c->nf_err_host, 2 * sizeof(int), hipHostMallocDefault));
   if (!c->nf_err_pending) {
     HIP_TRY(hipMemsetAsync(c->nf_err.p, 0, sizeof(int), s));
     c->nf_err_pending = true;
@@ -662,6 +673,13 @@ inline gicp_status publish_ties(gicp_ctx* c, hipStream_t s) {
   return GICP_OK;
 }
 
+// workgroups of the lazy tie search: one tied query each at a time, a
+// private copy of the cloud each (scratch bounded by ~256 MB)
+inline int lazy_workgroups(int n) {
+  const size_t per = nf_lazy_bytes(n, 1) - nf_lazy_bytes(n, 0);
+  return (int)std::max<size_t>(1, std::min<size_t>(64, (size_t(256) << 20) / std::max<size_t>(per, 1)));
+}
+
 // k_use > 0 overrides the ctx's k (a keyframe smaller than k, odom.hip)
 inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   if (!side.cloud) return fail(GICP_ESTATE, "no cloud on this side");
@@ -682,10 +700,15 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   // exact ties: the points whose k-th neighbour distance is tied get their
   // neighbourhood from nanoflann's own search (nftree.hip)
   TieList tl{nullptr, nullptr};
-  // (building the tree only after a covariance pass that met ties measured
-  // slower on cfg 5: every voxel-filtered scan has ~270 tied queries at k = 10)
+  // the previous pass's tie count (once its copy has landed): many ties make
+  // the whole tree cheaper than one lazy search per tied query
+  if (c->tie_cnt_pending && hipEventQuery(c->tie_cnt_ev) == hipSuccess) {
+    c->lazy_heavy = c->nf_err_host[1] > 2 * std::max(c->lazy_wgs_last, 1);
+    c->tie_cnt_pending = false;
+  }
+  const bool lazy = c->tie_exact && c->tie_lazy && !c->lazy_heavy && !side.cloud->nf;
   if (c->tie_exact) {
-    gicp_status st = ensure_nftree(c, *side.cloud, c->stream);
+    gicp_status st = lazy ? GICP_OK : ensure_nftree(c, *side.cloud, c->stream);
     if (!st) st = tie_scratch(c, side.cloud->n, c->stream, &tl);
     if (st) return st;
   }
@@ -756,11 +779,29 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[1], c->stream));
   c->st_resolve = c->tie_exact;
   if (c->tie_exact) {
-    HIP_TRY(nftree_join(*side.cloud->nf, c->stream));
-    if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[4], c->stream));
-    launch_nf_resolve_cov(c->stream, side.cloud->nf->dev(), cd, tl, k, c->params.regularization,
-                          cv->cov6.as<double>(), side.cloud->nf->status.as<int>(), c->nf_err.as<int>());
-    if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[5], c->stream));
+    if (lazy) {
+      const int n = side.cloud->n;
+      const int wgs = lazy_workgroups(n);
+      HIP_TRY(grow(c->lazy_buf, nf_lazy_bytes(n, wgs), c->stream));
+      if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[4], c->stream));
+      launch_nf_lazy(c->stream, cd, nullptr, tl, k, c->params.regularization, cv->cov6.as<double>(), nullptr, nullptr,
+                     c->lazy_buf.p, wgs, c->nf_err.as<int>());
+      if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[5], c->stream));
+      c->lazy_wgs_last = wgs;
+    } else {
+      HIP_TRY(nftree_join(*side.cloud->nf, c->stream));
+      if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[4], c->stream));
+      launch_nf_resolve_cov(c->stream, side.cloud->nf->dev(), cd, tl, k, c->params.regularization,
+                            cv->cov6.as<double>(), side.cloud->nf->status.as<int>(), c->nf_err.as<int>());
+      if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[5], c->stream));
+      c->lazy_wgs_last = lazy_workgroups(side.cloud->n);
+    }
+    if (c->tie_lazy) {   // the count for the next pass's choice
+      if (!c->tie_cnt_ev) HIP_TRY(hipEventCreateWithFlags(&c->tie_cnt_ev, hipEventDisableTiming));
+      HIP_TRY(hipMemcpyAsync(c->nf_err_host + 1, tl.count, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipEventRecord(c->tie_cnt_ev, c->stream));
+      c->tie_cnt_pending = true;
+    }
     gicp_status st = publish_ties(c, c->stream);
     if (st) return st;
     static const bool dbg = std::getenv("DDLO_TIE_DEBUG") != nullptr;   // development: tied queries per cloud
