@@ -209,7 +209,8 @@ struct AlignJob {
                                  // records, 4 no winner-slice check
   int tie_scan;                  // the scan's tie test: 1 second distance over every examined point, 2 the 8-point
                                  // slices' losing bests + k_moments' check of the winner's slice, 3 equal-distance
-                                 // flags at the merges + the mirrored key + the winner's slice check, 0 none (A/B)
+                                 // flags at the merges + the mirrored key + the winner's slice check, 4 as 3 with
+                                 // the key atomic's return instead of the mirrored key, 0 none (A/B)
   const int* tgt_nf_status;      // the tree build's error bits (device int; 0 = usable)
   NfTreeDev tgt_nf;              // nodes == nullptr: no tree (yet)
   const int* tie_map;            // tgt_nf is a whole cloud the target was cut from (slab shard): its original

@@ -1488,7 +1488,11 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   // tie_scan 3 (not recording): the Morton-order scan plus equal-distance
   // flags at its merges (slices, tasks of a run) and the mirrored key pushed
   // beside the key (runs): no atomic return is waited for
-  const bool tie3 = !rec && job->tie_scan == 3;
+  // tie_scan 4: the same, but the runs' ties come from the key's atomicMin
+  // return (consumed at the next run's merge) and a run's own merges instead
+  // of a mirrored key: one atomic per run, no key2 traffic
+  const bool tie3 = !rec && (job->tie_scan == 3 || job->tie_scan == 4);
+  const bool mirror = job->tie_scan == 3;
   const bool tie_xor = !(job->tie_ab & 2);
   unsigned long long* const key2 = job->key2;
   unsigned td = 0xffffffffu;   // smallest distance (bits) met twice at a slice merge of this run (any slice lane)
@@ -1521,7 +1525,17 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
       pend = false;
     }
   };
+  // tie_scan 4 (the same pending slot, reuse is off): the previous run's key
+  // atomicMin return at the same distance and another position is a tie
+  auto resolve4 = [&]() {
+    if (pend) {
+      if (key_real(pend_old) && pend_old != pend_acc && (pend_old >> 32) == (pend_acc >> 32))
+        atomicMin(sec + pend_q, (unsigned)(pend_acc >> 32));
+      pend = false;
+    }
+  };
   auto flush_run = [&]() {
+    if (tie3 && !mirror) resolve4();
     if (run_sg >= 0 && lane < 16 && (unsigned)(acc >> 32) <= __float_as_uint(run_bound)) {
       const size_t qidx = (size_t)run_sg * kTaskQ + qi;
       if (reuse) {
@@ -1532,6 +1546,11 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
         pend_acc = acc;
         pend_acc2 = acc2;
         pend_bound = run_bound;
+      } else if (tie3 && !mirror) {
+        pend_old = atomicMin(key + qidx, acc);
+        pend = true;
+        pend_q = qidx;
+        pend_acc = acc;
       } else {
         atomicMin(key + qidx, acc);
         if (tie3 && !(job->tie_ab & 1)) atomicMin(key2 + qidx, accm);   // with key: two of the run's tasks at the distance = a tie
@@ -1650,8 +1669,10 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
             }
             if (on) {
               td = min(td, tt);
+              // two of the run's tasks at one distance (tie_scan 4; a leaf met twice in a run is one key)
+              if (!mirror && acc != bk && (acc >> 32) == (bk >> 32)) td = min(td, (unsigned)(bk >> 32));
               acc = umin64(acc, bk);
-              accm = umin64(accm, mirror_key(bk));   // (a leaf met twice in a run is one key: no false tie)
+              if (mirror) accm = umin64(accm, mirror_key(bk));   // (a leaf met twice in a run is one key: no false tie)
             }
           } else {
             bk = xor_min64<16>(bk);
@@ -1665,7 +1686,8 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
     }
   }
   flush_run();
-  resolve();
+  if (tie3 && !mirror) resolve4();
+  else resolve();
 }
 
 template <int Q, int MINW>

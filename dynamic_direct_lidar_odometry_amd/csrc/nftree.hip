@@ -1276,6 +1276,18 @@ struct LzShared {
   int sh[17];
   int sp, fail;
   float worst;
+  int wb, wc;   // the node range held in LDS (LzWin), wc = 0: none
+};
+
+// A node of <= kLzL points is split in LDS: when the search enters one, its
+// range is copied there and its whole subtree is split in place in LDS (the
+// search leaves a subtree only when done with it, so nothing is written back).
+constexpr int kLzL = 6144;
+struct LzWin {
+  float x[kLzL], y[kLzL], z[kLzL];
+  int id[kLzL];
+  int ml[kLzL / 2 + 64], mr[kLzL / 2 + 64];
+  int cz[kLzL / 64 + 4], cr[kLzL / 64 + 4];
 };
 
 __device__ __forceinline__ float* lz_axis(const LzMem& m, int f) { return f == 0 ? m.x : (f == 1 ? m.y : m.z); }
@@ -1314,6 +1326,11 @@ __device__ __forceinline__ int lz_scan(int* a, int cnt, LzShared& S) {
   return tot;
 }
 
+// The passes below keep kLzU independent loads in flight per thread: one
+// workgroup reads its node from L2 at ~60 GB/s only with ~32 KB in flight
+// (a load-use loop waits a full L2 round trip per element).
+constexpr int kLzU = 16;
+
 // One Hoare pass of the node at base b (count n) as a rank pairing: the r-th
 // bad element of the zone [zlo, zhi) (ascending) swaps with the r-th good
 // element of [zhi, n) (descending); good = v < cut (pass 1) or v == cut
@@ -1322,25 +1339,28 @@ __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi
   const int lane = __lane_id(), w = threadIdx.x >> 6;
   const float* V = lz_axis(m, feat) + b;
   const int nz = (zhi - zlo + 63) / 64, nr = (n - zhi + 63) / 64;
-  for (int z = w; z < nz; z += kLzW) {
-    const int i = zlo + 64 * z + lane;
-    bool f = false;
-    if (i < zhi) {
-      const float x = V[i];
-      f = !(pass2 ? x == cut : x < cut);
+  // chunk j < nz: zone chunk j (ascending from zlo); j >= nz: right chunk j - nz (descending from n)
+  const int nch = nz + nr;
+  auto chunk_flag = [&](int j, float x, bool in) -> bool {
+    if (!in) return false;
+    const bool good = pass2 ? x == cut : x < cut;
+    return j < nz ? !good : good;
+  };
+  auto chunk_pos = [&](int j) -> int { return j < nz ? zlo + 64 * j + lane : n - 1 - 64 * (j - nz) - lane; };
+  auto chunk_in = [&](int j, int i) -> bool { return j < nch && (j < nz ? i < zhi : i >= zhi); };
+  for (int j0 = w; j0 < nch; j0 += kLzW * kLzU) {
+    float xs[kLzU];
+#pragma unroll
+    for (int u = 0; u < kLzU; ++u) {
+      const int j = j0 + u * kLzW, i = chunk_pos(j);
+      xs[u] = chunk_in(j, i) ? V[i] : 0.f;
     }
-    const int c = __popcll(__ballot(f));
-    if (lane == 0) m.cz[z] = c;
-  }
-  for (int r = w; r < nr; r += kLzW) {
-    const int i = n - 1 - 64 * r - lane;
-    bool f = false;
-    if (i >= zhi) {
-      const float x = V[i];
-      f = pass2 ? x == cut : x < cut;
+#pragma unroll
+    for (int u = 0; u < kLzU; ++u) {
+      const int j = j0 + u * kLzW, i = chunk_pos(j);
+      const int c = __popcll(__ballot(chunk_flag(j, xs[u], chunk_in(j, i))));
+      if (lane == 0 && j < nch) (j < nz ? m.cz[j] : m.cr[j - nz]) = c;
     }
-    const int c = __popcll(__ballot(f));
-    if (lane == 0) m.cr[r] = c;
   }
   __syncthreads();
   const int mz = lz_scan(m.cz, nz, S);
@@ -1348,35 +1368,50 @@ __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi
   __syncthreads();
   if (mz != mr) return false;
   if (mz == 0) return true;
-  for (int z = w; z < nz; z += kLzW) {
-    const int i = zlo + 64 * z + lane;
-    bool f = false;
-    if (i < zhi) {
-      const float x = V[i];
-      f = !(pass2 ? x == cut : x < cut);
+  for (int j0 = w; j0 < nch; j0 += kLzW * kLzU) {
+    float xs[kLzU];
+    int base[kLzU];
+#pragma unroll
+    for (int u = 0; u < kLzU; ++u) {
+      const int j = j0 + u * kLzW, i = chunk_pos(j);
+      xs[u] = chunk_in(j, i) ? V[i] : 0.f;
+      base[u] = j < nch ? (j < nz ? m.cz[j] : m.cr[j - nz]) : 0;
     }
-    const unsigned long long mask = __ballot(f);
-    const int slot = m.cz[z] + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-    if (f) m.ml[slot] = i;
-  }
-  for (int r = w; r < nr; r += kLzW) {
-    const int i = n - 1 - 64 * r - lane;   // lane order = descending positions
-    bool f = false;
-    if (i >= zhi) {
-      const float x = V[i];
-      f = pass2 ? x == cut : x < cut;
+#pragma unroll
+    for (int u = 0; u < kLzU; ++u) {
+      const int j = j0 + u * kLzW, i = chunk_pos(j);
+      const bool f = chunk_flag(j, xs[u], chunk_in(j, i));
+      const unsigned long long mask = __ballot(f);
+      const int slot = base[u] + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+      if (f) (j < nz ? m.ml : m.mr)[slot] = i;   // right chunks: lane order = descending positions
     }
-    const unsigned long long mask = __ballot(f);
-    const int slot = m.cr[r] + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-    if (f) m.mr[slot] = i;
   }
   __syncthreads();
-  for (int r = threadIdx.x; r < mz; r += kLzT) {
-    const int a = b + m.ml[r], c = b + m.mr[r];
-    const float ax = m.x[a], ay = m.y[a], az = m.z[a];
-    const int ai = m.id[a];
-    m.x[a] = m.x[c]; m.y[a] = m.y[c]; m.z[a] = m.z[c]; m.id[a] = m.id[c];
-    m.x[c] = ax; m.y[c] = ay; m.z[c] = az; m.id[c] = ai;
+  constexpr int U = kLzU / 2;
+  for (int r0 = threadIdx.x; r0 < mz; r0 += kLzT * U) {
+    int a[U], c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = r0 + u * kLzT;
+      a[u] = r < mz ? b + m.ml[r] : -1;
+      c[u] = r < mz ? b + m.mr[r] : -1;
+    }
+    float ax[U], ay[U], az[U], cx[U], cy[U], cz[U];
+    int ai[U], ci[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (a[u] >= 0) {
+        ax[u] = m.x[a[u]]; ay[u] = m.y[a[u]]; az[u] = m.z[a[u]]; ai[u] = m.id[a[u]];
+        cx[u] = m.x[c[u]]; cy[u] = m.y[c[u]]; cz[u] = m.z[c[u]]; ci[u] = m.id[c[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (a[u] >= 0) {
+        m.x[a[u]] = cx[u]; m.y[a[u]] = cy[u]; m.z[a[u]] = cz[u]; m.id[a[u]] = ci[u];
+        m.x[c[u]] = ax[u]; m.y[c[u]] = ay[u]; m.z[c[u]] = az[u]; m.id[c[u]] = ai[u];
+      }
+    }
   }
   __syncthreads();
   return true;
@@ -1385,31 +1420,59 @@ __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi
 // middleSplit_ + planeSplit of the node f (whole workgroup), in place; the
 // split position and the children's faces along the cut dimension (divlow =
 // the left child's max, divhigh = the right child's min, :1032-1033)
-__device__ __forceinline__ bool lz_split(const LzMem& m, const LzFrame& f, int* feat_out, float* cut_out, int* index_out,
-                         float* dlo, float* dhi, LzShared& S) {
-  const int b = f.begin, n = f.count;
+__device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f, int* feat_out, float* cut_out,
+                                         int* index_out, float* dlo, float* dhi, LzShared& S) {
+  const int n = f.count;
+  const float lo[3] = {f.lx, f.ly, f.lz}, hi[3] = {f.hx, f.hy, f.hz};
+  // computeMinMax (:965-978) only along the dimensions middleSplit_ measures
+  // (span > (1 - EPS) max_span of the passed-down box, the test of nf_cut3)
+  const float EPS = 0.00001f;
+  float max_span = hi[0] - lo[0];
+#pragma unroll
+  for (int i = 1; i < 3; ++i) max_span = fmaxf(max_span, hi[i] - lo[i]);
+  const bool c0 = hi[0] - lo[0] > (1 - EPS) * max_span, c1 = hi[1] - lo[1] > (1 - EPS) * max_span,
+             c2 = hi[2] - lo[2] > (1 - EPS) * max_span;
   float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int i = threadIdx.x; i < n; i += kLzT) {   // computeMinMax (:965-978)
-    const float x = m.x[b + i], y = m.y[b + i], z = m.z[b + i];
-    v[0] = fminf(v[0], x); v[1] = fminf(v[1], y); v[2] = fminf(v[2], z);
-    v[3] = fmaxf(v[3], x); v[4] = fmaxf(v[4], y); v[5] = fmaxf(v[5], z);
+  for (int i0 = threadIdx.x; i0 < n; i0 += kLzT * kLzU) {
+    float xs[kLzU], ys[kLzU], zs[kLzU];
+#pragma unroll
+    for (int u = 0; u < kLzU; ++u) {   // NaN for absent elements: fminf / fmaxf ignore it
+      const int i = i0 + u * kLzT;
+      const bool in = i < n;
+      xs[u] = c0 && in ? m.x[b + i] : NAN;
+      ys[u] = c1 && in ? m.y[b + i] : NAN;
+      zs[u] = c2 && in ? m.z[b + i] : NAN;
+    }
+#pragma unroll
+    for (int u = 0; u < kLzU; ++u) {
+      v[0] = fminf(v[0], xs[u]); v[1] = fminf(v[1], ys[u]); v[2] = fminf(v[2], zs[u]);
+      v[3] = fmaxf(v[3], xs[u]); v[4] = fmaxf(v[4], ys[u]); v[5] = fmaxf(v[5], zs[u]);
+    }
   }
   lz_reduce6(v, S);
   const float mn[3] = {v[0], v[1], v[2]}, mx[3] = {v[3], v[4], v[5]};
   int feat;
   float cut;
-  const float lo[3] = {f.lx, f.ly, f.lz}, hi[3] = {f.hx, f.hy, f.hz};
   nf_cut3(lo, hi, mn, mx, &feat, &cut);
   // lim1 = #(v < cut), lim2 = #(v <= cut), and the max below / min above the cut
   const float* V = lz_axis(m, feat) + b;
   int lt = 0, le = 0;
   float mlt = -INFINITY, mgt = INFINITY;
-  for (int i = threadIdx.x; i < n; i += kLzT) {
-    const float x = V[i];
-    lt += x < cut;
-    le += x <= cut;
-    if (x < cut) mlt = fmaxf(mlt, x);
-    if (x > cut) mgt = fminf(mgt, x);
+  for (int i0 = threadIdx.x; i0 < n; i0 += kLzT * kLzU) {
+    float xs[kLzU];
+#pragma unroll
+    for (int u = 0; u < kLzU; ++u) {
+      const int i = i0 + u * kLzT;
+      xs[u] = i < n ? V[i] : NAN;   // NaN: every comparison false
+    }
+#pragma unroll
+    for (int u = 0; u < kLzU; ++u) {
+      const float x = xs[u];
+      lt += x < cut;
+      le += x <= cut;
+      if (x < cut) mlt = fmaxf(mlt, x);
+      if (x > cut) mgt = fminf(mgt, x);
+    }
   }
   for (int d = 32; d >= 1; d >>= 1) {
     lt += __shfl_xor(lt, d);
@@ -1454,20 +1517,39 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
                                                   float* __restrict__ out_d, char* __restrict__ scr, size_t wg_bytes,
                                                   int* __restrict__ err) {
   __shared__ LzShared S;
+  __shared__ LzWin Wn;
   const int n = c.n;
   const int lane = __lane_id();
   const int nc = *ties.count;
   const int nl = min(nc, ties.cap);
   if (nc > ties.cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 8);
-  const LzMem m = lz_mem(scr + (size_t)blockIdx.x * wg_bytes, n);
+  const LzMem gm = lz_mem(scr + (size_t)blockIdx.x * wg_bytes, n);
+  LzMem wm;
+  wm.x = Wn.x; wm.y = Wn.y; wm.z = Wn.z; wm.id = Wn.id;
+  wm.ml = Wn.ml; wm.mr = Wn.mr; wm.cz = Wn.cz; wm.cr = Wn.cr;
+  const LzMem& m = gm;
   for (int li = blockIdx.x; li < nl; li += gridDim.x) {
     const int qi = ties.list[li];
     const float4 qp = COV ? c.pts[qi] : q[qi];
-    for (int j = threadIdx.x; j < n; j += kLzT) {   // vind = 0 .. n-1 (init_vind)
-      m.x[j] = X0[j];
-      m.y[j] = Y0[j];
-      m.z[j] = Z0[j];
-      m.id[j] = j;
+    for (int j0 = threadIdx.x; j0 < n; j0 += kLzT * kLzU) {   // vind = 0 .. n-1 (init_vind)
+      float xs[kLzU], ys[kLzU], zs[kLzU];
+#pragma unroll
+      for (int u = 0; u < kLzU; ++u) {
+        const int j = min(j0 + u * kLzT, n - 1);
+        xs[u] = X0[j];
+        ys[u] = Y0[j];
+        zs[u] = Z0[j];
+      }
+#pragma unroll
+      for (int u = 0; u < kLzU; ++u) {
+        const int j = j0 + u * kLzT;
+        if (j < n) {
+          m.x[j] = xs[u];
+          m.y[j] = ys[u];
+          m.z[j] = zs[u];
+          m.id[j] = j;
+        }
+      }
     }
     // computeInitialDistances (:1145-1164) against root_bbox
     const float rlo[3] = {c.quant[0], c.quant[1], c.quant[2]}, rhi[3] = {c.quant[4], c.quant[5], c.quant[6]};
@@ -1492,6 +1574,8 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
       S.sp = 1;
       S.fail = 0;
       S.worst = FLT_MAX;
+      S.wb = 0;
+      S.wc = 0;
     }
     float kd = FLT_MAX;   // wave 0: lane j's result slot (KNNResultSet)
     int kx = -1, count = 0;
@@ -1501,7 +1585,40 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
       if (sp == 0 || S.fail) break;
       const LzFrame f = S.F[sp - 1];
       const float worst = S.worst;
+      int wb = S.wb, wc = S.wc;
       __syncthreads();   // every thread has the frame before thread 0 rewrites it
+      bool inw = wc > 0 && f.begin >= wb && f.begin + f.count <= wb + wc;
+      if (!inw && f.state == 0 && f.count > kNfLeafMax && f.count <= kLzL) {   // enter a subtree that fits LDS
+        for (int j0 = threadIdx.x; j0 < f.count; j0 += kLzT * 4) {
+          float xs[4], ys[4], zs[4];
+          int is[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = min(j0 + u * kLzT, f.count - 1) + f.begin;
+            xs[u] = gm.x[j]; ys[u] = gm.y[j]; zs[u] = gm.z[j]; is[u] = gm.id[j];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kLzT;
+            if (j < f.count) {
+              Wn.x[j] = xs[u]; Wn.y[j] = ys[u]; Wn.z[j] = zs[u]; Wn.id[j] = is[u];
+            }
+          }
+        }
+        wb = f.begin;
+        wc = f.count;
+        inw = true;
+        if (threadIdx.x == 0) {
+          S.wb = wb;
+          S.wc = wc;
+        }
+        __syncthreads();
+      }
+      LzMem nm;   // the node's storage and its offset there (field selects: a selected struct reference
+                  // would put both in private memory)
+      nm.x = inw ? wm.x : gm.x; nm.y = inw ? wm.y : gm.y; nm.z = inw ? wm.z : gm.z; nm.id = inw ? wm.id : gm.id;
+      nm.ml = inw ? wm.ml : gm.ml; nm.mr = inw ? wm.mr : gm.mr; nm.cz = inw ? wm.cz : gm.cz; nm.cr = inw ? wm.cr : gm.cr;
+      const int off = inw ? wb : 0;
       if (f.count <= kNfLeafMax) {   // leaf: candidates below the worst distance read at the leaf (:1503-1516)
         if (threadIdx.x < 64) {
           for (int bb = f.begin; bb < f.begin + f.count; bb += 64) {
@@ -1511,13 +1628,13 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
             bool cand = false;
             if (i < f.begin + f.count) {
               r = 0.f;
-              float diff = qp.x - m.x[i];
+              float diff = qp.x - nm.x[i - off];
               r += diff * diff;
-              diff = qp.y - m.y[i];
+              diff = qp.y - nm.y[i - off];
               r += diff * diff;
-              diff = qp.z - m.z[i];
+              diff = qp.z - nm.z[i - off];
               r += diff * diff;
-              ip = m.id[i];
+              ip = nm.id[i - off];
               cand = r < worst;
             }
             unsigned long long mk = __ballot(cand);
@@ -1553,7 +1670,7 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
       if (f.state == 0) {   // first visit: split the node (divideTree's recursion step)
         int feat, index;
         float cut, dlo, dhi;
-        const bool ok = lz_split(m, f, &feat, &cut, &index, &dlo, &dhi, S);
+        const bool ok = lz_split(nm, f.begin - off, f, &feat, &cut, &index, &dlo, &dhi, S);
         const float val = feat == 0 ? qp.x : (feat == 1 ? qp.y : qp.z);
         const bool first1 = ((val - dlo) + (val - dhi)) < 0;   // searchLevel (:1525-1540)
         if (threadIdx.x == 0) {

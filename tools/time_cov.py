@@ -24,3 +24,15 @@ for k in (10, 20):
         c.close()
         out[f"k{k}_{'nanoflann' if exact else 'morton'}_ms"] = round(1e3 * float(np.median(ts[1:])), 4)
 print(out)
+# device stage times (HIP events) of the nanoflann-order pass: covariance kernel, tree build, tie resolution
+c = P.Context(0)
+c.set_params(P.default_params(k_correspondences=10))
+c.set_profiling(True)
+st = []
+for f in frames:
+    c.set_target(f)
+    c.compute_covariances(TARGET)
+    c.synchronize()
+    st.append(c.stage_times())
+c.close()
+print({"k10_stage_ms (cov, tree, resolve)": [round(float(v), 4) for v in np.median(np.array(st[1:]), axis=0)]})
