@@ -85,6 +85,8 @@ struct NfTreeDev {
   const NfNode* nodes; // node 0 = root
   const float4* box;   // [2]: root_bbox (lo, hi), computeInitialDistances
   int n;
+  int partial;         // the top levels only: a node with feat == -2 is an unsplit subtree (vind range [c1, c2),
+  const float4* sbox;  // the box divideTree passes it: sbox[2 id], sbox[2 id + 1]); the lazy search splits it
 };
 
 // Per-align device state (one per ctx, lives in device memory).
@@ -252,6 +254,7 @@ struct NfBuild {
   int *cA, *cAE, *cE2;     // [max_chunks] per-chunk counts
   float4 *tblL, *tblR;     // [n] rank tables of the Hoare pairing
   const float* quant;      // the cloud's bbox: min [0..2], max [4..6]
+  float4* sbox;            // partial build: the passed-down box of every unsplit node (indexed by node id)
   const float4* sorted;    // the cloud's Morton-sorted points (w = original index bits)
   int n, Lmax, max_task, max_pend, max_small, max_chunks;
   int nbucket;             // the size the grids are sized for (>= n): one captured graph per bucket

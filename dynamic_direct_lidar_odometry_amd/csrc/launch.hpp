@@ -85,14 +85,17 @@ bool launch_nf_resolve_cov(hipStream_t s, const NfTreeDev& t, const CloudDev& c,
                            double* cov6, const int* status, int* err);
 bool launch_nf_resolve_knn(hipStream_t s, const NfTreeDev& t, const float4* q, TieList ties, int k, int* out_idx,
                            float* out_d, const int* status, int* err);
-// the same re-run without a tree: each listed query's nanoflann search splits
-// only the nodes it enters, on a private copy of vind (one workgroup per
-// query, wgs workgroups; scratch: nf_lazy_bytes(c.n, wgs)).  cov6 != nullptr:
-// the cloud's own tied points get their covariances; else rows of q their
-// (out_idx, out_d).  *err |= 1 depth, 4 fewer than k, 16 pairing check.
+// the same re-run on the cloud's partial tree (nftree_build partial_levels):
+// each listed query's nanoflann search walks the built top levels and splits
+// the stubs it enters lazily, on a private copy of their vind ranges (one
+// workgroup per query, wgs workgroups; scratch: nf_lazy_bytes(c.n, wgs)).
+// cov6 != nullptr: the cloud's own tied points get their covariances; else
+// rows of q their (out_idx, out_d).  *err |= 1 depth, 2 build, 4 fewer than k,
+// 16 pairing check.
 size_t nf_lazy_bytes(int n, int wgs);
-bool launch_nf_lazy(hipStream_t s, const CloudDev& c, const float4* q, TieList ties, int k, int method, double* cov6,
-                    int* out_idx, float* out_d, void* scratch, int wgs, int* err);
+bool launch_nf_lazy(hipStream_t s, const NfTreeDev& t, const CloudDev& c, const float4* q, TieList ties, int k,
+                    int method, double* cov6, int* out_idx, float* out_d, void* scratch, int wgs, const int* status,
+                    int* err);
 void launch_cov_remap(hipStream_t s, const double* old_cov6, const int* old_inv_perm, const int* new_perm, int n,
                       double* cov6);
 

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdio>
+#include <cstdlib>
 
 #include "cov_math.hpp"
 #include "gicp_types.hpp"
@@ -1228,7 +1229,8 @@ struct LzFrame {
   float fm, fd, divlow, divhigh;     // mindistsq, the saved dists[feat], the split's divs
   int index;                         // split position (relative to begin)
   float cut;
-  int pad[2];
+  int node;                          // >= 0: a node of the built top levels (its record); -1: a lazily split range
+  int pad;
 };
 // left_bbox (.hi[feat] = cut) / right_bbox (.lo[feat] = cut) of divideTree (:1024-1030)
 // (value selects: a store through a feat-dependent field pointer keeps the frame in private memory)
@@ -1253,7 +1255,6 @@ static __host__ __device__ inline size_t lz_al(size_t b) { return (b + 255) / 25
 static __host__ __device__ inline size_t lz_wg_bytes(int n) {
   return 4 * lz_al(4 * (size_t)n) + 2 * lz_al(4 * ((size_t)n / 2 + 64)) + 2 * lz_al(4 * ((size_t)n / 64 + 4));
 }
-static __host__ __device__ inline size_t lz_shared_bytes(int n) { return 3 * lz_al(4 * (size_t)n); }
 
 __device__ __forceinline__ LzMem lz_mem(char* p, int n) {
   LzMem m;
@@ -1274,10 +1275,23 @@ struct LzShared {
   float rf[kLzW][8];
   int ri[kLzW][4];
   int sh[17];
+  int tot[2];
+  float ld[64];   // lz_leaf's staging (wave 0)
+  int lx[64];
   int sp, fail;
   float worst;
   int wb, wc;   // the node range held in LDS (LzWin), wc = 0: none
+  int prof;     // DDLO_LAZY_PROF (development): per-phase cycles of block 0's first query
+  unsigned long long pt, pa[16];
 };
+// development profile: thread 0 adds the cycles since the last mark to phase i
+__device__ __forceinline__ void lz_mark(LzShared& S, int i) {
+  if (S.prof && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    S.pa[i] += t - S.pt;
+    S.pt = t;
+  }
+}
 
 // A node of <= kLzL points is split in LDS: when the search enters one, its
 // range is copied there and its whole subtree is split in place in LDS (the
@@ -1310,8 +1324,20 @@ __device__ __forceinline__ void lz_reduce6(float v[6], LzShared& S) {
   __syncthreads();
 }
 
-// exclusive prefix of a[0, cnt) in place (global memory), returns the total
-__device__ __forceinline__ int lz_scan(int* a, int cnt, LzShared& S) {
+// exclusive prefix of a[0, cnt) in place, returns the total (slot: this
+// call site's total word; up to 64 entries one wavefront scans them)
+__device__ __forceinline__ int lz_scan(int* a, int cnt, LzShared& S, int slot) {
+  if (cnt <= 64) {
+    if (threadIdx.x < 64) {
+      const int lane = __lane_id();
+      const int v = lane < cnt ? a[lane] : 0;
+      const int inc = wave_incl_scan(v);
+      if (lane < cnt) a[lane] = inc - v;
+      if (lane == 63) S.tot[slot] = inc;
+    }
+    __syncthreads();
+    return S.tot[slot];
+  }
   const int per = (cnt + kLzT - 1) / kLzT;
   const int b0 = min((int)threadIdx.x * per, cnt), b1 = min(b0 + per, cnt);
   int s = 0;
@@ -1363,9 +1389,11 @@ __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi
     }
   }
   __syncthreads();
-  const int mz = lz_scan(m.cz, nz, S);
-  const int mr = lz_scan(m.cr, nr, S);
+  lz_mark(S, 3);
+  const int mz = lz_scan(m.cz, nz, S, 0);
+  const int mr = lz_scan(m.cr, nr, S, 1);
   __syncthreads();
+  lz_mark(S, 4);
   if (mz != mr) return false;
   if (mz == 0) return true;
   for (int j0 = w; j0 < nch; j0 += kLzW * kLzU) {
@@ -1387,6 +1415,7 @@ __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi
     }
   }
   __syncthreads();
+  lz_mark(S, 5);
   constexpr int U = kLzU / 2;
   for (int r0 = threadIdx.x; r0 < mz; r0 += kLzT * U) {
     int a[U], c[U];
@@ -1414,6 +1443,7 @@ __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi
     }
   }
   __syncthreads();
+  lz_mark(S, 6);
   return true;
 }
 
@@ -1450,6 +1480,7 @@ __device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f
     }
   }
   lz_reduce6(v, S);
+  lz_mark(S, 1);
   const float mn[3] = {v[0], v[1], v[2]}, mx[3] = {v[3], v[4], v[5]};
   int feat;
   float cut;
@@ -1497,6 +1528,7 @@ __device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f
     min_gt = fminf(min_gt, S.rf[i][1]);
   }
   __syncthreads();
+  lz_mark(S, 2);
   bool ok = lz_hoare(m, b, 0, lim1, n, feat, cut, false, S);
   if (ok && lim2 > lim1) ok = lz_hoare(m, b, lim1, lim2, n, feat, cut, true, S);   // pass 2 (:1128-1142)
   const int index = nf_index(n, lim1, lim2);
@@ -1508,14 +1540,99 @@ __device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f
   return ok;
 }
 
+// KNNResultSet::addPoint over one leaf (wave 0): candidates are the points
+// below the worst distance read at the leaf (:1503-1516), inserted in leaf
+// order; lane j < k holds the j-th result (kd, kx), count = results so far.
+// The serial insertions keep the first k of the stable order (distance, then
+// insertion time) of the kept list followed by the candidates in leaf order,
+// so every item's final slot is a count: a kept entry moves down by the
+// candidates strictly closer, a candidate lands after the entries and earlier
+// candidates no farther and the later candidates strictly closer.
+// (ld, lx: 64-entry LDS staging of wave 0.)
+template <class LOAD>
+__device__ __forceinline__ void lz_leaf(LOAD load, int b0, int b1, float qx, float qy, float qz, float worst, int k,
+                                        float& kd, int& kx, int& count, float* ld, int* lx) {
+  const int lane = __lane_id();
+  const int m = b1 - b0;   // <= kNfLeafMax (100): two rounds of 64
+  float r[2] = {FLT_MAX, FLT_MAX};
+  int ip[2] = {-1, -1};
+  bool cd[2] = {false, false};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = 64 * h + lane;
+    if (i < m) {
+      float px, py, pz;
+      load(b0 + i, px, py, pz, ip[h]);
+      float rr = 0.f;
+      float diff = qx - px;
+      rr += diff * diff;
+      diff = qy - py;
+      rr += diff * diff;
+      diff = qz - pz;
+      rr += diff * diff;
+      r[h] = rr;
+      cd[h] = rr < worst;
+    }
+  }
+  const unsigned long long cm[2] = {__ballot(cd[0]), __ballot(cd[1])};
+  const int nc = __popcll(cm[0]) + __popcll(cm[1]);
+  if (nc == 0) return;
+  // candidate ranks (own position p = 64 h + lane) and the entries' shifts
+  int rk[2] = {0, 0};
+  int sh_e = 0;   // candidates strictly closer than this lane's entry
+  for (int j = 0; j < count; ++j) {
+    const float e = __shfl(kd, j);
+    rk[0] += e <= r[0];
+    rk[1] += e <= r[1];
+  }
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    unsigned long long mk = cm[h2];
+    while (mk) {
+      const int bl = __ffsll((long long)mk) - 1;
+      mk &= mk - 1;
+      const float rc = __shfl(r[h2], bl);
+      const int pc = 64 * h2 + bl;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int p = 64 * h + lane;
+        rk[h] += pc < p ? (rc <= r[h]) : (pc > p ? (rc < r[h]) : 0);
+      }
+      sh_e += rc < kd;
+    }
+  }
+  if (lane < count && lane + sh_e < k) {
+    ld[lane + sh_e] = kd;
+    lx[lane + sh_e] = kx;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (cd[h] && rk[h] < k) {
+      ld[rk[h]] = r[h];
+      lx[rk[h]] = ip[h];
+    }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  count = min(k, count + nc);
+  if (lane < count) {
+    kd = ld[lane];
+    kx = lx[lane];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();   // the staging is read before the next leaf rewrites it
+}
+
 // COV: queries are the cloud's own points (sorted positions in the list),
 // the result is their covariance; else rows of q, the result (index, distance).
+// t: the cloud's partial tree (the top levels, stubs below, nftree_build
+// partial_levels): the search walks the built nodes as nf_search does and,
+// entering a stub, copies its range (vind order) into its private scratch and
+// splits the stub's subtree lazily from there.
 template <bool COV>
-__global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __restrict__ X0, const float* __restrict__ Y0,
-                                                  const float* __restrict__ Z0, const float4* __restrict__ q, TieList ties,
+__global__ __launch_bounds__(kLzT) void k_nf_lazy(NfTreeDev t, CloudDev c, const float4* __restrict__ q, TieList ties,
                                                   int k, int method, double* __restrict__ cov6, int* __restrict__ out_idx,
                                                   float* __restrict__ out_d, char* __restrict__ scr, size_t wg_bytes,
-                                                  int* __restrict__ err) {
+                                                  const int* __restrict__ status, int* __restrict__ err, int prof) {
   __shared__ LzShared S;
   __shared__ LzWin Wn;
   const int n = c.n;
@@ -1523,51 +1640,36 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
   const int nc = *ties.count;
   const int nl = min(nc, ties.cap);
   if (nc > ties.cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 8);
+  if (*status) {   // the partial build failed: report, keep the Morton-order answers
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nl > 0) atomicOr(err, 2 | (*status << 8));
+    return;
+  }
   const LzMem gm = lz_mem(scr + (size_t)blockIdx.x * wg_bytes, n);
   LzMem wm;
   wm.x = Wn.x; wm.y = Wn.y; wm.z = Wn.z; wm.id = Wn.id;
   wm.ml = Wn.ml; wm.mr = Wn.mr; wm.cz = Wn.cz; wm.cr = Wn.cr;
-  const LzMem& m = gm;
   for (int li = blockIdx.x; li < nl; li += gridDim.x) {
     const int qi = ties.list[li];
     const float4 qp = COV ? c.pts[qi] : q[qi];
-    for (int j0 = threadIdx.x; j0 < n; j0 += kLzT * kLzU) {   // vind = 0 .. n-1 (init_vind)
-      float xs[kLzU], ys[kLzU], zs[kLzU];
-#pragma unroll
-      for (int u = 0; u < kLzU; ++u) {
-        const int j = min(j0 + u * kLzT, n - 1);
-        xs[u] = X0[j];
-        ys[u] = Y0[j];
-        zs[u] = Z0[j];
-      }
-#pragma unroll
-      for (int u = 0; u < kLzU; ++u) {
-        const int j = j0 + u * kLzT;
-        if (j < n) {
-          m.x[j] = xs[u];
-          m.y[j] = ys[u];
-          m.z[j] = zs[u];
-          m.id[j] = j;
-        }
-      }
-    }
     // computeInitialDistances (:1145-1164) against root_bbox
-    const float rlo[3] = {c.quant[0], c.quant[1], c.quant[2]}, rhi[3] = {c.quant[4], c.quant[5], c.quant[6]};
+    const float4 rl = t.box[0], rh = t.box[1];
     float d0 = 0.f, d1 = 0.f, d2 = 0.f, distsq = 0.f;
-    if (qp.x < rlo[0]) { d0 = (qp.x - rlo[0]) * (qp.x - rlo[0]); distsq += d0; }
-    if (qp.x > rhi[0]) { d0 = (qp.x - rhi[0]) * (qp.x - rhi[0]); distsq += d0; }
-    if (qp.y < rlo[1]) { d1 = (qp.y - rlo[1]) * (qp.y - rlo[1]); distsq += d1; }
-    if (qp.y > rhi[1]) { d1 = (qp.y - rhi[1]) * (qp.y - rhi[1]); distsq += d1; }
-    if (qp.z < rlo[2]) { d2 = (qp.z - rlo[2]) * (qp.z - rlo[2]); distsq += d2; }
-    if (qp.z > rhi[2]) { d2 = (qp.z - rhi[2]) * (qp.z - rhi[2]); distsq += d2; }
+    if (qp.x < rl.x) { d0 = (qp.x - rl.x) * (qp.x - rl.x); distsq += d0; }
+    if (qp.x > rh.x) { d0 = (qp.x - rh.x) * (qp.x - rh.x); distsq += d0; }
+    if (qp.y < rl.y) { d1 = (qp.y - rl.y) * (qp.y - rl.y); distsq += d1; }
+    if (qp.y > rh.y) { d1 = (qp.y - rh.y) * (qp.y - rh.y); distsq += d1; }
+    if (qp.z < rl.z) { d2 = (qp.z - rl.z) * (qp.z - rl.z); distsq += d2; }
+    if (qp.z > rh.z) { d2 = (qp.z - rh.z) * (qp.z - rh.z); distsq += d2; }
     if (threadIdx.x == 0) {
+      S.prof = prof && li == 0;
+      S.pt = __builtin_amdgcn_s_memtime();
+      for (int e = 0; e < 16; ++e) S.pa[e] = 0;
       LzFrame r;
+      r.node = 0;
       r.begin = 0;
       r.count = n;
       r.state = 0;
       r.feat = 0;
-      r.lx = rlo[0]; r.ly = rlo[1]; r.lz = rlo[2];
-      r.hx = rhi[0]; r.hy = rhi[1]; r.hz = rhi[2];
       r.fm = distsq;
       r.fd = 0.f;
       S.F[0] = r;
@@ -1583,10 +1685,116 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
     for (;;) {
       const int sp = S.sp;
       if (sp == 0 || S.fail) break;
-      const LzFrame f = S.F[sp - 1];
+      LzFrame f = S.F[sp - 1];
       const float worst = S.worst;
       int wb = S.wb, wc = S.wc;
       __syncthreads();   // every thread has the frame before thread 0 rewrites it
+      // a built node: its record.  A stub (feat -2) turns into a lazily split
+      // range: its points (vind order) go to the private scratch first.
+      int bfeat = -3;
+      NfNode nd;
+      if (f.node >= 0) {
+        nd = t.nodes[f.node];
+        bfeat = nd.feat;
+        if (bfeat == -2) {
+          f.begin = nd.c1;
+          f.count = nd.c2 - nd.c1;
+          const float4 lo = t.sbox[2 * f.node], hi = t.sbox[2 * f.node + 1];
+          f.lx = lo.x; f.ly = lo.y; f.lz = lo.z;
+          f.hx = hi.x; f.hy = hi.y; f.hz = hi.z;
+          f.node = -1;
+          for (int j0 = threadIdx.x; j0 < f.count; j0 += kLzT * 4) {
+            float4 ps[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ps[u] = t.vpts[f.begin + min(j0 + u * kLzT, f.count - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int j = f.begin + j0 + u * kLzT;
+              if (j0 + u * kLzT < f.count) {
+                gm.x[j] = ps[u].x; gm.y[j] = ps[u].y; gm.z[j] = ps[u].z; gm.id[j] = __float_as_int(ps[u].w);
+              }
+            }
+          }
+          if (threadIdx.x == 0) {
+            S.F[sp - 1] = f;
+            if (S.prof) S.pa[14] += 1;
+          }
+          __syncthreads();
+          lz_mark(S, 0);
+          continue;
+        }
+      }
+      if (f.node >= 0 && bfeat == -1) {   // a built leaf: its vind range in the tree's points (:1503-1516)
+        if (threadIdx.x < 64) {
+          lz_leaf([&](int i, float& px, float& py, float& pz, int& ip) {
+                    const float4 p = t.vpts[i];
+                    px = p.x; py = p.y; pz = p.z; ip = __float_as_int(p.w);
+                  }, nd.c1, nd.c2, qp.x, qp.y, qp.z, worst, k, kd, kx, count, S.ld, S.lx);
+          const float wk = __shfl(kd, k - 1);
+          if (lane == 0) {
+            S.worst = count < k ? FLT_MAX : wk;
+            S.sp = sp - 1;
+          }
+        }
+        __syncthreads();
+        lz_mark(S, 8);
+        continue;
+      }
+      if (f.node >= 0) {   // a built inner node: searchLevel with its record (:1518-1566)
+        const int feat = bfeat;
+        const float val = feat == 0 ? qp.x : (feat == 1 ? qp.y : qp.z);
+        const float diff1 = val - nd.divlow, diff2 = val - nd.divhigh;
+        const bool first1 = (diff1 + diff2) < 0;
+        if (f.state == 0) {
+          if (threadIdx.x == 0) {
+            if (sp >= kLzStack) {
+              S.fail = 1;
+            } else {
+              S.F[sp - 1].state = 1;
+              LzFrame ch = f;
+              ch.node = first1 ? nd.c1 : nd.c2;
+              ch.state = 0;
+              S.F[sp] = ch;
+              S.sp = sp + 1;
+            }
+          }
+          __syncthreads();
+          continue;
+        }
+        if (f.state == 1) {
+          const float cut_dist = first1 ? (val - nd.divhigh) * (val - nd.divhigh) : (val - nd.divlow) * (val - nd.divlow);
+          const float dst = feat == 0 ? d0 : (feat == 1 ? d1 : d2);
+          const float mind = f.fm + cut_dist - dst;
+          if (feat == 0) d0 = cut_dist;
+          else if (feat == 1) d1 = cut_dist;
+          else d2 = cut_dist;
+          if (threadIdx.x == 0) {
+            S.F[sp - 1].fd = dst;
+            S.F[sp - 1].state = 2;
+            if (mind * 1.0f <= worst) {
+              if (sp >= kLzStack) {
+                S.fail = 1;
+              } else {
+                LzFrame ch = f;
+                ch.node = first1 ? nd.c2 : nd.c1;
+                ch.state = 0;
+                ch.fm = mind;
+                S.F[sp] = ch;
+                S.sp = sp + 1;
+              }
+            }
+          }
+          __syncthreads();
+          continue;
+        }
+        if (feat == 0) d0 = f.fd;   // state 2
+        else if (feat == 1) d1 = f.fd;
+        else d2 = f.fd;
+        if (threadIdx.x == 0) S.sp = sp - 1;
+        __syncthreads();
+        continue;
+      }
+      // a lazily split range
       bool inw = wc > 0 && f.begin >= wb && f.begin + f.count <= wb + wc;
       if (!inw && f.state == 0 && f.count > kNfLeafMax && f.count <= kLzL) {   // enter a subtree that fits LDS
         for (int j0 = threadIdx.x; j0 < f.count; j0 += kLzT * 4) {
@@ -1611,66 +1819,44 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
         if (threadIdx.x == 0) {
           S.wb = wb;
           S.wc = wc;
+          if (S.prof) S.pa[13] += 1;
         }
         __syncthreads();
+        lz_mark(S, 7);
       }
-      LzMem nm;   // the node's storage and its offset there (field selects: a selected struct reference
-                  // would put both in private memory)
-      nm.x = inw ? wm.x : gm.x; nm.y = inw ? wm.y : gm.y; nm.z = inw ? wm.z : gm.z; nm.id = inw ? wm.id : gm.id;
-      nm.ml = inw ? wm.ml : gm.ml; nm.mr = inw ? wm.mr : gm.mr; nm.cz = inw ? wm.cz : gm.cz; nm.cr = inw ? wm.cr : gm.cr;
-      const int off = inw ? wb : 0;
+      // the node's storage: the LDS window (offset wb) or the private scratch;
+      // two inlined copies of each access path, so that the window's get LDS
+      // instructions (a pointer select between the two would make both flat)
       if (f.count <= kNfLeafMax) {   // leaf: candidates below the worst distance read at the leaf (:1503-1516)
         if (threadIdx.x < 64) {
-          for (int bb = f.begin; bb < f.begin + f.count; bb += 64) {
-            const int i = bb + lane;
-            float r = FLT_MAX;
-            int ip = -1;
-            bool cand = false;
-            if (i < f.begin + f.count) {
-              r = 0.f;
-              float diff = qp.x - nm.x[i - off];
-              r += diff * diff;
-              diff = qp.y - nm.y[i - off];
-              r += diff * diff;
-              diff = qp.z - nm.z[i - off];
-              r += diff * diff;
-              ip = nm.id[i - off];
-              cand = r < worst;
-            }
-            unsigned long long mk = __ballot(cand);
-            while (mk) {
-              const int bl = __ffsll((long long)mk) - 1;
-              mk &= mk - 1;
-              const float dn = __shfl(r, bl);
-              const int xn = __shfl(ip, bl);
-              const int pos = __popcll(__ballot(lane < count && kd <= dn));
-              const float ud = __shfl_up(kd, 1);
-              const int ux = __shfl_up(kx, 1);
-              if (pos < k && lane < k) {
-                if (lane == pos) {
-                  kd = dn;
-                  kx = xn;
-                } else if (lane > pos) {
-                  kd = ud;
-                  kx = ux;
-                }
-              }
-              if (count < k) ++count;
-            }
-          }
+          if (inw)
+            lz_leaf([&](int i, float& px, float& py, float& pz, int& ip) {
+                      px = Wn.x[i - wb]; py = Wn.y[i - wb]; pz = Wn.z[i - wb]; ip = Wn.id[i - wb];
+                    }, f.begin, f.begin + f.count, qp.x, qp.y, qp.z, worst, k, kd, kx, count, S.ld, S.lx);
+          else
+            lz_leaf([&](int i, float& px, float& py, float& pz, int& ip) {
+                      px = gm.x[i]; py = gm.y[i]; pz = gm.z[i]; ip = gm.id[i];
+                    }, f.begin, f.begin + f.count, qp.x, qp.y, qp.z, worst, k, kd, kx, count, S.ld, S.lx);
           const float wk = __shfl(kd, k - 1);
           if (lane == 0) {
             S.worst = count < k ? FLT_MAX : wk;
             S.sp = sp - 1;
+            if (S.prof) S.pa[12] += 1;
           }
         }
         __syncthreads();
+        lz_mark(S, 8);
         continue;
       }
       if (f.state == 0) {   // first visit: split the node (divideTree's recursion step)
         int feat, index;
         float cut, dlo, dhi;
-        const bool ok = lz_split(nm, f.begin - off, f, &feat, &cut, &index, &dlo, &dhi, S);
+        const bool ok = inw ? lz_split(wm, f.begin - wb, f, &feat, &cut, &index, &dlo, &dhi, S)
+                            : lz_split(gm, f.begin, f, &feat, &cut, &index, &dlo, &dhi, S);
+        if (S.prof && threadIdx.x == 0) {
+          S.pa[10] += 1;
+          S.pa[11] += f.count;
+        }
         const float val = feat == 0 ? qp.x : (feat == 1 ? qp.y : qp.z);
         const bool first1 = ((val - dlo) + (val - dhi)) < 0;   // searchLevel (:1525-1540)
         if (threadIdx.x == 0) {
@@ -1744,6 +1930,12 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
       if (threadIdx.x == 0) S.sp = sp - 1;
       __syncthreads();
     }
+    lz_mark(S, 9);
+    if (S.prof && threadIdx.x == 0)
+      printf("[lazy] n %d cycles: stubcopy %llu minmax %llu stats %llu hcount %llu scan %llu scatter %llu swap %llu "
+             "window %llu leaf %llu rest %llu | splits %llu split_pts %llu leaves %llu windows %llu stubs %llu\n", n,
+             S.pa[0], S.pa[1], S.pa[2], S.pa[3], S.pa[4], S.pa[5], S.pa[6], S.pa[7], S.pa[8], S.pa[9], S.pa[10],
+             S.pa[11], S.pa[12], S.pa[13], S.pa[14]);
     const int fail = S.fail;
     if (threadIdx.x < 64) {
       if (fail || count < k) {
@@ -1759,24 +1951,36 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(CloudDev c, const float* __res
   }
 }
 
-// the cloud's points in original order (nanoflann's dataset order), SoA
-__global__ __launch_bounds__(256) void k_lz_unsort(CloudDev c, float* __restrict__ X, float* __restrict__ Y,
-                                                   float* __restrict__ Z) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= c.n) return;
-  const float4 p = c.pts[s];
-  const int o = __float_as_int(p.w);
-  X[o] = p.x;
-  Y[o] = p.y;
-  Z[o] = p.z;
-}
-
 // vind starts as the identity (init_vind): the cloud's points in original order
 __global__ __launch_bounds__(256) void k_nf_unsort(const NfBuild* __restrict__ bp) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= bp->n) return;
   const float4 p = bp->sorted[s];
   bp->vpts[__float_as_int(p.w)] = p;
+}
+
+// Partial build: after the top Lmax levels, every node the final map listed
+// (all of level Lmax's children, and the small nodes of the levels above)
+// becomes a stub: feat = -2, its vind range, the box divideTree passes it,
+// and its parent's divlow / divhigh from its points' min / max.
+__global__ __launch_bounds__(256) void k_nf_stub(const NfBuild* __restrict__ bp) {
+  const NfBuild& b = *bp;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b.ctl->nsmall) return;
+  const NfTask e = b.small[i];
+  if (e.node < 0 || e.node >= b.big_ids) {
+    atomicOr(&b.ctl->err, 1);
+    return;
+  }
+  NfNode* nd = b.nodes;
+  nd[e.node].c1 = e.begin;
+  nd[e.node].c2 = e.begin + e.count;
+  nd[e.node].feat = e.count <= kNfLeafMax ? -1 : -2;   // a node of <= leaf_max_size points is a leaf (:992)
+  b.sbox[2 * e.node] = make_float4(e.lo[0], e.lo[1], e.lo[2], 0.f);
+  b.sbox[2 * e.node + 1] = make_float4(e.hi[0], e.hi[1], e.hi[2], 0.f);
+  const float mn[3] = {o2f(e.mm[0]), o2f(e.mm[1]), o2f(e.mm[2])};
+  const float mx[3] = {o2f(e.mm[3]), o2f(e.mm[4]), o2f(e.mm[5])};
+  nf_set_div(nd, e.node, mn, mx);
 }
 
 // diagnostics / tests: the tree as nanoflann would hold it (status[1] = nodes)
@@ -1839,6 +2043,10 @@ void launch_nf_build(hipStream_t s, const NfBuild& hb, const NfBuild* db, int st
     k_nf_pass<2, false><<<G, kNfBT, 0, s>>>(db, L);
   }
   k_nf_map<<<1, 1024, 0, s>>>(db, hb.Lmax);
+  if (hb.sbox) {   // partial: the rest is split lazily by the searches that need it
+    k_nf_stub<<<cdivl(hb.max_small, 256), 256, 0, s>>>(db);
+    return;
+  }
   k_nf_sub<<<hb.max_small, 64 * kNfSubWaves, 0, s>>>(db);
   k_nf_small_global<<<hb.max_small, 64, 0, s>>>(db);
 }
@@ -1854,21 +2062,20 @@ bool launch_nf_resolve_cov(hipStream_t s, const NfTreeDev& t, const CloudDev& c,
   return true;
 }
 
-size_t nf_lazy_bytes(int n, int wgs) { return lz_shared_bytes(n) + (size_t)wgs * lz_wg_bytes(n); }
+size_t nf_lazy_bytes(int n, int wgs) { return (size_t)wgs * lz_wg_bytes(n); }
 
-bool launch_nf_lazy(hipStream_t s, const CloudDev& c, const float4* q, TieList ties, int k, int method, double* cov6,
-                    int* out_idx, float* out_d, void* scratch, int wgs, int* err) {
-  if (k > 64 || wgs < 1) return false;
-  char* base = static_cast<char*>(scratch);
-  float* X = reinterpret_cast<float*>(base);
-  float* Y = reinterpret_cast<float*>(base + lz_al(4 * (size_t)c.n));
-  float* Z = reinterpret_cast<float*>(base + 2 * lz_al(4 * (size_t)c.n));
-  k_lz_unsort<<<cdivl(c.n, 256), 256, 0, s>>>(c, X, Y, Z);
-  char* wg = base + lz_shared_bytes(c.n);
+bool launch_nf_lazy(hipStream_t s, const NfTreeDev& t, const CloudDev& c, const float4* q, TieList ties, int k,
+                    int method, double* cov6, int* out_idx, float* out_d, void* scratch, int wgs, const int* status,
+                    int* err) {
+  if (k > 64 || wgs < 1 || !t.partial) return false;
+  static const int prof = std::getenv("DDLO_LAZY_PROF") != nullptr;   // development: per-phase cycles (printf)
+  char* wg = static_cast<char*>(scratch);
   if (cov6)
-    k_nf_lazy<true><<<wgs, kLzT, 0, s>>>(c, X, Y, Z, q, ties, k, method, cov6, out_idx, out_d, wg, lz_wg_bytes(c.n), err);
+    k_nf_lazy<true><<<wgs, kLzT, 0, s>>>(t, c, q, ties, k, method, cov6, out_idx, out_d, wg, lz_wg_bytes(c.n), status,
+                                         err, prof);
   else
-    k_nf_lazy<false><<<wgs, kLzT, 0, s>>>(c, X, Y, Z, q, ties, k, method, cov6, out_idx, out_d, wg, lz_wg_bytes(c.n), err);
+    k_nf_lazy<false><<<wgs, kLzT, 0, s>>>(t, c, q, ties, k, method, cov6, out_idx, out_d, wg, lz_wg_bytes(c.n), status,
+                                          err, prof);
   return true;
 }
 

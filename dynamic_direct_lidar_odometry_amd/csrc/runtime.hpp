@@ -134,6 +134,8 @@ struct DevBuf {
 struct NfTreeData {
   int n = 0, cap = 0;
   DevBuf vpts, nodes, box, status;   // status: {the build's error bits, node count} (device ints)
+  bool partial = false;              // the top levels only (nftree_build partial_levels): stubs below
+  DevBuf sbox;                       // partial: the stubs' passed-down boxes
   hipEvent_t ready = nullptr;        // recorded after the build on the ctx's aux stream; users wait on it
   NfTreeData() = default;
   NfTreeData(const NfTreeData&) = delete;
@@ -147,6 +149,8 @@ struct NfTreeData {
     t.nodes = nodes.as<NfNode>();
     t.box = box.as<float4>();
     t.n = n;
+    t.partial = partial ? 1 : 0;
+    t.sbox = partial ? sbox.as<float4>() : nullptr;
     return t;
   }
 };
@@ -156,6 +160,7 @@ struct CloudData {
   int n = 0;
   DevBuf pts, keys, perm, inv_perm, box_lo, box_hi, quant, soa, dir;
   std::shared_ptr<NfTreeData> nf;   // nanoflann's tree (tie order), built on first need
+  std::shared_ptr<NfTreeData> nfp;  // its top levels only (the lazy covariance tie search)
   int nlevels = 0;
   int lvl_off[kMaxLevels] = {0};
   int lvl_cnt[kMaxLevels] = {0};
@@ -320,6 +325,7 @@ struct gicp_ctx {
   // tree instead (lazy_heavy: the previous pass listed more than 2 x the
   // lazy kernel's workgroups)
   bool tie_lazy = false;   // DDLO_TIE_LAZY=1 (measured slower than the whole tree so far)
+  int partial_levels = 6;  // big levels of the partial tree the lazy search starts from (DDLO_TIE_PARTIAL_LEVELS)
   bool lazy_heavy = false;
   DevBuf lazy_buf;
   hipEvent_t tie_cnt_ev = nullptr;   // recorded after the count's copy
@@ -375,6 +381,7 @@ inline hipError_t grow(DevBuf& b, size_t bytes, hipStream_t s) {
 // check_finite = false (device clouds known finite): no read-back, and the
 // call returns without waiting for the build.
 inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s);
+inline gicp_status ensure_nftree_partial(gicp_ctx* c, CloudData& cd, hipStream_t s);
 
 // nf_early: start nanoflann's tree of the cloud (ctx's aux stream) as soon
 // as its sorted points exist, beside the rest of the index build -- for a
@@ -438,9 +445,9 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(cd->pts.ensure(sizeof(float4) * npad));
   HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
   launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
-  if (nf_early && c->tie_exact && !(c->tie_lazy && !c->lazy_heavy)) {
+  if (nf_early && c->tie_exact) {
     drain.armed = true;
-    gicp_status st = ensure_nftree(c, *cd, s);
+    gicp_status st = (c->tie_lazy && !c->lazy_heavy) ? ensure_nftree_partial(c, *cd, s) : ensure_nftree(c, *cd, s);
     if (st) return st;
   }
   HIP_TRY(cd->dir.ensure(sizeof(int) * (size_t)fine_dir_ints(N)));
@@ -468,8 +475,9 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
 // Build nanoflann's tree of cd into t on the given stream.  stop >= 0 (the
 // diagnostics entry only) runs that many big levels and nothing after;
 // off (optional, 16 entries) receives the sizes and the scratch offsets.
+// partial_levels >= 0: only that many big levels, then stubs (k_nf_stub).
 inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, NfTreeData& tr, int stop = -1,
-                                long long* off = nullptr) {
+                                long long* off = nullptr, int partial_levels = -1) {
   NfTreeData* t = &tr;
   const int n = cd.n;
   // the cloud is ready on s_in; the build runs on the aux stream
@@ -503,7 +511,9 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
     c->nf_ntask_bucket = -1;
   }
   int Lmax = z.Lmax;
-  if (stop < 0 && !off) {
+  const bool partial = partial_levels >= 0 && stop < 0 && !off;
+  if (partial) Lmax = std::min(z.Lmax, partial_levels);
+  if (stop < 0 && !off && !partial) {
     const auto it = c->nf_hints.find(nbucket);
     if (it != c->nf_hints.end() && it->second.hint > 0) Lmax = std::min(z.Lmax, it->second.hint);
   }
@@ -512,6 +522,8 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   HIP_TRY(t->nodes.ensure(sizeof(NfNode) * (size_t)t->cap));
   HIP_TRY(t->box.ensure(2 * sizeof(float4)));   // root_bbox
   HIP_TRY(t->status.ensure(2 * sizeof(int)));
+  t->partial = partial;
+  if (partial) HIP_TRY(t->sbox.ensure(2 * sizeof(float4) * (size_t)z.big_ids));
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t o_ctl = 0, o_tasks = o_ctl + al(sizeof(NfCtl)),
                o_pend = o_tasks + al(sizeof(NfTask) * (size_t)(z.Lmax + 1) * z.max_task),
@@ -543,6 +555,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   b.tblL = reinterpret_cast<float4*>(u + o_tblL);
   b.tblR = reinterpret_cast<float4*>(u + o_tblR);
   b.quant = cd.quant.as<float>();
+  b.sbox = partial ? t->sbox.as<float4>() : nullptr;
   b.sorted = cd.pts.as<float4>();
   b.n = n;
   b.nbucket = nbucket;
@@ -566,7 +579,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
     launch_nf_build(s, b, db, stop);
     HIP_TRY(hipGetLastError());
   } else {
-    const long long gkey = (long long)nbucket * 64 + Lmax;
+    const long long gkey = ((long long)nbucket * 64 + Lmax) * 2 + (partial ? 1 : 0);
     ++c->nf_clock;
     gicp_ctx::NfGraph* ng = nullptr;
     for (auto& e : c->nf_graphs)
@@ -587,7 +600,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
       }
       hipGraph_t g = nullptr;
       HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      launch_nf_build(s, b, db, -1);
+      launch_nf_build(s, b, db, -1);   // (b.sbox set: the partial build)
       const hipError_t e1 = hipGetLastError();
       const hipError_t e2 = hipStreamEndCapture(s, &g);
       HIP_TRY(e1);
@@ -600,7 +613,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
     ng->last_use = c->nf_clock;
     HIP_TRY(hipGraphLaunch(ng->ge, s));
   }
-  if (stop < 0 && !off) {   // the level counts of this build, for the next one
+  if (stop < 0 && !off && !partial) {   // the level counts of this build, for the next one
     if (!c->nf_ntask_host) {
       HIP_TRY(hipHostMalloc((void**)&c->nf_ntask_host, sizeof(int) * (kNfMaxLevels + 1), hipHostMallocDefault));
       HIP_TRY(hipEventCreateWithFlags(&c->nf_ntask_ev, hipEventDisableTiming));
@@ -630,6 +643,16 @@ inline gicp_status ensure_nftree(gicp_ctx* c, CloudData& cd, hipStream_t s) {
   gicp_status st = nftree_build(c, cd, s, *t);
   if (st) return st;
   cd.nf = t;
+  return GICP_OK;
+}
+
+// the top levels of nanoflann's tree (the lazy covariance tie search), once per cloud
+inline gicp_status ensure_nftree_partial(gicp_ctx* c, CloudData& cd, hipStream_t s) {
+  if (cd.nfp || cd.nf) return GICP_OK;
+  auto t = std::make_shared<NfTreeData>();
+  gicp_status st = nftree_build(c, cd, s, *t, -1, nullptr, c->partial_levels);
+  if (st) return st;
+  cd.nfp = t;
   return GICP_OK;
 }
 
@@ -708,7 +731,7 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   }
   const bool lazy = c->tie_exact && c->tie_lazy && !c->lazy_heavy && !side.cloud->nf;
   if (c->tie_exact) {
-    gicp_status st = lazy ? GICP_OK : ensure_nftree(c, *side.cloud, c->stream);
+    gicp_status st = lazy ? ensure_nftree_partial(c, *side.cloud, c->stream) : ensure_nftree(c, *side.cloud, c->stream);
     if (!st) st = tie_scratch(c, side.cloud->n, c->stream, &tl);
     if (st) return st;
   }
@@ -783,9 +806,11 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
       const int n = side.cloud->n;
       const int wgs = lazy_workgroups(n);
       HIP_TRY(grow(c->lazy_buf, nf_lazy_bytes(n, wgs), c->stream));
+      const NfTreeData& tp = *side.cloud->nfp;
+      HIP_TRY(nftree_join(tp, c->stream));
       if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[4], c->stream));
-      launch_nf_lazy(c->stream, cd, nullptr, tl, k, c->params.regularization, cv->cov6.as<double>(), nullptr, nullptr,
-                     c->lazy_buf.p, wgs, c->nf_err.as<int>());
+      launch_nf_lazy(c->stream, tp.dev(), cd, nullptr, tl, k, c->params.regularization, cv->cov6.as<double>(), nullptr,
+                     nullptr, c->lazy_buf.p, wgs, tp.status.as<int>(), c->nf_err.as<int>());
       if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[5], c->stream));
       c->lazy_wgs_last = wgs;
     } else {
