@@ -122,7 +122,7 @@ const SearchKnobs& search_knobs() {
     v.reuse_rec_eps = env_float("DDLO_REUSE_REC_EPS", 0.05f);
     v.reuse_rec_conv = env_float("DDLO_REUSE_REC_CONV", 10.f);
     v.tie_ab = env_int("DDLO_TIE_AB", 0);
-    v.tie_scan = env_int("DDLO_TIE_SCAN", 3);   // 1 / 2 / 3 / 4 (see AlignJob::tie_scan); 0 = A/B only
+    v.tie_scan = env_int("DDLO_TIE_SCAN", 4);   // 1 / 2 / 3 / 4 (see AlignJob::tie_scan); 0 = A/B only
     return v;
   }();
   return k;

@@ -21,5 +21,6 @@ for leg in cfg2 cfg4 cfg5; do
 done
 DDLO_TRAFFIC_JSON=$O/traffic.json timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+timeout -k 10 300 python -u -m pytest -s -x -v --timeout 300 --timeout-method thread tests/test_gpu_configs.py -k slab > $O/slab_table.log 2>&1 || { echo SLAB_FAIL; tail -20 $O/slab_table.log; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 echo ALL_OK
