@@ -412,10 +412,16 @@ __global__ __launch_bounds__(kNfBT) void k_nf_count(const NfBuild* __restrict__ 
   nf_cut(v.tk, &feat, &cut);
   const int p0 = v.c * kNfCH, p1 = min(p0 + kNfCH, v.tk.count);
   int a = 0, ae = 0;
-  for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-    const float x = coord_at(&b.vpts[v.tk.begin + p], feat);
-    a += x < cut;
-    ae += x <= cut;
+  float xs[kNfPer];   // the chunk's kNfPer loads per thread in flight together
+#pragma unroll
+  for (int j = 0; j < kNfPer; ++j) {
+    const int p = p0 + (int)threadIdx.x + j * kNfBT;
+    xs[j] = p < p1 ? coord_at(&b.vpts[v.tk.begin + p], feat) : NAN;   // NaN: both comparisons false
+  }
+#pragma unroll
+  for (int j = 0; j < kNfPer; ++j) {
+    a += xs[j] < cut;
+    ae += xs[j] <= cut;
   }
   a = block_sum(a, sh);
   ae = block_sum(ae, sh);
@@ -1355,12 +1361,14 @@ __device__ __forceinline__ int lz_scan(int* a, int cnt, LzShared& S, int slot) {
 // The passes below keep kLzU independent loads in flight per thread: one
 // workgroup reads its node from L2 at ~60 GB/s only with ~32 KB in flight
 // (a load-use loop waits a full L2 round trip per element).
-constexpr int kLzU = 16;
+constexpr int kLzU = 8;    // global memory (the LDS window's passes use 2: a short
+                           // instruction stream matters more there, each runs once per query, cold in the cache)
 
 // One Hoare pass of the node at base b (count n) as a rank pairing: the r-th
 // bad element of the zone [zlo, zhi) (ascending) swaps with the r-th good
 // element of [zhi, n) (descending); good = v < cut (pass 1) or v == cut
 // (pass 2).  False on an (impossible) count mismatch.
+template <int kLzU>
 __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi, int n, int feat, float cut, bool pass2, LzShared& S) {
   const int lane = __lane_id(), w = threadIdx.x >> 6;
   const float* V = lz_axis(m, feat) + b;
@@ -1416,7 +1424,7 @@ __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi
   }
   __syncthreads();
   lz_mark(S, 5);
-  constexpr int U = kLzU / 2;
+  constexpr int U = kLzU > 1 ? kLzU / 2 : 1;
   for (int r0 = threadIdx.x; r0 < mz; r0 += kLzT * U) {
     int a[U], c[U];
 #pragma unroll
@@ -1450,6 +1458,7 @@ __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi
 // middleSplit_ + planeSplit of the node f (whole workgroup), in place; the
 // split position and the children's faces along the cut dimension (divlow =
 // the left child's max, divhigh = the right child's min, :1032-1033)
+template <int kLzU>
 __device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f, int* feat_out, float* cut_out,
                                          int* index_out, float* dlo, float* dhi, LzShared& S) {
   const int n = f.count;
@@ -1529,8 +1538,8 @@ __device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f
   }
   __syncthreads();
   lz_mark(S, 2);
-  bool ok = lz_hoare(m, b, 0, lim1, n, feat, cut, false, S);
-  if (ok && lim2 > lim1) ok = lz_hoare(m, b, lim1, lim2, n, feat, cut, true, S);   // pass 2 (:1128-1142)
+  bool ok = lz_hoare<kLzU>(m, b, 0, lim1, n, feat, cut, false, S);
+  if (ok && lim2 > lim1) ok = lz_hoare<kLzU>(m, b, lim1, lim2, n, feat, cut, true, S);   // pass 2 (:1128-1142)
   const int index = nf_index(n, lim1, lim2);
   *feat_out = feat;
   *cut_out = cut;
@@ -1703,20 +1712,31 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(NfTreeDev t, CloudDev c, const
           f.lx = lo.x; f.ly = lo.y; f.lz = lo.z;
           f.hx = hi.x; f.hy = hi.y; f.hz = hi.z;
           f.node = -1;
+          // a stub that fits LDS goes straight into the window, a larger one
+          // into the private scratch (at its own positions)
+          const bool to_win = f.count <= kLzL;
           for (int j0 = threadIdx.x; j0 < f.count; j0 += kLzT * 4) {
             float4 ps[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) ps[u] = t.vpts[f.begin + min(j0 + u * kLzT, f.count - 1)];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const int j = f.begin + j0 + u * kLzT;
-              if (j0 + u * kLzT < f.count) {
-                gm.x[j] = ps[u].x; gm.y[j] = ps[u].y; gm.z[j] = ps[u].z; gm.id[j] = __float_as_int(ps[u].w);
+              const int jl = j0 + u * kLzT, j = f.begin + jl;
+              if (jl < f.count) {
+                if (to_win) {
+                  Wn.x[jl] = ps[u].x; Wn.y[jl] = ps[u].y; Wn.z[jl] = ps[u].z; Wn.id[jl] = __float_as_int(ps[u].w);
+                } else {
+                  gm.x[j] = ps[u].x; gm.y[j] = ps[u].y; gm.z[j] = ps[u].z; gm.id[j] = __float_as_int(ps[u].w);
+                }
               }
             }
           }
           if (threadIdx.x == 0) {
             S.F[sp - 1] = f;
+            if (to_win) {
+              S.wb = f.begin;
+              S.wc = f.count;
+            }
             if (S.prof) S.pa[14] += 1;
           }
           __syncthreads();
@@ -1851,8 +1871,8 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(NfTreeDev t, CloudDev c, const
       if (f.state == 0) {   // first visit: split the node (divideTree's recursion step)
         int feat, index;
         float cut, dlo, dhi;
-        const bool ok = inw ? lz_split(wm, f.begin - wb, f, &feat, &cut, &index, &dlo, &dhi, S)
-                            : lz_split(gm, f.begin, f, &feat, &cut, &index, &dlo, &dhi, S);
+        const bool ok = inw ? lz_split<2>(wm, f.begin - wb, f, &feat, &cut, &index, &dlo, &dhi, S)
+                            : lz_split<kLzU>(gm, f.begin, f, &feat, &cut, &index, &dlo, &dhi, S);
         if (S.prof && threadIdx.x == 0) {
           S.pa[10] += 1;
           S.pa[11] += f.count;
