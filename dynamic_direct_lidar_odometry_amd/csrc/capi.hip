@@ -617,8 +617,8 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   {
     const char* v = std::getenv("DDLO_TIE_EXACT");   // A/B of the tie resolution (default: nanoflann's order)
     c->tie_exact = !(v && *v == '0');
-    const char* lz = std::getenv("DDLO_TIE_LAZY");   // 1: covariance ties through per-query lazy searches (A/B)
-    c->tie_lazy = lz && *lz == '1';
+    const char* lz = std::getenv("DDLO_TIE_LAZY");   // 0: covariance ties through the whole tree (A/B)
+    c->tie_lazy = !(lz && *lz == '0');
     const char* pl = std::getenv("DDLO_TIE_PARTIAL_LEVELS");
     if (pl) c->partial_levels = std::max(0, std::atoi(pl));
   }

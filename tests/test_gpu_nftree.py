@@ -47,9 +47,10 @@ def test_device_tree_raycast_scan():
     assert O.same_tree(c.nftree(SOURCE), O.tree(src)) is None
 
 
+@pytest.mark.parametrize("lazy", ["1", "0"])
 @pytest.mark.parametrize("spacing", [0.25, 1.5])
 @pytest.mark.parametrize("k", [10, 20])
-def test_covariance_ties_lattice(k, spacing):
+def test_covariance_ties_lattice(k, spacing, lazy, monkeypatch):
     """An integer lattice: nearly every point's k-th neighbour distance is tied.
     At 1.5 m spacing a 64-point Morton group spans more than the 5 m split
     extent, so the groups are searched as sub-ranges whose traversals re-scan
@@ -58,6 +59,7 @@ def test_covariance_ties_lattice(k, spacing):
     lat = np.stack(np.meshgrid(np.arange(24), np.arange(24), np.arange(5), indexing="ij"), -1).reshape(-1, 3)
     pts = (lat.astype(np.float32) * np.float32(spacing))
     pts = pts + (np.arange(len(pts)) % 7 == 0)[:, None].astype(np.float32) * np.float32(0.04 * spacing)   # some irregularity
+    monkeypatch.setenv("DDLO_TIE_LAZY", lazy)   # the lazy search on the partial tree, or the whole tree
     c = P.Context(0)
     c.set_params(P.default_params(k_correspondences=k))
     c.set_target(pts)
