@@ -47,7 +47,7 @@ METRIC = "GICP iters/sec + ms/scan, 131k-pt source → 500k-pt submap; pose Δ v
 HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same workload
 # (tools/pmc_traffic.sh -> tools/pmc_traffic.py), committed per round
-TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r03_traffic.json"))
+TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r04_traffic.json"))
 
 
 def pmc_traffic():

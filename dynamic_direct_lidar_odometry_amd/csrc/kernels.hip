@@ -380,7 +380,7 @@ struct KnnVisitor : VisitStats {
       // points count for td: an inactive lane (another sub-range of a split
       // group) re-scans leaves whose points it may already keep.
       if (active && key < wk && d <= tight) insert(key);
-      else if (active) td = fminf(td, d);
+      else td = fminf(td, active ? d : INFINITY);   // (a select: a second branch cost 24 VGPRs in k_covariances2)
     }
   }
   __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
@@ -531,7 +531,7 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
       const float d = dist2(this->qx, this->qy, this->qz, L->px[h0 + j], L->py[h0 + j], L->pz[h0 + j]);
       const unsigned long long key = dkey(d, start + h0 + j);
       if (this->active && key < wk_both() && d <= this->tight) this->insert(key);
-      else if (this->active) this->td = fminf(this->td, d);   // active lanes only (see KnnVisitor::process)
+      else this->td = fminf(this->td, this->active ? d : INFINITY);   // active lanes only (see KnnVisitor::process)
     }
     exchange();
   }
