@@ -1312,11 +1312,39 @@ struct LzWin {
 
 __device__ __forceinline__ float* lz_axis(const LzMem& m, int f) { return f == 0 ? m.x : (f == 1 ? m.y : m.z); }
 
+// Wave folds with DPP moves (no LDS round trip per step): quad xor 1 / 2,
+// half-row and row mirrors, then row_bcast15 / 31 fold the rows into lane
+// 63, which is read back.  OP: 0 min, 1 max, 2 integer sum.
+template <int OP>
+__device__ __forceinline__ int lz_dpp_step(int x, int c) {
+  int r;
+  switch (c) {
+    case 0: r = __builtin_amdgcn_update_dpp(x, x, 0xb1, 0xf, 0xf, false); break;    // quad_perm [1,0,3,2]
+    case 1: r = __builtin_amdgcn_update_dpp(x, x, 0x4e, 0xf, 0xf, false); break;    // quad_perm [2,3,0,1]
+    case 2: r = __builtin_amdgcn_update_dpp(x, x, 0x141, 0xf, 0xf, false); break;   // row_half_mirror
+    case 3: r = __builtin_amdgcn_update_dpp(x, x, 0x140, 0xf, 0xf, false); break;   // row_mirror
+    case 4: r = __builtin_amdgcn_update_dpp(OP == 2 ? 0 : x, x, 0x142, 0xa, 0xf, false); break;   // row_bcast15
+    default: r = __builtin_amdgcn_update_dpp(OP == 2 ? 0 : x, x, 0x143, 0xc, 0xf, false); break; // row_bcast31
+  }
+  if (OP == 2) return x + r;
+  const float a = __int_as_float(x), b = __int_as_float(r);
+  return __float_as_int(OP == 1 ? fmaxf(a, b) : fminf(a, b));
+}
+template <int OP>
+__device__ __forceinline__ int lz_wave_fold(int x) {
+#pragma unroll
+  for (int c = 0; c < 6; ++c) x = lz_dpp_step<OP>(x, c);
+  return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ float lz_wmin(float v) { return __int_as_float(lz_wave_fold<0>(__float_as_int(v))); }
+__device__ __forceinline__ float lz_wmax(float v) { return __int_as_float(lz_wave_fold<1>(__float_as_int(v))); }
+__device__ __forceinline__ int lz_wsum(int v) { return lz_wave_fold<2>(v); }
+
 // min (v[0..2]) and max (v[3..5]) over the workgroup; every thread gets the result
 __device__ __forceinline__ void lz_reduce6(float v[6], LzShared& S) {
   const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int a = 0; a < 6; ++a) v[a] = wred(v[a], a >= 3);
+  for (int a = 0; a < 6; ++a) v[a] = a >= 3 ? lz_wmax(v[a]) : lz_wmin(v[a]);
   if (__lane_id() == 0)
 #pragma unroll
     for (int a = 0; a < 6; ++a) S.rf[w][a] = v[a];
@@ -1514,12 +1542,10 @@ __device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f
       if (x > cut) mgt = fminf(mgt, x);
     }
   }
-  for (int d = 32; d >= 1; d >>= 1) {
-    lt += __shfl_xor(lt, d);
-    le += __shfl_xor(le, d);
-    mlt = fmaxf(mlt, __shfl_xor(mlt, d));
-    mgt = fminf(mgt, __shfl_xor(mgt, d));
-  }
+  lt = lz_wsum(lt);
+  le = lz_wsum(le);
+  mlt = lz_wmax(mlt);
+  mgt = lz_wmin(mgt);
   const int w = threadIdx.x >> 6;
   if (__lane_id() == 0) {
     S.ri[w][0] = lt;
@@ -1589,8 +1615,8 @@ __device__ __forceinline__ void lz_leaf(LOAD load, int b0, int b1, float qx, flo
   // candidate ranks (own position p = 64 h + lane) and the entries' shifts
   int rk[2] = {0, 0};
   int sh_e = 0;   // candidates strictly closer than this lane's entry
-  for (int j = 0; j < count; ++j) {
-    const float e = __shfl(kd, j);
+  for (int j = 0; j < count; ++j) {   // (uniform lanes: v_readlane, not an LDS permute per step)
+    const float e = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kd), j));
     rk[0] += e <= r[0];
     rk[1] += e <= r[1];
   }
@@ -1600,7 +1626,7 @@ __device__ __forceinline__ void lz_leaf(LOAD load, int b0, int b1, float qx, flo
     while (mk) {
       const int bl = __ffsll((long long)mk) - 1;
       mk &= mk - 1;
-      const float rc = __shfl(r[h2], bl);
+      const float rc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r[h2]), bl));
       const int pc = 64 * h2 + bl;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {

@@ -325,7 +325,7 @@ struct gicp_ctx {
   // tree instead (lazy_heavy: the previous pass listed more than 2 x the
   // lazy kernel's workgroups)
   bool tie_lazy = true;    // DDLO_TIE_LAZY=0: the whole tree for covariance ties too
-  int partial_levels = 5;  // big levels of the partial tree the lazy search starts from (DDLO_TIE_PARTIAL_LEVELS)
+  int partial_levels = 3;  // big levels of the partial tree the lazy search starts from (DDLO_TIE_PARTIAL_LEVELS)
   bool lazy_heavy = false;
   DevBuf lazy_buf;
   hipEvent_t tie_cnt_ev = nullptr;   // recorded after the count's copy
