@@ -257,6 +257,26 @@ def sharded_leg(dist, rank, world, local_rank, args):
         c.close()
         out_leg["pose_delta_vs_1gpu"] = {"trans_m": float(np.abs(out[:3, 3] - ref[:3, 3]).max()),
                                          "rot_rad": rot_err(out, ref)}
+        if not args.no_cpu:
+            # the OpenMP oracle on the same cfg4 align, at the cfg3 sweep's fastest thread count
+            from oracle import oracle as O
+            nthr = getattr(args, "cpu_best_threads", 16)
+            g = O.Gicp(src, sub, O.as_params(params), threads=nthr)
+            g.set_covariances(0, scov)
+            g.set_covariances(1, tcov)
+            g.align(guess)
+            times = []
+            oo = None
+            for _ in range(3):
+                c0 = time.perf_counter()
+                oo, _ = g.align(guess)
+                times.append(time.perf_counter() - c0)
+            cms = 1e3 * float(np.median(times))
+            out_leg["cpu_oracle"] = {"ms_per_scan": round(cms, 3), "threads": nthr, "kind": "port",
+                                     "sample": "median of 3 full cfg4 aligns after 1 warm-up, oracle/cpu_ref.cpp",
+                                     "speedup_gpu_vs_cpu": round(cms / out_leg["ms_per_scan"], 2),
+                                     "pose_delta_vs_cpu": {"trans_m": float(np.abs(out[:3, 3] - oo[:3, 3]).max()),
+                                                           "rot_rad": rot_err(out, oo)}}
     return out_leg
 
 
@@ -684,6 +704,7 @@ def main():
                 oout, ores = oo, ro
         best_t = min(by_threads, key=by_threads.get)
         cpu_ms = by_threads[best_t]
+        args.cpu_best_threads = best_t   # the cfg4 leg's oracle timing uses the same thread count
         result["cpu_baseline"] = {"value": round(cpu_ms, 3), "unit": "ms/scan", "cores": best_t, "kind": "port",
                                   "sample": f"median of {args.cpu_runs} full S2M aligns of the same cfg3 problem after "
                                             f"{args.cpu_warmup} warm-ups ({ores.iterations_run} iters each), OpenMP "
