@@ -329,6 +329,18 @@ struct KnnVisitor : VisitStats {
       if (s < k) t |= dist(s) == dist(s - 1);
     return t;
   }
+  // the slot j of the one equal-distance pair (j, j + 1) among the kept k, -1
+  // if there are more (or three at one distance)
+  __device__ __forceinline__ int single_pair() const {
+    int cnt = 0, j = -1;
+#pragma unroll
+    for (int s = 1; s < KCAP; ++s)
+      if (s < k && dist(s) == dist(s - 1)) {
+        ++cnt;
+        j = s - 1;
+      }
+    return cnt == 1 ? j : -1;
+  }
   __device__ __forceinline__ void update_worst() {
     if constexpr (EXACT) {
       wk = K[KCAP - 1];
@@ -395,16 +407,29 @@ struct KnnVisitor : VisitStats {
 };
 
 // Mean and biased covariance of the kept neighbours in their order
-// (nano_gicp_impl.hpp:392-399), regularised, stored as sym6.  The neighbour
-// points are loaded four at a time (compiler barriers between the groups):
-// with all KCAP loads hoisted, k = 20 held 20 float4s live and spilled.
+// (nano_gicp_impl.hpp:392-399), regularised.  The neighbour points are loaded
+// four at a time (compiler barriers between the groups): with all KCAP loads
+// hoisted, k = 20 held 20 float4s live and spilled.  swap >= 0: slots swap and
+// swap + 1 exchanged (cov_order_free).
 template <int KCAP, class KL>
-__device__ __forceinline__ void cov_from_keys(const CloudDev& c, const KL& K, int k, int method, double* o) {
+__device__ __forceinline__ void cov_compute(const CloudDev& c, const KL& K, int k, int method, int swap, double* out) {
+  unsigned long long ka = 0, kb = 0;   // the swapped pair's keys (slot selects, no runtime index into the list)
+  if (swap >= 0) {
+#pragma unroll
+    for (int s = 0; s < KCAP; ++s) {
+      if (s == swap) ka = K[s];
+      if (s == swap + 1) kb = K[s];
+    }
+  }
+  auto slot_pos = [&](int s) -> int {
+    const unsigned long long v = swap < 0 ? K[s] : (s == swap ? kb : (s == swap + 1 ? ka : K[s]));
+    return (int)(unsigned)v;
+  };
   double mx = 0, my = 0, mz = 0;
 #pragma unroll
   for (int s = 0; s < KCAP; ++s) {
     if (s < k) {
-      const float4 p = ldg4(c.pts, (int)(unsigned)K[s]);
+      const float4 p = ldg4(c.pts, slot_pos(s));
       mx += (double)p.x;
       my += (double)p.y;
       mz += (double)p.z;
@@ -418,7 +443,7 @@ __device__ __forceinline__ void cov_from_keys(const CloudDev& c, const KL& K, in
 #pragma unroll
   for (int s = 0; s < KCAP; ++s) {
     if (s < k) {
-      const float4 p = ldg4(c.pts, (int)(unsigned)K[s]);
+      const float4 p = ldg4(c.pts, slot_pos(s));
       const double d0 = (double)p.x - mx, d1 = (double)p.y - my, d2 = (double)p.z - mz;
       C[0] += d0 * d0; C[1] += d0 * d1; C[2] += d0 * d2;
       C[3] += d1 * d0; C[4] += d1 * d1; C[5] += d1 * d2;
@@ -427,9 +452,27 @@ __device__ __forceinline__ void cov_from_keys(const CloudDev& c, const KL& K, in
     if ((s & 3) == 3) asm volatile("" ::: "memory");
   }
   for (int e = 0; e < 9; ++e) C[e] /= k;
-  double out[6];
   regularize(C, method, out);
+}
+template <int KCAP, class KL>
+__device__ __forceinline__ void cov_from_keys(const CloudDev& c, const KL& K, int k, int method, double* o) {
+  double out[6];
+  cov_compute<KCAP>(c, K, k, method, -1, out);
   for (int e = 0; e < 6; ++e) o[e] = out[e];
+}
+
+// An inner tie whose order cannot change the result: the covariance with the
+// tied neighbours j and j + 1 exchanged (the other order nanoflann's walk may
+// have met them in) equals the one stored from the Morton order, bit for bit
+// after the regularisation.  Then the stored result is nanoflann's whatever
+// its order, and the query needs no re-run.
+template <int KCAP, class KL>
+__device__ __forceinline__ bool cov_order_free(const CloudDev& c, const KL& K, int k, int method, int j, const double* stored) {
+  double out[6];
+  cov_compute<KCAP>(c, K, k, method, j, out);
+  bool same = true;
+  for (int e = 0; e < 6; ++e) same = same && __double_as_longlong(out[e]) == __double_as_longlong(stored[e]);
+  return same;
 }
 
 // Seed a kNN visitor with the leaves [s0, s1] and then run the full traversal.
@@ -490,8 +533,12 @@ __global__ __launch_bounds__(256) void k_covariances(CloudDev c, int k, int meth
     // a tie at the k-th distance changes the set; one inside the k changes the
     // summation order, which the eigen-decomposition of a degenerate
     // (isotropic) neighbourhood turns into a different regularized covariance
-    if (ties.list && (vis.outside_min() == vis.kth_dist() || vis.inner_tie())) ties.push(i);
+    const bool kth_tie = vis.outside_min() == vis.kth_dist(), inner = vis.inner_tie();
     cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
+    if (ties.list && (kth_tie || inner)) {
+      const int j = kth_tie ? -1 : vis.single_pair();
+      if (j < 0 || !cov_order_free<KCAP>(c, vis.K, k, method, j, cov6 + 6 * (size_t)i)) ties.push(i);
+    }
   }
 }
 
@@ -601,8 +648,16 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
     }
     vis.merge_halves();
     if (!vis.active || lane_id() >= 32) continue;
-    if (ties.list && (vis.td == vis.kth_dist() || vis.inner_tie())) ties.push(i);
+    const bool kth_tie = vis.td == vis.kth_dist(), inner = vis.inner_tie();
     cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
+    if (ties.list && (kth_tie || inner)) {   // rare: a tie whose order matters is re-run (nftree.hip)
+      bool push = true;
+      if constexpr (KCAP <= 16) {   // (k = 20: a second covariance spills at the 3-wave budget; re-run them all)
+        const int j = kth_tie ? -1 : vis.single_pair();
+        if (j >= 0) push = !cov_order_free<KCAP>(c, vis.K, k, method, j, cov6 + 6 * (size_t)i);
+      }
+      if (push) ties.push(i);
+    }
   }
 }
 template __global__ void k_covariances2<10, true, 3>(CloudDev, int, int, double*, TieList);

@@ -103,6 +103,21 @@ def test_lazy_tie_search_matches_oracle(name, levels, monkeypatch):
         assert len(bad) == 0, f"round {rnd}: {len(bad)} mismatches, e.g. {bad[:8]}"
 
 
+def test_covariances_bit_identical_to_oracle():
+    """The device covariances equal the oracle's bit for bit on ray-cast scans
+    (k = 10, PLANE): the same neighbour order (nanoflann's, ties included:
+    re-run on the partial tree, or kept from the Morton order when exchanging
+    the tied pair gives the same regularised matrix), the same fp64 summation
+    order and the same Jacobi sequence."""
+    frames = scene.loop_sequence(64, 2048, 0, 2, device=0)[0]
+    c = P.Context(0)
+    c.set_params(P.default_params(k_correspondences=10))
+    for pts in frames:
+        c.set_target(pts)
+        c.compute_covariances(TARGET)
+        np.testing.assert_array_equal(c.get_covariances(TARGET), O.covariances(pts, 10, threads=16))
+
+
 def test_knn_ties_random_duplicates():
     rng = np.random.default_rng(3)
     base = (rng.standard_normal((2000, 3)) * 3).astype(np.float32)
