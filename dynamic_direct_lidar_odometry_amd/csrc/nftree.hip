@@ -1396,6 +1396,36 @@ constexpr int kLzU = 8;    // global memory (the LDS window's passes use 2: a sh
 // bad element of the zone [zlo, zhi) (ascending) swaps with the r-th good
 // element of [zhi, n) (descending); good = v < cut (pass 1) or v == cut
 // (pass 2).  False on an (impossible) count mismatch.
+// Every element of A[b, b + n) through f (order-free reductions, global
+// memory): 16-byte loads for the body from the first 16-byte boundary (the
+// scratch arrays are 256-byte aligned), U of them in flight per thread, the
+// head and tail element by element.  Absent elements are NaN (every
+// comparison false; fminf / fmaxf ignore them).
+template <int U, class F>
+__device__ __forceinline__ void lz_vec_each(const float* A, int b, int n, F f) {
+  const int h = min(n, (4 - (b & 3)) & 3);
+  const int nv = (n - h) >> 2;
+  const int t0 = h + 4 * nv;
+  if ((int)threadIdx.x < h) f(A[b + threadIdx.x]);
+  if ((int)threadIdx.x < n - t0) f(A[b + t0 + threadIdx.x]);
+  const float4* V = reinterpret_cast<const float4*>(A + b + h);
+  for (int i0 = threadIdx.x; i0 < nv; i0 += kLzT * U) {
+    float4 q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * kLzT;
+      q[u] = i < nv ? V[i] : make_float4(NAN, NAN, NAN, NAN);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f(q[u].x);
+      f(q[u].y);
+      f(q[u].z);
+      f(q[u].w);
+    }
+  }
+}
+
 template <int kLzU>
 __device__ __forceinline__ bool lz_hoare(const LzMem& m, int b, int zlo, int zhi, int n, int feat, float cut, bool pass2, LzShared& S) {
   const int lane = __lane_id(), w = threadIdx.x >> 6;
@@ -1500,20 +1530,26 @@ __device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f
   const bool c0 = hi[0] - lo[0] > (1 - EPS) * max_span, c1 = hi[1] - lo[1] > (1 - EPS) * max_span,
              c2 = hi[2] - lo[2] > (1 - EPS) * max_span;
   float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int i0 = threadIdx.x; i0 < n; i0 += kLzT * kLzU) {
-    float xs[kLzU], ys[kLzU], zs[kLzU];
+  if constexpr (kLzU >= 4) {   // global memory: 16-byte loads, one pass per measured dimension
+    if (c0) lz_vec_each<4>(m.x, b, n, [&](float x) { v[0] = fminf(v[0], x); v[3] = fmaxf(v[3], x); });
+    if (c1) lz_vec_each<4>(m.y, b, n, [&](float x) { v[1] = fminf(v[1], x); v[4] = fmaxf(v[4], x); });
+    if (c2) lz_vec_each<4>(m.z, b, n, [&](float x) { v[2] = fminf(v[2], x); v[5] = fmaxf(v[5], x); });
+  } else {
+    for (int i0 = threadIdx.x; i0 < n; i0 += kLzT * kLzU) {
+      float xs[kLzU], ys[kLzU], zs[kLzU];
 #pragma unroll
-    for (int u = 0; u < kLzU; ++u) {   // NaN for absent elements: fminf / fmaxf ignore it
-      const int i = i0 + u * kLzT;
-      const bool in = i < n;
-      xs[u] = c0 && in ? m.x[b + i] : NAN;
-      ys[u] = c1 && in ? m.y[b + i] : NAN;
-      zs[u] = c2 && in ? m.z[b + i] : NAN;
-    }
+      for (int u = 0; u < kLzU; ++u) {   // NaN for absent elements: fminf / fmaxf ignore it
+        const int i = i0 + u * kLzT;
+        const bool in = i < n;
+        xs[u] = c0 && in ? m.x[b + i] : NAN;
+        ys[u] = c1 && in ? m.y[b + i] : NAN;
+        zs[u] = c2 && in ? m.z[b + i] : NAN;
+      }
 #pragma unroll
-    for (int u = 0; u < kLzU; ++u) {
-      v[0] = fminf(v[0], xs[u]); v[1] = fminf(v[1], ys[u]); v[2] = fminf(v[2], zs[u]);
-      v[3] = fmaxf(v[3], xs[u]); v[4] = fmaxf(v[4], ys[u]); v[5] = fmaxf(v[5], zs[u]);
+      for (int u = 0; u < kLzU; ++u) {
+        v[0] = fminf(v[0], xs[u]); v[1] = fminf(v[1], ys[u]); v[2] = fminf(v[2], zs[u]);
+        v[3] = fmaxf(v[3], xs[u]); v[4] = fmaxf(v[4], ys[u]); v[5] = fmaxf(v[5], zs[u]);
+      }
     }
   }
   lz_reduce6(v, S);
@@ -1526,20 +1562,24 @@ __device__ __forceinline__ bool lz_split(const LzMem& m, int b, const LzFrame& f
   const float* V = lz_axis(m, feat) + b;
   int lt = 0, le = 0;
   float mlt = -INFINITY, mgt = INFINITY;
-  for (int i0 = threadIdx.x; i0 < n; i0 += kLzT * kLzU) {
-    float xs[kLzU];
+  auto stat = [&](float x) {   // NaN: every comparison false
+    lt += x < cut;
+    le += x <= cut;
+    if (x < cut) mlt = fmaxf(mlt, x);
+    if (x > cut) mgt = fminf(mgt, x);
+  };
+  if constexpr (kLzU >= 4) {
+    lz_vec_each<4>(lz_axis(m, feat), b, n, stat);
+  } else {
+    for (int i0 = threadIdx.x; i0 < n; i0 += kLzT * kLzU) {
+      float xs[kLzU];
 #pragma unroll
-    for (int u = 0; u < kLzU; ++u) {
-      const int i = i0 + u * kLzT;
-      xs[u] = i < n ? V[i] : NAN;   // NaN: every comparison false
-    }
+      for (int u = 0; u < kLzU; ++u) {
+        const int i = i0 + u * kLzT;
+        xs[u] = i < n ? V[i] : NAN;
+      }
 #pragma unroll
-    for (int u = 0; u < kLzU; ++u) {
-      const float x = xs[u];
-      lt += x < cut;
-      le += x <= cut;
-      if (x < cut) mlt = fmaxf(mlt, x);
-      if (x > cut) mgt = fminf(mgt, x);
+      for (int u = 0; u < kLzU; ++u) stat(xs[u]);
     }
   }
   lt = lz_wsum(lt);
