@@ -68,3 +68,20 @@ def test_batch_single_frame_and_errors(frames):
         P.s2s_batch(frames[:3], p, nstreams=0)
     with pytest.raises(P.GicpError):
         P.s2s_batch([frames[0], np.zeros((0, 3), np.float32)], p)
+
+
+def test_batch_nonfinite_frame_leaves_pool_clean(frames):
+    """A frame with a NaN fails the batch with GICP_ENONFINITE (the reference
+    would feed NaNs to its kd-tree); the buffers its worker had started
+    filling (index, the early nanoflann tree on the second stream) go back to
+    the device pool only after that stream has drained, so a batch run right
+    after, on the same pool, is bit-identical to the chained single-ctx run."""
+    p = P.default_params(**S2S)
+    bad = [f.copy() for f in frames]
+    bad[3][17] = np.nan
+    with pytest.raises(P.GicpError) as e:
+        P.s2s_batch(bad, p, nstreams=3)
+    assert e.value.status == 8
+    bp, _ = P.s2s_batch(frames, p, nstreams=3)
+    sp, _ = sequential(frames, p)
+    assert np.array_equal(bp, sp)
