@@ -621,6 +621,10 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
     c->tie_lazy = !(lz && *lz == '0');
     const char* pl = std::getenv("DDLO_TIE_PARTIAL_LEVELS");
     if (pl) c->partial_levels = std::max(0, std::atoi(pl));
+    // DDLO_NF_OWN_STREAM=1: every ctx builds its trees on its own stream, the
+    // partial tree gated on the tie count (the S2S batch's workers always do)
+    const char* os = std::getenv("DDLO_NF_OWN_STREAM");
+    c->nf_same_stream = os && *os == '1';
   }
   *out = c.release();
   return GICP_OK;
@@ -1352,6 +1356,10 @@ gicp_status gicp_s2s_batch(int device, const gicp_params* p, const float* const*
   for (int w = 0; w < nthreads; ++w) {
     gicp_status s = gicp_ctx_create(device, &ctxs[w]);
     if (!s) s = gicp_set_params(ctxs[w], p);
+    if (!s) {
+      const char* os = std::getenv("DDLO_NF_OWN_STREAM");   // 0: the second stream (A/B)
+      ctxs[w]->nf_same_stream = !(os && *os == '0');
+    }
     if (s) {
       const std::string why = g_last_error;
       for (auto* c : ctxs)

@@ -256,6 +256,7 @@ struct NfBuild {
   const float* quant;      // the cloud's bbox: min [0..2], max [4..6]
   float4* sbox;            // partial build: the passed-down box of every unsplit node (indexed by node id)
   const float4* sorted;    // the cloud's Morton-sorted points (w = original index bits)
+  const int* gate;         // optional: a count (the tied-query list's) that, when 0, makes every kernel a no-op
   int n, Lmax, max_task, max_pend, max_small, max_chunks;
   int nbucket;             // the size the grids are sized for (>= n): one captured graph per bucket
   int big_ids;             // node ids [0, big_ids) for the big levels; a small task of vind range

@@ -199,7 +199,16 @@ __device__ __forceinline__ void task_chunk_sums(const int* cnt, const NfTask& tk
 
 // ---------------------------------------------------------------------------
 // build kernels
+
+// a gated build (NfBuild::gate, the tied-query count) does nothing when no
+// query is tied: one scalar load per block
+__device__ __forceinline__ bool nf_gated_off(const NfBuild* __restrict__ bp) {
+  const int* g = bp->gate;
+  return g && *g == 0;
+}
+
 __global__ void k_nf_init(const NfBuild* __restrict__ bp) {
+  if (nf_gated_off(bp)) return;
   const NfBuild& b = *bp;
   if (threadIdx.x == 0) {
     NfCtl* ctl = b.ctl;
@@ -236,6 +245,7 @@ __global__ void k_nf_init(const NfBuild* __restrict__ bp) {
 // nodes > kNfT points become big tasks (their chunks listed), the others
 // small tasks; the final call lists every remaining node as small.
 __global__ __launch_bounds__(1024) void k_nf_map(const NfBuild* __restrict__ bp, int L) {
+  if (nf_gated_off(bp)) return;
   const NfBuild& b = *bp;
   __shared__ int sh[17];
   __shared__ int s_big, s_small, s_ch, s_small0;
@@ -403,6 +413,7 @@ __device__ __forceinline__ bool map_level_block(const NfBuild& b, int L, TaskVie
 
 // middleSplit_'s cut per task; #{v < cut} and #{v <= cut} per chunk
 __global__ __launch_bounds__(kNfBT) void k_nf_count(const NfBuild* __restrict__ bp, int L) {
+  if (nf_gated_off(bp)) return;
   const NfBuild& b = *bp;
   __shared__ int sh[17];
   TaskView v;
@@ -442,6 +453,7 @@ __global__ __launch_bounds__(kNfBT) void k_nf_count(const NfBuild* __restrict__ 
 // slot; else (APPLY) overwrite each misplaced position with its partner.
 template <int PASS, bool TABLE>
 __global__ __launch_bounds__(kNfBT) void k_nf_pass(const NfBuild* __restrict__ bp, int L) {
+  if (nf_gated_off(bp)) return;
   const NfBuild& b = *bp;
   __shared__ int sh[17];
   TaskView v;
@@ -994,6 +1006,7 @@ __device__ void group_depth(const NfBuild& b, SubLds& S, int cur, int nq, int ba
 }
 
 __global__ __launch_bounds__(64 * kNfSubWaves) void k_nf_sub(const NfBuild* __restrict__ bp) {
+  if (nf_gated_off(bp)) return;
   const NfBuild& b = *bp;
   __shared__ SubLds S;   // ~157 KB: one workgroup per CU
   if ((int)blockIdx.x >= b.ctl->nsmall) return;
@@ -1061,6 +1074,7 @@ struct NfGStack {
   NfSubNode e[kNfStack];
 };
 __global__ __launch_bounds__(64) void k_nf_small_global(const NfBuild* __restrict__ bp) {
+  if (nf_gated_off(bp)) return;
   const NfBuild& b = *bp;
   __shared__ NfGStack S;
   if ((int)blockIdx.x >= b.ctl->nsmall) return;
@@ -2039,6 +2053,7 @@ __global__ __launch_bounds__(kLzT) void k_nf_lazy(NfTreeDev t, CloudDev c, const
 
 // vind starts as the identity (init_vind): the cloud's points in original order
 __global__ __launch_bounds__(256) void k_nf_unsort(const NfBuild* __restrict__ bp) {
+  if (nf_gated_off(bp)) return;
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= bp->n) return;
   const float4 p = bp->sorted[s];
@@ -2050,6 +2065,7 @@ __global__ __launch_bounds__(256) void k_nf_unsort(const NfBuild* __restrict__ b
 // becomes a stub: feat = -2, its vind range, the box divideTree passes it,
 // and its parent's divlow / divhigh from its points' min / max.
 __global__ __launch_bounds__(256) void k_nf_stub(const NfBuild* __restrict__ bp) {
+  if (nf_gated_off(bp)) return;
   const NfBuild& b = *bp;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= b.ctl->nsmall) return;

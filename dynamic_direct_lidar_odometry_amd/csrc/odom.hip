@@ -461,7 +461,7 @@ struct ddlo_odom {
   float* median_pin = nullptr;   // pinned: the median range of the current scan
   // DDLO_ODOM_TIMING=1: host wall time per phase, printed at destroy (development)
   bool timing = false;
-  double t_phase[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double t_phase[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // [8] device drain before a frame, [9] H2D call
   long frames = 0;
   // state
   bool initialized = false;   // ddlo_initialized_
@@ -723,9 +723,10 @@ gicp_status ddlo_odom_destroy(ddlo_odom* o) {
   (void)hipStreamSynchronize(o->s2m->stream);
   (void)hipStreamSynchronize(o->s);
   if (o->timing && o->frames > 0) {
-    static const char* names[8] = {"upload", "preprocess", "cloud", "s2s_align", "submap", "s2m_align", "keyframe", "total"};
+    static const char* names[10] = {"upload", "preprocess", "cloud", "s2s_align", "submap", "s2m_align", "keyframe",
+                                    "total", "drain_before", "h2d_call"};
     std::fprintf(stderr, "[odom timing] %ld frames, us/frame:", o->frames);
-    for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %s %.1f", names[k], 1e6 * o->t_phase[k] / o->frames);
+    for (int k = 0; k < 10; ++k) std::fprintf(stderr, " %s %.1f", names[k], 1e6 * o->t_phase[k] / o->frames);
     std::fprintf(stderr, "\n");
   }
   o->keyframes.clear();
@@ -763,6 +764,11 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
     }
   }
   using clk = std::chrono::steady_clock;
+  if (o->timing) {   // work of the previous frame still queued on any stream (aux included)
+    const auto td = clk::now();
+    (void)hipDeviceSynchronize();
+    o->t_phase[8] += std::chrono::duration<double>(clk::now() - td).count();
+  }
   auto t0 = clk::now(), tl = t0;
   auto mark = [&](int k) {
     if (!o->timing) return;
@@ -776,6 +782,7 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
   const int N = (int)n;
   HIP_TRY(o->up.ensure((n - 1) * stride + 12));
   HIP_TRY(hipMemcpyAsync(o->up.p, xyz, (n - 1) * stride + 12, hipMemcpyHostToDevice, o->s));
+  if (o->timing) o->t_phase[9] += std::chrono::duration<double>(clk::now() - t0).count();
   HIP_TRY(o->a.ensure(sizeof(float4) * n));
   launch_pack4(o->s, o->up.as<unsigned char>(), stride, N, o->a.as<float4>());
   mark(0);

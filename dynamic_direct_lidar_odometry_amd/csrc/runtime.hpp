@@ -327,6 +327,15 @@ struct gicp_ctx {
   bool tie_lazy = true;    // DDLO_TIE_LAZY=0: the whole tree for covariance ties too
   int partial_levels = 3;  // big levels of the partial tree the lazy search starts from (DDLO_TIE_PARTIAL_LEVELS)
   bool lazy_heavy = false;
+  // nanoflann's tree on the ctx's own stream, not beside it (gicp_s2s_batch's
+  // workers: the other workers fill the device, and a second stream per
+  // worker shares the 4 hardware queues with them -- 0.44 against 0.55 ms per
+  // pair at 4 workers, tools/batch_streams.py)
+  bool nf_same_stream = false;
+  // ... and then builds the partial tree after the covariance kernel, into
+  // this ctx-owned tree, gated on the tie count (no work for a scan without
+  // ties, about half of cfg 5's)
+  std::unique_ptr<NfTreeData> nf_gated;
   DevBuf lazy_buf;
   hipEvent_t tie_cnt_ev = nullptr;   // recorded after the count's copy
   bool tie_cnt_pending = false;
@@ -445,7 +454,9 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(cd->pts.ensure(sizeof(float4) * npad));
   HIP_TRY(cd->inv_perm.ensure(sizeof(int) * n));
   launch_gather(s, c->raw_pts.as<float4>(), cd->perm.as<int>(), N, npad, cd->pts.as<float4>(), cd->inv_perm.as<int>());
-  if (nf_early && c->tie_exact) {
+  // (a ctx building its trees on its own stream gates the partial tree on the
+  // covariance pass's tie count instead: compute_cov)
+  if (nf_early && c->tie_exact && !(c->nf_same_stream && c->tie_lazy && !c->lazy_heavy)) {
     drain.armed = true;
     gicp_status st = (c->tie_lazy && !c->lazy_heavy) ? ensure_nftree_partial(c, *cd, s) : ensure_nftree(c, *cd, s);
     if (st) return st;
@@ -477,11 +488,12 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
 // off (optional, 16 entries) receives the sizes and the scratch offsets.
 // partial_levels >= 0: only that many big levels, then stubs (k_nf_stub).
 inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, NfTreeData& tr, int stop = -1,
-                                long long* off = nullptr, int partial_levels = -1) {
+                                long long* off = nullptr, int partial_levels = -1, const int* gate = nullptr) {
   NfTreeData* t = &tr;
   const int n = cd.n;
   // the cloud is ready on s_in; the build runs on the aux stream
-  static const bool same_stream = std::getenv("DDLO_NF_SAME_STREAM") != nullptr;   // A/B, diagnostics
+  static const bool same_env = std::getenv("DDLO_NF_SAME_STREAM") != nullptr;   // A/B, diagnostics
+  const bool same_stream = same_env || c->nf_same_stream;
   const hipStream_t s = same_stream ? s_in : c->aux_stream;
   if (!same_stream) {
     HIP_TRY(hipEventRecord(c->aux_ev, s_in));
@@ -557,6 +569,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   b.quant = cd.quant.as<float>();
   b.sbox = partial ? t->sbox.as<float4>() : nullptr;
   b.sorted = cd.pts.as<float4>();
+  b.gate = gate;
   b.n = n;
   b.nbucket = nbucket;
   b.Lmax = Lmax;
@@ -575,7 +588,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   NfBuild* db = c->nf_desc.as<NfBuild>();
   launch_nf_set_desc(s, b, db);   // by value as a kernel argument: no host buffer has to outlive the call
   static const bool no_graph = std::getenv("DDLO_NF_NO_GRAPH") != nullptr;   // A/B, diagnostics
-  if (stop >= 0 || no_graph || same_stream) {
+  if (stop >= 0 || no_graph || same_env) {
     launch_nf_build(s, b, db, stop);
     HIP_TRY(hipGetLastError());
   } else {
@@ -730,8 +743,11 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     c->tie_cnt_pending = false;
   }
   const bool lazy = c->tie_exact && c->tie_lazy && !c->lazy_heavy && !side.cloud->nf;
+  const bool gated = lazy && c->nf_same_stream && !side.cloud->nfp;
   if (c->tie_exact) {
-    gicp_status st = lazy ? ensure_nftree_partial(c, *side.cloud, c->stream) : ensure_nftree(c, *side.cloud, c->stream);
+    gicp_status st = gated ? GICP_OK
+                     : lazy ? ensure_nftree_partial(c, *side.cloud, c->stream)
+                            : ensure_nftree(c, *side.cloud, c->stream);
     if (!st) st = tie_scratch(c, side.cloud->n, c->stream, &tl);
     if (st) return st;
   }
@@ -806,7 +822,12 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
       const int n = side.cloud->n;
       const int wgs = lazy_workgroups(n);
       HIP_TRY(grow(c->lazy_buf, nf_lazy_bytes(n, wgs), c->stream));
-      const NfTreeData& tp = *side.cloud->nfp;
+      if (gated) {   // after the covariance kernel, on the stream: no work when no query is tied
+        if (!c->nf_gated) c->nf_gated = std::make_unique<NfTreeData>();
+        gicp_status st = nftree_build(c, *side.cloud, c->stream, *c->nf_gated, -1, nullptr, c->partial_levels, tl.count);
+        if (st) return st;
+      }
+      const NfTreeData& tp = gated ? *c->nf_gated : *side.cloud->nfp;
       HIP_TRY(nftree_join(tp, c->stream));
       if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[4], c->stream));
       launch_nf_lazy(c->stream, tp.dev(), cd, nullptr, tl, k, c->params.regularization, cv->cov6.as<double>(), nullptr,

@@ -85,3 +85,19 @@ def test_batch_nonfinite_frame_leaves_pool_clean(frames):
     bp, _ = P.s2s_batch(frames, p, nstreams=3)
     sp, _ = sequential(frames, p)
     assert np.array_equal(bp, sp)
+
+def test_batch_gated_tree_equals_chained_single_ctx():
+    """cfg 5's 64x2048 frames, about half of whose scans have tied k = 10
+    neighbourhoods (tools/gpu_tiecount.sh): the batch workers build the
+    partial tree after the covariance kernel, gated on the tie count, on their
+    own stream; the single ctx builds it beside the kernel on its second
+    stream. Same covariances, so bit-identical poses."""
+    fr, _ = scene.loop_sequence(64, 2048, 0, 9, device=0)
+    p = P.default_params(k_correspondences=10, max_correspondence_distance=1.0, max_iterations=32,
+                         transformation_epsilon=0.01)
+    bp, br = P.s2s_batch(fr, p, nstreams=3)
+    sp, sr = sequential(fr, p)
+    assert np.array_equal(bp, sp)
+    for t in range(1, len(fr)):
+        assert br[t].iterations_run == sr[t].iterations_run
+        assert br[t].num_correspondences == sr[t].num_correspondences
