@@ -596,14 +596,14 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   auto c = std::make_unique<gicp_ctx>();
   c->device = device;
   gicp_default_params(&c->params);
-  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+  HIP_TRY(stream_pool().acquire(&c->stream));
+  HIP_TRY(stream_pool().acquire(&c->aux_stream));
   HIP_TRY(hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming));
-  HIP_TRY(hipHostMalloc((void**)&c->job_host, sizeof(AlignJob), hipHostMallocMapped));
-  HIP_TRY(hipHostMalloc((void**)&c->state_host, 2 * sizeof(AlignState), hipHostMallocMapped));
+  HIP_TRY(pinned_pool().alloc((void**)&c->job_host, sizeof(AlignJob), hipHostMallocMapped));
+  HIP_TRY(pinned_pool().alloc((void**)&c->state_host, 2 * sizeof(AlignState), hipHostMallocMapped));
   HIP_TRY(hipHostGetDevicePointer((void**)&c->job_host_dev, c->job_host, 0));
   HIP_TRY(hipHostGetDevicePointer((void**)&c->state_host_dev, c->state_host, 0));
-  HIP_TRY(hipHostMalloc((void**)&c->flag_host, sizeof(int) * 4, hipHostMallocDefault));
+  HIP_TRY(pinned_pool().alloc((void**)&c->flag_host, sizeof(int) * 4, hipHostMallocDefault));
   HIP_TRY(c->job_dev.ensure(sizeof(AlignJob)));
   HIP_TRY(c->state_dev.ensure(sizeof(AlignState)));
   std::memset(c->state_host, 0, 2 * sizeof(AlignState));
@@ -644,20 +644,20 @@ gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   for (auto e : c->chunk_ev) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
-  if (c->job_host) (void)hipHostFree(c->job_host);
-  if (c->state_host) (void)hipHostFree(c->state_host);
-  if (c->flag_host) (void)hipHostFree(c->flag_host);
-  if (c->nf_err_host) (void)hipHostFree(c->nf_err_host);
+  pinned_pool().release(c->job_host, sizeof(AlignJob), hipHostMallocMapped);
+  pinned_pool().release(c->state_host, 2 * sizeof(AlignState), hipHostMallocMapped);
+  pinned_pool().release(c->flag_host, sizeof(int) * 4, hipHostMallocDefault);
+  pinned_pool().release(c->nf_err_host, 2 * sizeof(int), hipHostMallocDefault);
   if (c->tie_cnt_ev) (void)hipEventDestroy(c->tie_cnt_ev);
   c->src = Side();
   c->tgt = Side();
-  (void)hipStreamDestroy(c->stream);
   (void)hipStreamSynchronize(c->aux_stream);
   for (auto& e : c->nf_graphs)
     if (e.ge) (void)hipGraphExecDestroy(e.ge);
-  if (c->nf_ntask_host) (void)hipHostFree(c->nf_ntask_host);
+  pinned_pool().release(c->nf_ntask_host, sizeof(int) * (kNfMaxLevels + 1), hipHostMallocDefault);
   if (c->nf_ntask_ev) (void)hipEventDestroy(c->nf_ntask_ev);
-  (void)hipStreamDestroy(c->aux_stream);
+  stream_pool().release(c->device, c->aux_stream);   // (both synchronized above)
+  stream_pool().release(c->device, c->stream);
   (void)hipEventDestroy(c->aux_ev);
   delete c;
   return GICP_OK;

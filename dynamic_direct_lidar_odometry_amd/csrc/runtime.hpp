@@ -97,6 +97,71 @@ inline DevicePool& device_pool() {
   return *pool;
 }
 
+// HIP streams are recycled, not destroyed: a context made after others were
+// destroyed gets their streams (and hardware queues) back instead of new
+// ones.  The S2S batch in a fresh process: 0.42 ms per pair with recycling,
+// 0.46-0.47 without; after 10 contexts made and destroyed it still runs at
+// ~0.59-0.64 either way (cause not found: not the streams, not the pinned
+// blocks; tools/batch_leg_alone.py).  A released stream is idle (its owner
+// synchronized it); the last released is handed out first.
+struct StreamPool {
+  std::mutex m;
+  std::vector<std::pair<int, hipStream_t>> free_streams;
+  hipError_t acquire(hipStream_t* s) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+      std::lock_guard<std::mutex> lk(m);
+      for (size_t i = free_streams.size(); i-- > 0;)
+        if (free_streams[i].first == dev) {
+          *s = free_streams[i].second;
+          free_streams.erase(free_streams.begin() + (long)i);
+          return hipSuccess;
+        }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  }
+  void release(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(m);
+    free_streams.emplace_back(dev, s);
+  }
+};
+inline StreamPool& stream_pool() {
+  static StreamPool* pool = new StreamPool();  // never destroyed: streams live until exit
+  return *pool;
+}
+
+// Pinned host blocks of the contexts (job / state descriptors the device
+// reads, read-back flags), recycled like the streams: freed to this list at
+// context destruction and handed out again by (size, flags)
+struct PinnedPool {
+  std::mutex m;
+  std::multimap<std::pair<size_t, unsigned>, void*> free_blocks;
+  hipError_t alloc(void** p, size_t bytes, unsigned flags) {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      auto it = free_blocks.find({bytes, flags});
+      if (it != free_blocks.end()) {
+        *p = it->second;
+        free_blocks.erase(it);
+        std::memset(*p, 0, bytes);   // no state of the previous owner
+        return hipSuccess;
+      }
+    }
+    return hipHostMalloc(p, bytes, flags);
+  }
+  void release(void* p, size_t bytes, unsigned flags) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(m);
+    free_blocks.insert({{bytes, flags}, p});
+  }
+};
+inline PinnedPool& pinned_pool() {
+  static PinnedPool* pool = new PinnedPool();  // never destroyed: blocks live until exit
+  return *pool;
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -628,7 +693,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   }
   if (stop < 0 && !off && !partial) {   // the level counts of this build, for the next one
     if (!c->nf_ntask_host) {
-      HIP_TRY(hipHostMalloc((void**)&c->nf_ntask_host, sizeof(int) * (kNfMaxLevels + 1), hipHostMallocDefault));
+      HIP_TRY(pinned_pool().alloc((void**)&c->nf_ntask_host, sizeof(int) * (kNfMaxLevels + 1), hipHostMallocDefault));
       HIP_TRY(hipEventCreateWithFlags(&c->nf_ntask_ev, hipEventDisableTiming));
     }
     HIP_TRY(hipMemcpyAsync(c->nf_ntask_host, b.ctl->ntask, sizeof(int) * (kNfMaxLevels + 1), hipMemcpyDeviceToHost, s));
@@ -674,7 +739,7 @@ inline gicp_status tie_scratch(gicp_ctx* c, int n, hipStream_t s, TieList* tl) {
   // a point is listed at most twice (the task-based kNN, then the lane-per-query kernel for its group)
   HIP_TRY(grow(c->tie_buf, sizeof(int) * (2 * (size_t)n + 64), s));
   HIP_TRY(c->nf_err.ensure(sizeof(int)));
-  if (!c->nf_err_host) HIP_TRY(hipHostMalloc((void**)&c->nf_err_host, 2 * sizeof(int), hipHostMallocDefault));
+  if (!c->nf_err_host) HIP_TRY(pinned_pool().alloc((void**)&c->nf_err_host, 2 * sizeof(int), hipHostMallocDefault));
   if (!c->nf_err_pending) {
     HIP_TRY(hipMemsetAsync(c->nf_err.p, 0, sizeof(int), s));
     c->nf_err_pending = true;

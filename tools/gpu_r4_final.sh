@@ -10,6 +10,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 python3 tools/profile_summary.py $O/prof_bench run > $O/bench_summary.md
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_cfg5 -o run -- python3 tools/legs.py cfg5 24 > $O/prof_cfg5.log 2>&1 || { echo PROF5_FAIL; tail -20 $O/prof_cfg5.log; exit 1; }
 python3 tools/profile_summary.py $O/prof_cfg5 run > $O/cfg5_summary.md
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_batch -o run -- python3 tools/batch_prof.py 1 > $O/prof_batch.log 2>&1 || { echo PROFB_FAIL; tail -20 $O/prof_batch.log; exit 1; }
+python3 tools/profile_summary.py $O/prof_batch run > $O/batch_summary.md
 timeout -k 10 120 python -u tools/time_cov.py > $O/time_cov.log 2>&1 || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 cat $O/time_cov.log
