@@ -551,8 +551,9 @@ def main():
                     help="cfg4 ownership: interleaved source groups (replicated target) or source-balanced slabs")
     ap.add_argument("--no-batch", action="store_true", help="skip the frame-parallel S2S cfg5 leg")
     ap.add_argument("--batch-frames", type=int, default=1000, help="cfg 5 sequence length (unique frames)")
-    ap.add_argument("--batch-streams", type=int, default=4,
-                    help="frame-parallel S2S workers (one ctx + stream pair each); 4 = the hardware queues per process")
+    ap.add_argument("--batch-streams", type=int, default=3,
+                    help="frame-parallel S2S workers (one ctx each); inside this process 3 measured best (0.47 ms/pair "
+                         "against 0.60 at 4 or 6; a fresh process prefers 4, DESIGN.md §5)")
     ap.add_argument("--no-gn", action="store_true", help="skip the cfg2 S2S 20-GN-iteration leg")
     ap.add_argument("--gn-steps", type=int, default=10)
     ap.add_argument("--no-odom", action="store_true", help="skip the cfg5 odometry-driver (S2M chain) leg")
