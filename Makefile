@@ -8,7 +8,7 @@ PKG := dynamic_direct_lidar_odometry_amd
 CSRC := $(PKG)/csrc
 LIBDIR := $(PKG)/_lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
-OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/nftree.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o $(LIBDIR)/segment.o
+OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/nftree.o $(LIBDIR)/cellgrid.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o $(LIBDIR)/segment.o
 
 all: lib oracle facade raycast
 
@@ -26,7 +26,11 @@ $(LIBDIR)/nftree.o: $(CSRC)/nftree.hip $(CSRC)/nftree.hpp $(CSRC)/cov_math.hpp $
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/runtime.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h
+$(LIBDIR)/cellgrid.o: $(CSRC)/cellgrid.hip $(CSRC)/cellgrid.hpp $(CSRC)/search.hpp $(CSRC)/gicp_types.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/runtime.hpp $(CSRC)/cellgrid.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

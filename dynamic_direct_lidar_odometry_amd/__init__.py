@@ -79,6 +79,31 @@ class GicpResult(C.Structure):
     ]
 
 
+class GicpGridInfo(C.Structure):
+    _fields_ = [
+        ("built", C.c_int32),
+        ("build_ms", C.c_float),
+        ("cell_size", C.c_float),
+        ("bytes", C.c_int64),
+        ("coarse_cells", C.c_int64),
+        ("band_cells", C.c_int64),
+        ("nomatch_cells", C.c_int64),
+        ("overflow_cells", C.c_int64),
+        ("level_cells", C.c_int64 * 4),
+        ("fine_cells", C.c_int64),
+        ("fallback_fine", C.c_int64),
+        ("entries", C.c_int64),
+    ]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["level_cells"] = list(self.level_cells)
+        return d
+
+
+GRID_OFF, GRID_AUTO, GRID_ON = 0, 1, 2
+
+
 def lib_path() -> str:
     # DDLO_GICP_LIB: an alternative in-tree build of the same library (A/B runs)
     return os.environ.get("DDLO_GICP_LIB") or os.path.join(_HERE, "_lib", "libddlo_gicp.so")
@@ -136,6 +161,9 @@ def load():
         "gicp_set_tie_order": (I, [P, I]),
         "gicp_debug_nftree": (I, [P, I, P, P, P, S, C.POINTER(S)]),
         "gicp_debug_nfbuild": (I, [P, I, I, P, P, P, P, S]),
+        "gicp_set_target_grid": (I, [P, I]),
+        "gicp_get_target_grid_info": (I, [P, C.POINTER(GicpGridInfo)]),
+        "gicp_get_lookup_stats": (I, [P, C.POINTER(C.c_int64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -345,6 +373,21 @@ class Context:
         d = np.zeros((len(q), k), np.float32)
         self._check(self.L.gicp_knn_target(self.h, _ptr(q), len(q), stride, k, _ptr(idx), _ptr(d)))
         return idx, d
+
+    def set_target_grid(self, mode=GRID_AUTO):
+        """Candidate cells of the target (gicp_set_target_grid): GRID_OFF / GRID_AUTO / GRID_ON."""
+        self._check(self.L.gicp_set_target_grid(self.h, int(mode)))
+
+    def grid_info(self) -> dict:
+        info = GicpGridInfo()
+        self._check(self.L.gicp_get_target_grid_info(self.h, C.byref(info)))
+        return info.as_dict()
+
+    def lookup_walk_groups(self) -> int:
+        """16-query sub-groups the last align left to the walk (summed over its iterations)."""
+        v = C.c_int64(0)
+        self._check(self.L.gicp_get_lookup_stats(self.h, C.byref(v)))
+        return int(v.value)
 
     def set_tie_order(self, nanoflann_order=True):
         """Exact distance ties in nanoflann's traversal order (default) or by Morton position."""

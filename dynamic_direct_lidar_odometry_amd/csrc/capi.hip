@@ -33,6 +33,7 @@
 #include "gicp_types.hpp"
 #include "launch.hpp"
 #include "runtime.hpp"
+#include "cellgrid.hpp"
 
 
 namespace {
@@ -150,6 +151,314 @@ struct SearchLayout {
   }
 };
 
+// the search bound of an align: nextafter(float(max_corr^2), +inf) (AlignJob::cap2)
+float search_cap2(const gicp_params& p) {
+  const double r = p.max_correspondence_distance;
+  float f = (float)(r * r);
+  if (!std::isfinite(f)) f = FLT_MAX;
+  return std::nextafter(f, INFINITY);
+}
+
+// The target's candidate cells answer this ctx's searches (same bound)
+bool grid_active(const gicp_ctx* c) {
+  if (!c->grid_mode || !c->tgt.cloud || !search_uses_tasks()) return false;
+  const auto& g = c->tgt.cloud->grid;
+  return g && g->ok && g->cap2 == search_cap2(c->params);
+}
+
+// byte layout of ctx->fb (the lookup's walk list) for ns source points
+struct FbLayout {
+  size_t ctr, list, mask, total;
+  int seg_cap;
+  explicit FbLayout(int ns) {
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    seg_cap = (ns + 15) / 16 + 1;
+    ctr = 0;
+    list = al(sizeof(unsigned) * (kFbSegs + 1) * 32);   // + the align's total
+    mask = list + al(sizeof(int) * (size_t)kFbSegs * seg_cap);
+    total = mask + al(sizeof(unsigned short) * (size_t)seg_cap);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Candidate cells of a target (cellgrid.hip): coarse cells of
+// kGridCell metres over the target's box plus the bound's reach, split up to
+// 3 times where lists are longer than kGridListMax points.
+constexpr double kGridCell = 0.4;
+constexpr double kGridMaxReach = 4.0;     // bounds beyond this: cells farther than it use the walk
+constexpr int kGridListMax = 24;
+constexpr int kGridListCap = 256;         // finest level: longer lists are not stored (the walk)
+constexpr long kGridMaxCells = 48L << 20; // coarse cells (the directory is 4 B per cell)
+
+gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_ptr<CellGridData>* out) {
+  hipStream_t s = c->stream;
+  auto g = std::make_shared<CellGridData>();
+  g->cap2 = cap2;
+  *out = g;
+  float q[8];
+  HIP_TRY(hipMemcpyAsync(q, cd.quant.p, sizeof(float) * 7, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const double S = kGridCell;
+  const double capm = std::sqrt((double)cap2) * (1.0 + 1e-5) + 1e-6;
+  const double reach = std::min(capm, kGridMaxReach);
+  const int r = (int)std::ceil(reach / S) + 1;
+  const double M = (r + 1) * S;   // the box: the target's bbox plus M on every side
+  double lo[3], ext[3];
+  long dims[3];
+  double amax = 0.0;
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = (double)q[a] - M;
+    ext[a] = (double)q[4 + a] - (double)q[a] + 2 * M;
+    dims[a] = (long)std::ceil(ext[a] / S) + 1;
+    amax = std::max({amax, std::fabs((double)q[a]), std::fabs((double)q[4 + a])});
+  }
+  const long ncells = dims[0] * dims[1] * dims[2];
+  if (ncells > kGridMaxCells || !std::isfinite(ext[0] + ext[1] + ext[2])) return GICP_OK;   // not built: the walk
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  struct EvGuard {
+    hipEvent_t a, b;
+    ~EvGuard() {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+    }
+  } evg{e0, e1};
+  HIP_TRY(hipEventRecord(e0, s));
+  CgBuild b{};
+  b.tgt = cd.dev();
+  // the build's geometry is the lookup's fp32 origin and scale, exactly
+  b.fox = (float)lo[0]; b.foy = (float)lo[1]; b.foz = (float)lo[2];
+  b.inv_s = (float)(1.0 / S);
+  b.ox = b.fox; b.oy = b.foy; b.oz = b.foz;
+  b.s = 1.0 / (double)b.inv_s;
+  b.nx = (int)dims[0]; b.ny = (int)dims[1]; b.nz = (int)dims[2];
+  b.r = r;
+  // the lookup maps a query to its cell in fp32: |error| <~ 3 ulp of the
+  // coordinate; every box is widened by delta to cover it
+  b.delta = 1e-4 + 4e-6 * (amax + M + S);
+  b.capm = capm;
+  b.nomatch_dist = (r - 1) * S - 1e-3;
+  b.lmax = kGridListMax;
+  b.lcap = kGridListCap;
+  const bool outside_nomatch = capm <= b.nomatch_dist;
+  // scratch
+  const long nbx = (dims[0] + 3) / 4, nby = (dims[1] + 3) / 4, nbz = (dims[2] + 3) / 4;
+  const long nblocked = nbx * nby * nbz * 64;
+  DevBuf occ, tmp, flags, ctr, band, dnum, cub_tmp, centers, cnn, cnd, db_buf;
+  HIP_TRY(occ.ensure((size_t)ncells));
+  HIP_TRY(tmp.ensure((size_t)ncells));
+  HIP_TRY(flags.ensure((size_t)std::max(nblocked, ncells)));
+  HIP_TRY(ctr.ensure(sizeof(unsigned) * kCgCtrWords));
+  HIP_TRY(band.ensure(sizeof(int) * (size_t)ncells));
+  HIP_TRY(dnum.ensure(sizeof(int) * 8));
+  HIP_TRY(db_buf.ensure(sizeof(CgBuild)));
+  HIP_TRY(g->dir.ensure(sizeof(unsigned) * (size_t)ncells));
+  b.occ = occ.as<unsigned char>();
+  b.tmp = tmp.as<unsigned char>();
+  b.dir = g->dir.as<unsigned>();
+  b.band = band.as<int>();
+  b.ctr = ctr.as<unsigned>();
+  CgBuild* db = db_buf.as<CgBuild>();
+  auto upload = [&]() -> hipError_t { return hipMemcpyAsync(db, &b, sizeof(CgBuild), hipMemcpyHostToDevice, s); };
+  HIP_TRY(upload());
+  HIP_TRY(hipMemsetAsync(occ.p, 0, (size_t)ncells, s));
+  HIP_TRY(hipMemsetAsync(ctr.p, 0, sizeof(unsigned) * kCgCtrWords, s));
+  launch_cg_occ(s, db, cd.n, ncells);
+  launch_cg_dilate(s, db, 0, b.occ, b.tmp, ncells);
+  launch_cg_dilate(s, db, 1, b.tmp, b.occ, ncells);
+  launch_cg_dilate(s, db, 2, b.occ, b.tmp, ncells);   // band = tmp
+  launch_cg_dir_fill(s, b.dir, b.tmp, ncells, outside_nomatch ? kCgNoMatch : kCgFallback);
+  launch_cg_band_flags(s, db, b.tmp, flags.as<unsigned char>(), nblocked);
+  HIP_TRY(hipGetLastError());
+  // band cells in blocked order (selected blocked ids; k_cg_centers turns them into cell ids)
+  auto select = [&](const unsigned char* fl, long n, int* outp, int* nsel) -> gicp_status {
+    size_t tb = 0;
+    hipcub::CountingInputIterator<int> it(0);
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, fl, outp, dnum.as<int>(), (int)n, s));
+    HIP_TRY(cub_tmp.ensure(std::max<size_t>(tb, 256)));
+    tb = cub_tmp.bytes;
+    HIP_TRY(hipcub::DeviceSelect::Flagged(cub_tmp.p, tb, it, fl, outp, dnum.as<int>(), (int)n, s));
+    HIP_TRY(hipMemcpyAsync(c->flag_host, dnum.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *nsel = *c->flag_host;
+    return GICP_OK;
+  };
+  int nband = 0;
+  gicp_status st = select(flags.as<unsigned char>(), nblocked, b.band, &nband);
+  if (st) return st;
+  g->info.coarse_cells = ncells;
+  g->info.band_cells = nband;
+  g->info.cell_size = (float)S;
+  // level-0 lists
+  DevBuf hdr[4], pool[4], cmax[4], sband[4], sparent[4], fin_sel[4], fl_final, fl_next;
+  int nfin[4] = {0, 0, 0, 0}, nslot[4] = {0, 0, 0, 0};
+  if (nband > 0) {
+    HIP_TRY(centers.ensure(sizeof(float4) * (size_t)nband));
+    HIP_TRY(cnn.ensure(sizeof(int) * (size_t)nband));
+    HIP_TRY(cnd.ensure(sizeof(float) * (size_t)nband));
+    b.centers = centers.as<float4>();
+    b.cnn = cnn.as<int>();
+    b.cnd = cnd.as<float>();
+    HIP_TRY(upload());
+    launch_cg_centers(s, db, nband);
+    if (!launch_knn_query(s, b.tgt, b.centers, nband, 1, b.cnn, b.cnd, TieList{nullptr, nullptr}))
+      return fail(GICP_EINVAL, "candidate cells: nearest-point pass");
+    HIP_TRY(hdr[0].ensure(sizeof(uint2) * (size_t)nband));
+    HIP_TRY(fl_final.ensure((size_t)nband));
+    HIP_TRY(fl_next.ensure((size_t)nband));
+    nslot[0] = nband;
+  }
+  std::vector<unsigned> counters(kCgCtrWords);
+  auto read_counters = [&]() -> gicp_status {
+    HIP_TRY(hipMemcpyAsync(counters.data(), ctr.p, sizeof(unsigned) * kCgCtrWords, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return GICP_OK;
+  };
+  for (int l = 0; l <= kCgMaxLevel && nslot[l] > 0; ++l) {
+    const long nf = 1L << (3 * l);
+    // the level's lists: pools sized from the parent level, doubled on overflow
+    // (a wave's chunks leave at most kCgChunk unused entries per shard range)
+    size_t used_above = 0;
+    if (l > 0)
+      for (int k = 0; k < kCgShardsHost; ++k) used_above += counters[(kCgCounters + (l - 1) * kCgShardsHost + k) * 32];
+    size_t pcap = l == 0 ? (size_t)nband * 64 + (1u << 23) : 3 * used_above + (size_t)nslot[l] * nf * 4 + (1u << 23);
+    for (int attempt = 0;; ++attempt) {
+      pcap = std::min<size_t>(pcap, 0xfff00000u);
+      HIP_TRY(pool[l].ensure(sizeof(unsigned) * pcap));
+      b.lv[l].pool = pool[l].as<unsigned>();
+      b.lv[l].pool_cap = (unsigned)(pcap / kCgShardsHost * kCgShardsHost);
+      if (l > 0) {
+        HIP_TRY(hdr[l].ensure(sizeof(uint2) * (size_t)nslot[l] * nf));
+        b.lv[l].hdr = hdr[l].as<uint2>();
+      } else {
+        b.lv[0].hdr = hdr[0].as<uint2>();
+      }
+      HIP_TRY(upload());
+      HIP_TRY(hipMemsetAsync(ctr.as<unsigned>() + (kCgCounters + l * kCgShardsHost) * 32, 0,
+                             sizeof(unsigned) * kCgShardsHost * 32, s));
+      HIP_TRY(hipMemsetAsync(ctr.as<unsigned>() + kCtrPoolFull * 32, 0, sizeof(unsigned), s));
+      if (l == 0) launch_cg_coarse(s, db, nband);
+      else launch_cg_refine(s, db, l, nslot[l]);
+      HIP_TRY(hipGetLastError());
+      st = read_counters();
+      if (st) return st;
+      if (!counters[kCtrPoolFull * 32]) break;
+      if (attempt >= 4 || pcap >= 0xfff00000u) return fail(GICP_ENOMEM, "candidate cells: list pool overflow");
+      pcap *= 2;
+    }
+    // decisions: final at this level, or split once more
+    HIP_TRY(fl_final.ensure((size_t)nslot[l]));
+    HIP_TRY(fl_next.ensure((size_t)nslot[l]));
+    launch_cg_decide(s, db, l, nslot[l], fl_final.as<unsigned char>(), fl_next.as<unsigned char>());
+    HIP_TRY(fin_sel[l].ensure(sizeof(int) * (size_t)nslot[l]));
+    st = select(fl_final.as<unsigned char>(), nslot[l], fin_sel[l].as<int>(), &nfin[l]);
+    if (st) return st;
+    if (l < kCgMaxLevel) {
+      HIP_TRY(sparent[l + 1].ensure(sizeof(int) * (size_t)nslot[l] + 64));
+      int nn = 0;
+      st = select(fl_next.as<unsigned char>(), nslot[l], sparent[l + 1].as<int>(), &nn);
+      if (st) return st;
+      nslot[l + 1] = nn;
+      if (nn > 0) {
+        HIP_TRY(sband[l + 1].ensure(sizeof(int) * (size_t)nn));
+        HIP_TRY(cmax[l + 1].ensure(sizeof(int) * (size_t)nn));
+        b.lv[l + 1].slot_parent = sparent[l + 1].as<int>();
+        b.lv[l + 1].slot_band = sband[l + 1].as<int>();
+        b.lv[l + 1].cmax = cmax[l + 1].as<int>();
+        b.lv[l + 1].slot_cap = nn;
+        HIP_TRY(upload());
+        launch_cg_slots(s, db, l + 1, nn);
+      }
+    }
+  }
+  // emission: per level, list entries and fine cells of each final, scanned
+  DevBuf ent_n[4], fine_n[4];
+  unsigned ent_base[5] = {0, 0, 0, 0, 0}, fine_base[5] = {0, 0, 0, 0, 0};
+  for (int l = 0; l <= kCgMaxLevel; ++l) {
+    ent_base[l + 1] = ent_base[l];
+    fine_base[l + 1] = fine_base[l];
+    g->info.level_cells[l] = nfin[l];
+    if (nfin[l] == 0) continue;
+    HIP_TRY(ent_n[l].ensure(sizeof(unsigned) * ((size_t)nfin[l] + 1)));
+    HIP_TRY(fine_n[l].ensure(sizeof(unsigned) * ((size_t)nfin[l] + 1)));
+    launch_cg_emit_count(s, db, l, fin_sel[l].as<int>(), nfin[l], ent_n[l].as<unsigned>(), fine_n[l].as<unsigned>());
+    for (DevBuf* v : {&ent_n[l], &fine_n[l]}) {
+      // exclusive scan in place over nfin + 1 entries (the last one = the total)
+      HIP_TRY(hipMemsetAsync(v->as<unsigned>() + nfin[l], 0, sizeof(unsigned), s));
+      size_t tb = 0;
+      HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, v->as<unsigned>(), v->as<unsigned>(), nfin[l] + 1, s));
+      HIP_TRY(cub_tmp.ensure(std::max<size_t>(tb, 256)));
+      tb = cub_tmp.bytes;
+      HIP_TRY(hipcub::DeviceScan::ExclusiveSum(cub_tmp.p, tb, v->as<unsigned>(), v->as<unsigned>(), nfin[l] + 1, s));
+    }
+    unsigned tot[2];
+    HIP_TRY(hipMemcpyAsync(&tot[0], ent_n[l].as<unsigned>() + nfin[l], sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&tot[1], fine_n[l].as<unsigned>() + nfin[l], sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ent_base[l + 1] += tot[0];
+    fine_base[l + 1] += tot[1];
+  }
+  if ((size_t)fine_base[4] >= 0x3ffffffeu) return fail(GICP_ENOMEM, "candidate cells: fine table too large");
+  HIP_TRY(g->fine.ensure(sizeof(uint2) * std::max<size_t>(fine_base[4], 1)));
+  HIP_TRY(g->ent.ensure(sizeof(float4) * std::max<size_t>(ent_base[4], 1)));
+  b.fine = g->fine.as<uint2>();
+  b.ent = g->ent.as<float4>();
+  HIP_TRY(upload());
+  for (int l = 0; l <= kCgMaxLevel; ++l)
+    if (nfin[l] > 0)
+      launch_cg_emit_write(s, db, l, fin_sel[l].as<int>(), nfin[l], ent_n[l].as<unsigned>(), fine_n[l].as<unsigned>(),
+                           ent_base[l], fine_base[l]);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(e1, s));
+  st = read_counters();   // (waits for the build)
+  if (st) return st;
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  g->info.build_ms = ms;
+  g->info.nomatch_cells = counters[kCtrNoMatch * 32];
+  g->info.overflow_cells = counters[kCtrOverflow * 32];
+  g->info.fallback_fine = counters[kCtrFineFb * 32];
+  g->info.fine_cells = (int64_t)fine_base[4] - g->info.fallback_fine;
+  g->info.entries = ent_base[4];
+  g->info.bytes = (int64_t)(g->dir.bytes + g->fine.bytes + g->ent.bytes);
+  g->info.built = 1;
+  CellGridDev& d = g->dev;
+  d.dir = g->dir.as<unsigned>();
+  d.fine = g->fine.as<uint2>();
+  d.ent = g->ent.as<float4>();
+  d.ox = b.fox;
+  d.oy = b.foy;
+  d.oz = b.foz;
+  d.inv_s = b.inv_s;
+  d.nx = b.nx;
+  d.ny = b.ny;
+  d.nz = b.nz;
+  d.outside_nomatch = outside_nomatch ? 1 : 0;
+  g->ok = true;
+  return GICP_OK;
+}
+
+// gicp_set_target_grid policy: build the target's candidate cells for this
+// ctx's bound (auto: at the second align against the same target and bound)
+gicp_status maybe_build_grid(gicp_ctx* c) {
+  if (!c->grid_mode || !c->tgt.cloud || !search_uses_tasks()) return GICP_OK;
+  CloudData& t = *c->tgt.cloud;
+  const float cap2 = search_cap2(c->params);
+  if (t.grid && t.grid->cap2 == cap2) return GICP_OK;   // built (or found too large) for this bound
+  if (t.grid_aligns_cap2 != cap2) {
+    t.grid_aligns_cap2 = cap2;
+    t.grid_aligns = 0;
+  }
+  ++t.grid_aligns;
+  if (c->grid_mode == GICP_GRID_AUTO && t.grid_aligns < 2) return GICP_OK;
+  std::shared_ptr<CellGridData> g;
+  const gicp_status s = cellgrid_build(c, t, cap2, &g);
+  if (s) return s;
+  t.grid = g;
+  return GICP_OK;
+}
+
 gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   const SearchKnobs& kn = search_knobs();
   AlignJob& j = *c->job_host;
@@ -241,6 +550,17 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
     }
     if (c->tie_ref) j.tie_map = c->tie_map.as<int>();
   }
+  // the target's candidate cells answer the search first (k_cell_lookup)
+  j.grid_on = grid_active(c) ? 1 : 0;
+  if (j.grid_on) {
+    j.grid = c->tgt.cloud->grid->dev;
+    const FbLayout fl(c->src.cloud->n);
+    char* u = c->fb.as<char>();
+    j.fb_count = reinterpret_cast<unsigned*>(u + fl.ctr);
+    j.fb_list = reinterpret_cast<int*>(u + fl.list);
+    j.fb_seg_cap = fl.seg_cap;
+    j.fb_mask = reinterpret_cast<unsigned short*>(u + fl.mask);
+  }
   // no copy here: k_align_init reads the pinned job and writes the device one
   return GICP_OK;
 }
@@ -249,6 +569,7 @@ int linearize_blocks(int nsrc) { return linearize_geometry(nsrc, 0).mom_blocks; 
 LinGeom geometry(const gicp_ctx* c) {
   LinGeom g = linearize_geometry(c->src.cloud->n, c->tgt.cloud->upper_count());
   g.fuse_lm = !c->comm && lm_fusion_enabled();   // a sharded align all-reduces between the moments and the LM step
+  g.grid = grid_active(c);
   return g;
 }
 
@@ -269,9 +590,10 @@ gicp_status prepare_align(gicp_ctx* c) {
   // previous align must not still reference it
   const size_t need_corr = sizeof(int) * ns, need_sqd = sizeof(float) * ns,
                need_slab = sizeof(double) * kSlabStride * linearize_blocks(ns),
-               need_search = SearchLayout(ns).total;
+               need_search = SearchLayout(ns).total, need_fb = grid_active(c) ? FbLayout(ns).total : 0;
   if (need_corr > c->corr.bytes || need_sqd > c->sqd.bytes || need_slab > c->slab.bytes ||
-      need_search > c->search.bytes || (c->stats_on && sizeof(unsigned int) * kStatFields * (ns + 15) > c->stats.bytes)) {
+      need_search > c->search.bytes || need_fb > c->fb.bytes ||
+      (c->stats_on && sizeof(unsigned int) * kStatFields * (ns + 15) > c->stats.bytes)) {
     gicp_status s = drain_tail(c);
     if (s) return s;
   }
@@ -280,6 +602,7 @@ gicp_status prepare_align(gicp_ctx* c) {
   HIP_TRY(c->slab.ensure(sizeof(double) * kSlabStride * linearize_blocks(ns)));
   HIP_TRY(c->mom.ensure(sizeof(double) * kSlabStride));
   HIP_TRY(c->search.ensure(need_search));
+  if (need_fb) HIP_TRY(c->fb.ensure(need_fb));
   // the target's nanoflann tree (tie order): a sharded align builds it up
   // front (every rank the same tree, so no rank ever re-runs alone and the
   // collectives stay matched); otherwise it is built only when an align
@@ -386,7 +709,7 @@ void drop_graphs(gicp_ctx* c) {
 // single-iteration graphs now, first chunks on demand), evicting the least
 // recently used set -- after the stream's queued chunk, which may be one of
 // its graphs, has run.
-gicp_status graph_set(gicp_ctx* c, const std::array<long long, 7>& key, int nblocks, GraphSet** out);
+gicp_status graph_set(gicp_ctx* c, const std::array<long long, 8>& key, int nblocks, GraphSet** out);
 
 // Launch the align as a first chunk of n outer iterations (n = the previous
 // align's iteration count on this ctx: aligns of consecutive scans converge
@@ -401,8 +724,8 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   // key: whether RCCL is in the chunk, the job buffer and the launch geometry
   const LinGeom g = geometry(c);
   (void)nblocks;   // = g.mom_blocks
-  const std::array<long long, 7> key{{c->comm ? 1 : 0, (long long)(uintptr_t)jd, g.seed_blocks, g.collect_blocks,
-                                      g.scan_blocks, g.mom_blocks, g.lds_boxes}};
+  const std::array<long long, 8> key{{c->comm ? 1 : 0, (long long)(uintptr_t)jd, g.seed_blocks, g.collect_blocks,
+                                      g.scan_blocks, g.mom_blocks, g.lds_boxes, g.grid ? g.lookup_blocks : 0}};
   const bool use_graph = !c->comm || c->comm_graphs;
   const int first = std::max(1, std::min({c->predicted_iters, max_it, kMaxFirstChunk}));
   GraphSet* gs = nullptr;
@@ -498,7 +821,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   return GICP_OK;
 }
 
-gicp_status graph_set(gicp_ctx* c, const std::array<long long, 7>& key, int nblocks, GraphSet** out) {
+gicp_status graph_set(gicp_ctx* c, const std::array<long long, 8>& key, int nblocks, GraphSet** out) {
   ++c->graph_clock;
   for (auto& gs : c->gsets)
     if (gs.key == key) {
@@ -829,6 +1152,8 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
   begin_ties(c);
   gicp_status s = set_device(c);
   if (s) return s;
+  s = maybe_build_grid(c);
+  if (s) return s;
   s = prepare_align(c);
   if (s) return s;
   const int ns = c->src.cloud->n;
@@ -1018,6 +1343,8 @@ gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, doubl
   begin_ties(c);
   gicp_status s = set_device(c);
   if (s) return s;
+  s = maybe_build_grid(c);
+  if (s) return s;
   s = prepare_align(c);
   if (s) return s;
   const int ns = c->src.cloud->n;
@@ -1106,6 +1433,37 @@ gicp_status gicp_knn_target(gicp_ctx* c, const float* q, size_t nq, size_t strid
 gicp_status gicp_set_tie_order(gicp_ctx* c, int nanoflann_order) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
   c->tie_exact = nanoflann_order != 0;
+  return GICP_OK;
+}
+
+gicp_status gicp_set_target_grid(gicp_ctx* c, int mode) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  if (mode < GICP_GRID_OFF || mode > GICP_GRID_ON) return fail(GICP_EINVAL, "grid mode must be 0 (off), 1 (auto) or 2 (on)");
+  c->grid_mode = mode;
+  return GICP_OK;
+}
+
+gicp_status gicp_get_target_grid_info(gicp_ctx* c, gicp_grid_info* out) {
+  if (!c || !out) return fail(GICP_EINVAL, "null argument");
+  std::memset(out, 0, sizeof(*out));
+  if (!c->tgt.cloud || !c->tgt.cloud->grid) return GICP_OK;
+  *out = c->tgt.cloud->grid->info;
+  out->built = grid_active(c) ? 1 : 0;
+  return GICP_OK;
+}
+
+gicp_status gicp_get_lookup_stats(gicp_ctx* c, int64_t* walk_groups) {
+  if (!c || !walk_groups) return fail(GICP_EINVAL, "null argument");
+  *walk_groups = -1;
+  if (!c->fb.p || !c->src.cloud) return GICP_OK;
+  gicp_status s = set_device(c);
+  if (s) return s;
+  unsigned v = 0;
+  const FbLayout fl(c->src.cloud->n);
+  HIP_TRY(hipMemcpyAsync(&v, c->fb.as<char>() + fl.ctr + sizeof(unsigned) * kFbSegs * 32, sizeof(unsigned),
+                         hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  *walk_groups = v;
   return GICP_OK;
 }
 

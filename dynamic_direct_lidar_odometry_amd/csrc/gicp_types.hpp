@@ -89,6 +89,28 @@ struct NfTreeDev {
   const float4* sbox;  // the box divideTree passes it: sbox[2 id], sbox[2 id + 1]); the lazy search splits it
 };
 
+// ---------------------------------------------------------------------------
+// Candidate cells of a target (cellgrid.hip, DESIGN.md §4 "Candidate cells"):
+// built once per target and bound, they answer the bounded 1-NN of
+// update_correspondences (nano_gicp_impl.hpp:249-258) for a query in cell C
+// from C's list: every target point that can be the fp32-nearest (or tie
+// with it) for some point of C.  Coarse cells of size s tile the target's
+// box plus the bound; a coarse cell is split uniformly into (2^level)^3 fine
+// cells.
+constexpr unsigned kCgNoMatch = 0xffffffffu;    // dir: no target point within the bound of any point of the cell
+constexpr unsigned kCgFallback = 0xfffffffeu;   // dir: no list (the walk searches the cell's queries)
+constexpr unsigned kCgFineFallback = 0xffffffffu;   // fine entry count: no list (the walk)
+constexpr int kCgMaxLevel = 3;
+
+struct CellGridDev {
+  const unsigned* dir;     // [nx * ny * nz] (level << 30) | fine-table base, or kCgNoMatch / kCgFallback
+  const uint2* fine;       // per fine cell: (first entry, count)
+  const float4* ent;       // list entries: x, y, z, sorted target position (int bits)
+  float ox, oy, oz, inv_s; // grid origin, 1 / coarse cell size
+  int nx, ny, nz;
+  int outside_nomatch;     // a query outside the grid box has no target point within the bound (else the walk)
+};
+
 // Per-align device state (one per ctx, lives in device memory).
 struct AlignState {
   double R[9];           // x0 (current estimate), row-major
@@ -217,7 +239,20 @@ struct AlignJob {
   NfTreeDev tgt_nf;              // nodes == nullptr: no tree (yet)
   const int* tie_map;            // tgt_nf is a whole cloud the target was cut from (slab shard): its original
                                  // index -> the target's sorted position (-1: not in it); nullptr: tgt.inv_perm
+  // Candidate-cell lookup (k_cell_lookup, before the walk): grid_on = 1 when
+  // the target has candidate cells built for this bound.  The lookup answers
+  // every query whose cell has a list; the 16-query sub-groups left with an
+  // unanswered owned query are listed for the walk (fb_list, fb_mask: the
+  // unanswered queries of each sub-group, bit qi).
+  int grid_on;
+  CellGridDev grid;
+  unsigned* fb_count;            // [kFbSegs * 32]: sub-groups listed for the walk per segment (zeroed by
+                                 // k_align_init / k_moments; one counter per segment, 128 B apart)
+  int* fb_list;                  // [kFbSegs][fb_seg_cap]
+  int fb_seg_cap;
+  unsigned short* fb_mask;       // [n_src / 16]
 };
+constexpr int kFbSegs = 8;       // walk-list segments (a wavefront appends to segment wave % kFbSegs)
 
 constexpr int kNfMaxLevels = 40;   // big levels of the device build (deeper: the build reports a failure)
 constexpr int kNfLevelSpare = 2;   // big levels a ctx's build carries beyond those its last build used

@@ -920,6 +920,7 @@ __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_d
   }
   AlignState* st = job->state;
   if (threadIdx.x <= kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;   // + the moment kernel's arrival counter
+  if (job->grid_on && threadIdx.x <= kFbSegs) job->fb_count[threadIdx.x * 32] = 0u;   // the lookup's walk list (+ total)
   if (threadIdx.x < 64) {   // source radius from the top-level boxes (<= 64 of them)
     const CloudDev& c = job->src;
     const int top = c.nlevels - 1;
@@ -954,6 +955,124 @@ __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_d
     st->tie_pending = 0;
     st->ties_resolved = 0;
     st->tie_err = 0;
+  }
+}
+
+// K3g: candidate-cell lookup (cellgrid.hip), one query per lane, before the
+// walk.  The fp32 query transform of update_correspondences
+// (nano_gicp_impl.hpp:240,253; k_nn_seed's operations), the query's cell, and
+// the (squared distance, sorted position) minimum over the cell's list: the
+// key the full search returns, because every point that can be the fp32
+// nearest point of a query of the cell, or tie with it, is on the list.  The
+// tie test of k_moments gets sec = the key's distance when a second list
+// point has it (nanoflann's order then re-runs the query), else all ones (no
+// test).  A query without a list (its cell was not built, or its list
+// exceeded the cap) marks its 16-query sub-group for the walk (fb_mask bit,
+// fb_list entry); the walk then searches only those queries.
+__global__ __launch_bounds__(256) void k_cell_lookup(const AlignJob* __restrict__ job) {
+  AlignState* st = job->state;
+  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+  const CloudDev src = job->src;
+  const CellGridDev G = job->grid;
+  const float cap2 = job->cap2;
+  const int lane = lane_id();
+  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
+  const int n64 = (src.n + 63) >> 6;
+  const int own_axis = job->own_axis;
+  const float own_lo = job->own_lo, own_hi = job->own_hi;
+  const int own_mod = job->own_mod, own_rem = job->own_rem;
+  const int tie_detect = job->tie_detect;
+  float Rf[9], tf[3];
+  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
+  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
+  for (int w = wave; w < n64; w += nwaves) {
+    const int i = w * 64 + lane;
+    const bool inrange = i < src.n;
+    const float4 a = ldg4(src.pts, inrange ? i : src.n - 1);
+    const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
+    const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
+    const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
+    const int g = i >> 4;
+    const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
+    const bool owned = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi)) &&
+                       (own_mod == 0 || (g % own_mod) == own_rem);
+    bool walk = false;
+    unsigned off = 0, cnt = 0;
+    if (owned) {
+      const float tx = (qx - G.ox) * G.inv_s, ty = (qy - G.oy) * G.inv_s, tz = (qz - G.oz) * G.inv_s;
+      if (!(tx >= 0.f && tx < (float)G.nx && ty >= 0.f && ty < (float)G.ny && tz >= 0.f && tz < (float)G.nz)) {
+        walk = !G.outside_nomatch;   // beyond every target point's reach (or outside the built box)
+      } else {
+        const int cx = min((int)tx, G.nx - 1), cy = min((int)ty, G.ny - 1), cz = min((int)tz, G.nz - 1);
+        const unsigned d = gp(G.dir)[((long)cx * G.ny + cy) * G.nz + cz];
+        if (d == kCgFallback) {
+          walk = true;
+        } else if (d != kCgNoMatch) {
+          const int lvl = (int)(d >> 30), m = 1 << lvl;
+          const int fx = min((int)((tx - (float)cx) * (float)m), m - 1);
+          const int fy = min((int)((ty - (float)cy) * (float)m), m - 1);
+          const int fz = min((int)((tz - (float)cz) * (float)m), m - 1);
+          const unsigned long long e =
+              gp(reinterpret_cast<const unsigned long long*>(G.fine))[(d & 0x3fffffffu) + (unsigned)((fx * m + fy) * m + fz)];
+          if ((unsigned)(e >> 32) == kCgFineFallback) walk = true;
+          else {
+            off = (unsigned)e;
+            cnt = (unsigned)(e >> 32);
+          }
+        }
+      }
+    }
+    // the list's (distance, position) minimum and the smallest other distance
+    unsigned long long bk = ~0ull;
+    float d2 = INFINITY;
+    for (unsigned k = 0; k < cnt; k += 4) {
+      float4 p[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[j] = ldg4(G.ent, off + min(k + j, cnt - 1));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (k + j < cnt) {
+          const float dd = dist2(qx, qy, qz, p[j].x, p[j].y, p[j].z);
+          const unsigned long long kk = dkey(dd, __float_as_int(p[j].w));
+          if (kk < bk) {
+            if (bk != ~0ull) d2 = fminf(d2, __uint_as_float((unsigned)(bk >> 32)));
+            bk = kk;
+          } else {
+            d2 = fminf(d2, dd);
+          }
+        }
+      }
+    }
+    if (inrange && !walk) {
+      job->qstate[i] = make_float4(qx, qy, qz, -1.f);
+      const unsigned long long key = owned ? umin64(bk, dkey(cap2, -1)) : dkey(INFINITY, -1);
+      job->key[i] = key;
+      if (tie_detect) {
+        const float kd = __uint_as_float((unsigned)(key >> 32));
+        const bool tied = owned && (unsigned)key != 0xffffffffu && d2 == kd;
+        job->sec[i] = tied ? (unsigned)(key >> 32) : 0xffffffffu;
+      }
+      if (job->tie_scan == 3) job->key2[i] = mirror_key(key);
+    }
+    // sub-groups with a query for the walk
+    const unsigned long long wb = __ballot(walk);
+    if (wb) {
+      const int r = lane >> 4;
+      const unsigned m16 = (unsigned)(wb >> (16 * r)) & 0xffffu;
+      const int nz = ((wb & 0xffffull) != 0) + ((wb & 0xffff0000ull) != 0) + ((wb & 0xffff00000000ull) != 0) +
+                     ((wb >> 48) != 0);
+      const int seg = w & (kFbSegs - 1);
+      int base = 0;
+      if (lane == 0) base = (int)atomicAdd(job->fb_count + seg * 32, (unsigned)nz);
+      base = __builtin_amdgcn_readfirstlane(base);
+      if ((lane & 15) == 0 && m16) {
+        int rank = 0;
+        for (int t = 0; t < r; ++t) rank += ((wb >> (16 * t)) & 0xffffull) != 0;
+        job->fb_list[seg * job->fb_seg_cap + base + rank] = g;
+        job->fb_mask[g] = (unsigned short)m16;
+      }
+    }
   }
 }
 
@@ -1023,11 +1142,38 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
     fill_upper(tgt, upper);
     __syncthreads();
   }
-  for (int g = wave; g < ngroups; g += nwaves_total) {
+  // candidate cells (k_cell_lookup): only the listed sub-groups, only their
+  // unanswered queries; the answered ones keep the lookup's outputs
+  const int grid_on = job->grid_on;
+  int seg_end[kFbSegs];
+  int nitems = ngroups;
+  if (grid_on) {
+    nitems = 0;
+#pragma unroll
+    for (int sg = 0; sg < kFbSegs; ++sg) {
+      nitems += (int)job->fb_count[sg * 32];
+      seg_end[sg] = nitems;
+    }
+  }
+  for (int item = wave; item < nitems; item += nwaves_total) {
+    int g = item;
+    unsigned gmask = 0xffffu;
+    if (grid_on) {
+      int sg = 0, s0 = 0;
+#pragma unroll
+      for (int t = 0; t < kFbSegs - 1; ++t)
+        if (item >= seg_end[t]) {
+          sg = t + 1;
+          s0 = seg_end[t];
+        }
+      g = job->fb_list[sg * job->fb_seg_cap + (item - s0)];
+      gmask = job->fb_mask[g];
+    }
+    const bool mine = (gmask >> qi) & 1u;   // this search writes the query's outputs
     const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const int i = g * Q + qi;
-    const bool inrange = i < src.n;
-    const int ic = inrange ? i : src.n - 1;
+    const bool inrange = i < src.n && mine;
+    const int ic = i < src.n ? i : src.n - 1;
     // every independent per-query load of the prologue in one round trip
     const float4 a = ldg4(src.pts, ic);
     const int jprev = have_prev ? corr[ic] : -1;
@@ -2052,6 +2198,12 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
   const int ngroups = (src.n + 63) >> 6;
   // the search's task counters are free again: zero them for the next one
   if (blockIdx.x == 0 && threadIdx.x < kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;
+  if (blockIdx.x == 0 && job->grid_on && threadIdx.x == 0) {   // the walk list is consumed: its total, then reset
+    unsigned t = 0;
+    for (int sg = 0; sg < kFbSegs; ++sg) t += job->fb_count[sg * 32];
+    job->fb_count[kFbSegs * 32] += t;
+    for (int sg = 0; sg < kFbSegs; ++sg) job->fb_count[sg * 32] = 0u;
+  }
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   for (int g = wave; g < ngroups; g += nwaves_total) {
     const int i = g * 64 + lane;
@@ -3057,10 +3209,12 @@ LinGeom linearize_geometry(int nsrc, int tgt_upper) {
   g.scan_blocks = scan_blocks(gcap * kSearchQ);                   // any grid is exact
   g.mom_blocks = moment_blocks(cdiv(std::max(nsrc, 1), 32768) * 32768);   // grid-stride; = the slab rows
   g.lds_boxes = std::min(2048, cdiv(std::max(tgt_upper, 1), 128) * 128);   // >= the target's upper boxes
+  g.lookup_blocks = std::max(1, gcap * kSearchQ / 256);                    // one query per lane
   return g;
 }
 
 void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
+  if (g.grid) k_cell_lookup<<<g.lookup_blocks, 256, 0, s>>>(job);
   if (!search_uses_tasks()) {
     k_nn_search<kSearchQ, 3><<<g.seed_blocks, 64 * kLinWaves, search_lds_bytes(g.lds_boxes), s>>>(job);
   } else {

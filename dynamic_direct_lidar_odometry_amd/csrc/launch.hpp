@@ -49,8 +49,9 @@ void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src);
 // Launch geometry of one linearize (grids, upper-box LDS cache), bucketed by
 // cloud size; part of the chunk-graph key.
 struct LinGeom {
-  int seed_blocks, collect_blocks, scan_blocks, mom_blocks, lds_boxes;
+  int seed_blocks, collect_blocks, scan_blocks, mom_blocks, lds_boxes, lookup_blocks;
   bool fuse_lm = false;   // the LM step runs in the moment kernel's last block (no k_lm_step launch)
+  bool grid = false;      // the target's candidate cells answer the search first (k_cell_lookup)
 };
 bool lm_fusion_enabled();   // DDLO_FUSE_LM (unsharded graph aligns)
 LinGeom linearize_geometry(int nsrc, int tgt_upper);

@@ -220,12 +220,25 @@ struct NfTreeData {
   }
 };
 
+// Candidate cells of a target cloud for one correspondence bound
+// (cellgrid.hip; built by cellgrid_build in capi.hip).
+struct CellGridData {
+  float cap2 = 0.f;            // the bound (AlignJob::cap2) the lists were built for
+  bool ok = false;             // built (else the walk answers every query)
+  DevBuf dir, fine, ent;
+  CellGridDev dev{};
+  gicp_grid_info info{};
+};
+
 // Immutable device cloud + search hierarchy (shared between ctxs/sides).
 struct CloudData {
   int n = 0;
   DevBuf pts, keys, perm, inv_perm, box_lo, box_hi, quant, soa, dir;
   std::shared_ptr<NfTreeData> nf;   // nanoflann's tree (tie order), built on first need
   std::shared_ptr<NfTreeData> nfp;  // its top levels only (the lazy covariance tie search)
+  std::shared_ptr<CellGridData> grid;   // candidate cells (S2M targets), built on demand
+  float grid_aligns_cap2 = -1.f;        // the bound of the aligns counted in grid_aligns
+  int grid_aligns = 0;                  // aligns against this cloud as the target with that bound
   int nlevels = 0;
   int lvl_off[kMaxLevels] = {0};
   int lvl_cnt[kMaxLevels] = {0};
@@ -294,7 +307,7 @@ struct hipExecGraphPair {
 // publishing to state slot s = 0, 1; captured for: RCCL in the chunk, job
 // buffer, launch geometry (LinGeom).
 struct GraphSet {
-  std::array<long long, 7> key{{-1, -1, -1, -1, -1, -1, -1}};
+  std::array<long long, 8> key{{-1, -1, -1, -1, -1, -1, -1, -1}};
   std::vector<hipExecGraphPair> first;
   hipExecGraphPair rest[2];
   long long last_use = 0;
@@ -412,6 +425,9 @@ struct gicp_ctx {
   // orders the ties) and its original index -> local sorted position
   std::shared_ptr<CloudData> tie_ref;
   DevBuf tie_map;
+  // candidate cells of the target (gicp_set_target_grid): 0 off, 1 auto, 2 on
+  int grid_mode = GICP_GRID_AUTO;
+  DevBuf fb;                      // the lookup's walk list: [counters][list segments][masks]
   // stage timing of compute_cov (profiling on): covariance kernel, tree build, resolvers
   hipEvent_t st_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool st_tree = false;          // the last compute_cov built a tree (events 2, 3 recorded)

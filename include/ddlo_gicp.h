@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DDLO_GICP_ABI_VERSION 2
+#define DDLO_GICP_ABI_VERSION 3
 
 typedef enum gicp_status {
   GICP_OK = 0,
@@ -212,6 +212,43 @@ gicp_status gicp_knn_target(struct gicp_ctx* ctx, const float* q, size_t nq, siz
  * is built).  Distances are identical either way.  Applies to covariances
  * and gicp_knn_target. */
 gicp_status gicp_set_tie_order(struct gicp_ctx* ctx, int nanoflann_order);
+
+/* Candidate cells of the target (DESIGN.md §4 "Candidate cells"): a
+ * per-target structure built once per (target cloud, max correspondence
+ * distance) that answers update_correspondences' bounded 1-NN
+ * (nano_gicp_impl.hpp:249-258, the nanoflann knnSearch it calls) by a cell
+ * lookup and a short list scan instead of a walk of the index, on every
+ * outer iteration of every align against that target.  Results are
+ * identical with or without it (same correspondences, distances and tie
+ * order); only the time differs.  It pays for a target that is aligned
+ * against several times (the S2M submap: OdomNode keeps a submap for many
+ * scans, odom.cc:1215-1315).  mode: 0 = off; 1 = auto (default): built at the
+ * second align against the same target and bound; 2 = built at the next
+ * align.  The structure belongs to the target cloud (it follows
+ * gicp_swap_source_target). */
+#define GICP_GRID_OFF 0
+#define GICP_GRID_AUTO 1
+#define GICP_GRID_ON 2
+gicp_status gicp_set_target_grid(struct gicp_ctx* ctx, int mode);
+typedef struct gicp_grid_info {
+  int32_t built;             /* 1 = the target has candidate cells for the ctx's bound */
+  float build_ms;            /* device time of the build (HIP events)                 */
+  float cell_size;           /* coarse cell edge (m); fine cells are 1/2..1/8 of it  */
+  int64_t bytes;             /* device memory held by the structure                   */
+  int64_t coarse_cells;      /* cells of the grid box                                 */
+  int64_t band_cells;        /* coarse cells within reach of the target               */
+  int64_t nomatch_cells;     /* ... of which no point is within the bound             */
+  int64_t overflow_cells;    /* ... whose candidates overflowed (the walk answers)   */
+  int64_t level_cells[4];    /* coarse cells finished at fine level 0..3              */
+  int64_t fine_cells;        /* fine cells with a list                                */
+  int64_t fallback_fine;     /* fine cells whose list exceeded the cap (the walk)     */
+  int64_t entries;           /* list entries (16 B each)                              */
+} gicp_grid_info;
+gicp_status gicp_get_target_grid_info(struct gicp_ctx* ctx, gicp_grid_info* out);
+/* Queries the last align's final linearize answered from the candidate cells
+ * and sub-groups of 16 it left to the walk (diagnostics). */
+gicp_status gicp_get_lookup_stats(struct gicp_ctx* ctx, int64_t* walk_groups);
+
 /* nanoflann's kd-tree of a side's cloud as the device built it (tests):
  * vind[n]; per node (c1, c2, divfeat, parent) with divfeat -1 for a leaf
  * whose vind range is [c1, c2), and (divlow, divhigh).  With all three
