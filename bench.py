@@ -423,6 +423,9 @@ def s2s_gn_leg(local_rank, args):
     c = P.Context(local_rank)
     c.set_params(P.default_params(k_correspondences=10, max_correspondence_distance=1.0, optimizer=P.GAUSS_NEWTON,
                                   fixed_iterations=20, max_iterations=20))
+    # S2S targets are used once (OdomNode swaps every scan, odom.cc:768): the
+    # walk, as in the pipeline (AUTO would build cells at this loop's 2nd align)
+    c.set_target_grid(P.GRID_OFF)
     c.set_target(tgt)
     c.set_source(src)
     c.compute_covariances(SOURCE)
@@ -572,7 +575,7 @@ def main():
         td.init_process_group(backend="nccl")
         dist = td
 
-    from dynamic_direct_lidar_odometry_amd import Context, default_params, SOURCE, TARGET
+    from dynamic_direct_lidar_odometry_amd import Context, default_params, SOURCE, TARGET, GRID_ON, GRID_OFF
 
     t0 = time.time()
     prob = build_problem()
@@ -590,10 +593,17 @@ def main():
     ctx.compute_covariances(SOURCE)
     scov = ctx.get_covariances(SOURCE)
     ctx.set_params(params)
+    ctx.set_target_grid(GRID_ON)   # the submap's candidate cells, built at the first align
     ctx.set_target(sub)
     ctx.set_covariances(TARGET, tcov)
     guess = prob["guess"].astype(np.float32)
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s: src {len(src)} tgt {len(sub)}")
+    # the per-target build (once per setInputTarget; like the index, outside ms/scan): the first align
+    ctx.synchronize()
+    t_b = time.perf_counter()
+    ctx.align(guess)
+    first_align_ms = 1e3 * (time.perf_counter() - t_b)
+    grid_info = ctx.grid_info()
 
     # warmup
     for _ in range(args.warmup):
@@ -652,10 +662,37 @@ def main():
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_unit": "bytes per linearize launch (L2->fabric, Infinity-Cache hits included; counters as read)",
                      "traffic_source": traffic_src,
-                     "kernel": "linearize = k_nn_seed (seed + tree walk) + k_nn_scan + k_moments (per outer iteration)",
+                     "kernel": "linearize = k_cell_lookup (candidate cells) + k_nn_seed (walk of the sub-groups "
+                               "without a list; none here) + k_moments (per outer iteration)",
                      "avg_launch_us": round(avg_launch_s * 1e6, 2),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch)},
     }
+
+    result["target_grid"] = {**grid_info, "first_align_ms": round(first_align_ms, 3),
+                             "walk_groups_last_align": ctx.lookup_walk_groups(),
+                             "note": "candidate cells of the submap, built once per target (first align, outside "
+                                     "ms/scan like the index build, SURVEY.md §8(d)); the odometry leg pays them"}
+    # the same aligns with the cells off (the round-4 walk), for comparison
+    ctx.set_target_grid(GRID_OFF)
+    for _ in range(3):
+        ctx.align(guess)
+    ctx.synchronize()
+    t_w = time.perf_counter()
+    nw = max(20, args.steps // 4)
+    for _ in range(nw):
+        ctx.align(guess)
+    ctx.synchronize()
+    walk_ms = 1e3 * (time.perf_counter() - t_w) / nw
+    ctx.set_profiling(True)
+    wl_ms, wl_n = 0.0, 0
+    for _ in range(5):
+        _, r = ctx.align(guess)
+        wl_ms += r.linearize_ms
+        wl_n += r.iterations_run
+    ctx.set_profiling(False)
+    ctx.set_target_grid(GRID_ON)
+    result["cfg3_walk"] = {"ms_per_scan": round(walk_ms, 4), "linearize_us": round(1e3 * wl_ms / max(wl_n, 1), 2),
+                           "note": "candidate cells off (gicp_set_target_grid 0): the seed + walk + scan search"}
 
     # the launch predictor's misses in the number: cycle 8 distinct guesses
     # (the headline repeats one, so its iteration count is always predicted)

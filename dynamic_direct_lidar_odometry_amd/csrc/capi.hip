@@ -186,7 +186,7 @@ struct FbLayout {
 // 3 times where lists are longer than kGridListMax points.
 constexpr double kGridCell = 0.4;
 constexpr double kGridMaxReach = 4.0;     // bounds beyond this: cells farther than it use the walk
-constexpr int kGridListMax = 24;
+constexpr int kGridListMax = 32;
 constexpr int kGridListCap = 256;         // finest level: longer lists are not stored (the walk)
 constexpr long kGridMaxCells = 48L << 20; // coarse cells (the directory is 4 B per cell)
 
@@ -245,31 +245,33 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   // scratch
   const long nbx = (dims[0] + 3) / 4, nby = (dims[1] + 3) / 4, nbz = (dims[2] + 3) / 4;
   const long nblocked = nbx * nby * nbz * 64;
-  DevBuf occ, tmp, flags, ctr, band, dnum, cub_tmp, centers, cnn, cnd, db_buf;
-  HIP_TRY(occ.ensure((size_t)ncells));
-  HIP_TRY(tmp.ensure((size_t)ncells));
+  DevBuf rep, rep_tmp, flags, ctr, band, dnum, cub_tmp, cnn, db_buf;
+  HIP_TRY(rep.ensure(sizeof(int) * (size_t)ncells));
+  HIP_TRY(rep_tmp.ensure(sizeof(int) * (size_t)ncells));
   HIP_TRY(flags.ensure((size_t)std::max(nblocked, ncells)));
   HIP_TRY(ctr.ensure(sizeof(unsigned) * kCgCtrWords));
   HIP_TRY(band.ensure(sizeof(int) * (size_t)ncells));
   HIP_TRY(dnum.ensure(sizeof(int) * 8));
   HIP_TRY(db_buf.ensure(sizeof(CgBuild)));
   HIP_TRY(g->dir.ensure(sizeof(unsigned) * (size_t)ncells));
-  b.occ = occ.as<unsigned char>();
-  b.tmp = tmp.as<unsigned char>();
+  b.rep = rep.as<int>();
+  b.rep_tmp = rep_tmp.as<int>();
+  b.rep_final = rep.as<int>();   // x: rep -> tmp, y: tmp -> rep, z: rep -> tmp; see below
   b.dir = g->dir.as<unsigned>();
   b.band = band.as<int>();
   b.ctr = ctr.as<unsigned>();
   CgBuild* db = db_buf.as<CgBuild>();
   auto upload = [&]() -> hipError_t { return hipMemcpyAsync(db, &b, sizeof(CgBuild), hipMemcpyHostToDevice, s); };
+  b.rep_final = rep_tmp.as<int>();
   HIP_TRY(upload());
-  HIP_TRY(hipMemsetAsync(occ.p, 0, (size_t)ncells, s));
+  HIP_TRY(hipMemsetAsync(rep.p, 0x7f, sizeof(int) * (size_t)ncells, s));   // 0x7f7f7f7f: none (> any position)
   HIP_TRY(hipMemsetAsync(ctr.p, 0, sizeof(unsigned) * kCgCtrWords, s));
-  launch_cg_occ(s, db, cd.n, ncells);
-  launch_cg_dilate(s, db, 0, b.occ, b.tmp, ncells);
-  launch_cg_dilate(s, db, 1, b.tmp, b.occ, ncells);
-  launch_cg_dilate(s, db, 2, b.occ, b.tmp, ncells);   // band = tmp
-  launch_cg_dir_fill(s, b.dir, b.tmp, ncells, outside_nomatch ? kCgNoMatch : kCgFallback);
-  launch_cg_band_flags(s, db, b.tmp, flags.as<unsigned char>(), nblocked);
+  launch_cg_occ(s, db, cd.n);
+  launch_cg_prop(s, db, 0, b.rep, b.rep_tmp, ncells);
+  launch_cg_prop(s, db, 1, b.rep_tmp, b.rep, ncells);
+  launch_cg_prop(s, db, 2, b.rep, b.rep_tmp, ncells);   // band: rep_tmp != none
+  launch_cg_dir_fill(s, b.dir, b.rep_tmp, ncells, outside_nomatch ? kCgNoMatch : kCgFallback);
+  launch_cg_band_flags(s, db, b.rep_tmp, flags.as<unsigned char>(), nblocked);
   HIP_TRY(hipGetLastError());
   // band cells in blocked order (selected blocked ids; k_cg_centers turns them into cell ids)
   auto select = [&](const unsigned char* fl, long n, int* outp, int* nsel) -> gicp_status {
@@ -294,16 +296,10 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   DevBuf hdr[4], pool[4], cmax[4], sband[4], sparent[4], fin_sel[4], fl_final, fl_next;
   int nfin[4] = {0, 0, 0, 0}, nslot[4] = {0, 0, 0, 0};
   if (nband > 0) {
-    HIP_TRY(centers.ensure(sizeof(float4) * (size_t)nband));
     HIP_TRY(cnn.ensure(sizeof(int) * (size_t)nband));
-    HIP_TRY(cnd.ensure(sizeof(float) * (size_t)nband));
-    b.centers = centers.as<float4>();
     b.cnn = cnn.as<int>();
-    b.cnd = cnd.as<float>();
     HIP_TRY(upload());
     launch_cg_centers(s, db, nband);
-    if (!launch_knn_query(s, b.tgt, b.centers, nband, 1, b.cnn, b.cnd, TieList{nullptr, nullptr}))
-      return fail(GICP_EINVAL, "candidate cells: nearest-point pass");
     HIP_TRY(hdr[0].ensure(sizeof(uint2) * (size_t)nband));
     HIP_TRY(fl_final.ensure((size_t)nband));
     HIP_TRY(fl_next.ensure((size_t)nband));
@@ -416,7 +412,7 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
   g->info.build_ms = ms;
-  g->info.nomatch_cells = counters[kCtrNoMatch * 32];
+  g->info.nomatch_cells = nband - nfin[0] - nslot[1];   // band cells neither final at level 0 nor split
   g->info.overflow_cells = counters[kCtrOverflow * 32];
   g->info.fallback_fine = counters[kCtrFineFb * 32];
   g->info.fine_cells = (int64_t)fine_base[4] - g->info.fallback_fine;
@@ -553,6 +549,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   // the target's candidate cells answer the search first (k_cell_lookup)
   j.grid_on = grid_active(c) ? 1 : 0;
   if (j.grid_on) {
+    j.task_cap_r = 0;   // the walk's few sub-groups scan their leaves inline (no k_nn_scan launch)
     j.grid = c->tgt.cloud->grid->dev;
     const FbLayout fl(c->src.cloud->n);
     char* u = c->fb.as<char>();
@@ -1067,6 +1064,7 @@ gicp_status gicp_clear_source(gicp_ctx* c) {
 gicp_status gicp_clear_target(gicp_ctx* c) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
   c->tgt = Side();
+  c->tie_ref.reset();   // a slab's whole-target tie order belongs to the cleared target
   invalidate_align(c);
   return GICP_OK;
 }
@@ -1135,6 +1133,7 @@ gicp_status gicp_has_covariances(const gicp_ctx* c, int side, int* has) {
 gicp_status gicp_swap_source_target(gicp_ctx* c) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
   std::swap(c->src, c->tgt);  // clouds, indices and covariances (:100-102)
+  c->tie_ref.reset();         // the whole-target tie order (and its index map) belonged to the old target
   invalidate_align(c);        // correspondences_.clear() (:104-105)
   return GICP_OK;
 }
@@ -1605,10 +1604,29 @@ gicp_status gicp_set_tie_target(gicp_ctx* c, const float* xyz, size_t n, size_t 
   }
   if (!xyz || !local_index) return fail(GICP_EINVAL, "null argument");
   if (!c->tgt.cloud || (int)n_local != c->tgt.cloud->n) return fail(GICP_ESTATE, "set the local target first (n_local = its size)");
-  for (size_t i = 0; i < n_local; ++i)
+  std::vector<unsigned char> seen(n, 0);
+  for (size_t i = 0; i < n_local; ++i) {
     if (local_index[i] < 0 || (size_t)local_index[i] >= n) return fail(GICP_EINVAL, "local_index out of range");
+    if (seen[(size_t)local_index[i]]++) return fail(GICP_EINVAL, "local_index is not one-to-one");
+  }
   gicp_status s = set_device(c);
   if (s) return s;
+  {
+    // the local target's point i must be the whole cloud's point local_index[i]
+    // (a tied correspondence is remapped through this index)
+    std::vector<float4> lp((size_t)n_local);
+    HIP_TRY(hipMemcpyAsync(lp.data(), c->tgt.cloud->pts.p, sizeof(float4) * n_local, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(xyz);
+    for (size_t j = 0; j < n_local; ++j) {
+      int orig;
+      std::memcpy(&orig, &lp[j].w, sizeof(int));
+      float w[3];
+      std::memcpy(w, base + (size_t)local_index[orig] * stride, sizeof(w));
+      if (w[0] != lp[j].x || w[1] != lp[j].y || w[2] != lp[j].z)
+        return fail(GICP_EINVAL, "local_index does not map the local target's points onto the whole cloud's");
+    }
+  }
   std::shared_ptr<CloudData> cd;
   s = build_cloud(c, xyz, n, stride, &cd);
   if (s) return s;

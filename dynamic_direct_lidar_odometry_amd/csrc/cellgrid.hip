@@ -137,6 +137,8 @@ __device__ __forceinline__ unsigned long long wave_umin64(unsigned long long v) 
 }
 
 constexpr unsigned kHdrSkip = 0xffffffffu;       // hdr count: no list (NoMatch cell, dir final)
+constexpr int kNoMatchList = -2;                 // direct_list: no target point within the bound of the box
+constexpr int kRepNone = 0x7f7f7f7f;             // no representative (the host fills with bytes 0x7f)
 constexpr unsigned kHdrOverflow = 0xfffffffeu;   // hdr count: more than kCgCandMax points (split directly)
 
 // A node box entirely dominated by d over the cell box (every point of it
@@ -267,6 +269,7 @@ __device__ __forceinline__ int direct_list(const CgBuild& b, const CgBox& B, flo
   Rel dom[10];
   float dmin2 = far2(p0, hb);
   dom[9] = p0;
+  float cd2 = INFINITY;   // the centre's nearest squared distance (fp32) within reach
 #pragma unroll
   for (int q = 0; q < 9; ++q) {
     const unsigned long long kq = wave_umin64(ck[q]);
@@ -274,10 +277,16 @@ __device__ __forceinline__ int direct_list(const CgBuild& b, const CgBox& B, flo
     if (kq != ~0ull) {
       const float4 p = ldg4(c.pts, (int)(unsigned)kq);
       d = rel(B, p.x, p.y, p.z);
+      if (q == 8) cd2 = __uint_as_float((unsigned)(kq >> 32));
     }
     dom[q] = d;
     dmin2 = fminf(dmin2, far2(d, hb));
   }
+  // every point of the box is farther than the bound from every target point:
+  // the centre's nearest distance (exact within reach: pass 1 examined every
+  // point p0 does not dominate, and the nearest is never dominated) minus the
+  // half diagonal exceeds it
+  if (sqrt((double)cd2 / (1.0 + 1e-6)) - 1.7320509 * B.hb - 1e-5 > b.capm) return kNoMatchList;
   // pass 2: the kept points
   const float Rsq = list_radius2(dmin2, b.capm);
   region(Rsq, qlo, qhi);
@@ -312,19 +321,28 @@ __device__ __forceinline__ int direct_list(const CgBuild& b, const CgBox& B, flo
 // point), and the band cells in 4x4x4-blocked order (spatially coherent
 // wavefronts for the nearest-point pass).
 __global__ __launch_bounds__(256) void k_cg_occ(const CgBuild* __restrict__ bp, int n) {
+  // representative of every occupied coarse cell: its lowest sorted position
+  // (the Morton-sorted points of a cell form few runs: one atomic per run)
   const CgBuild& b = *bp;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float4 p = ldg4(b.tgt.pts, i);
-  const int cx = min(max((int)floorf((p.x - b.fox) * b.inv_s), 0), b.nx - 1);
-  const int cy = min(max((int)floorf((p.y - b.foy) * b.inv_s), 0), b.ny - 1);
-  const int cz = min(max((int)floorf((p.z - b.foz) * b.inv_s), 0), b.nz - 1);
-  b.occ[((long)cx * b.ny + cy) * b.nz + cz] = 1;
+  auto cell_of = [&](int j) {
+    const float4 p = ldg4(b.tgt.pts, j);
+    const int cx = min(max((int)floorf((p.x - b.fox) * b.inv_s), 0), b.nx - 1);
+    const int cy = min(max((int)floorf((p.y - b.foy) * b.inv_s), 0), b.ny - 1);
+    const int cz = min(max((int)floorf((p.z - b.foz) * b.inv_s), 0), b.nz - 1);
+    return ((long)cx * b.ny + cy) * b.nz + cz;
+  };
+  const long c = cell_of(i);
+  if (i == 0 || cell_of(i - 1) != c) atomicMin(b.rep + c, i);
 }
 
-__global__ __launch_bounds__(256) void k_cg_dilate(const CgBuild* __restrict__ bp, int axis,
-                                                   const unsigned char* __restrict__ in, unsigned char* __restrict__ out,
-                                                   long ncells) {
+// Separable propagation of the nearest representative along one axis within
+// r cells (the three passes give every cell within Chebyshev distance r of an
+// occupied cell a near target point: the band, and each band cell's first
+// dominator p0; any target point is a valid dominator, so near is enough)
+__global__ __launch_bounds__(256) void k_cg_prop(const CgBuild* __restrict__ bp, int axis, const int* __restrict__ in,
+                                                 int* __restrict__ out, long ncells) {
   const CgBuild& b = *bp;
   const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ncells) return;
@@ -333,19 +351,31 @@ __global__ __launch_bounds__(256) void k_cg_dilate(const CgBuild* __restrict__ b
   const int v = axis == 0 ? cx : axis == 1 ? cy : cz;
   const int nv = axis == 0 ? b.nx : axis == 1 ? b.ny : b.nz;
   const long stride = axis == 0 ? (long)b.ny * b.nz : axis == 1 ? (long)b.nz : 1;
-  unsigned char o = 0;
+  const float ccx = b.fox + ((float)cx + 0.5f) / b.inv_s, ccy = b.foy + ((float)cy + 0.5f) / b.inv_s,
+              ccz = b.foz + ((float)cz + 0.5f) / b.inv_s;
+  int best = kRepNone;
+  float bd = INFINITY;
   const int lo = max(v - b.r, 0), hi = min(v + b.r, nv - 1);
-  for (int k = lo; k <= hi && !o; ++k) o = in[c + (long)(k - v) * stride];
-  out[c] = o;
+  for (int k = lo; k <= hi; ++k) {
+    const int r = in[c + (long)(k - v) * stride];
+    if (r == kRepNone) continue;
+    const float4 p = ldg4(b.tgt.pts, r);
+    const float d = dist2(ccx, ccy, ccz, p.x, p.y, p.z);
+    if (d < bd) {
+      bd = d;
+      best = r;
+    }
+  }
+  out[c] = best;
 }
 
-__global__ __launch_bounds__(256) void k_cg_dir_fill(unsigned* __restrict__ dir, const unsigned char* __restrict__ band,
+__global__ __launch_bounds__(256) void k_cg_dir_fill(unsigned* __restrict__ dir, const int* __restrict__ band,
                                                      long ncells, unsigned outside) {
   const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < ncells) dir[c] = band[c] ? kCgFallback : outside;
+  if (c < ncells) dir[c] = band[c] != kRepNone ? kCgFallback : outside;
 }
 
-__global__ __launch_bounds__(256) void k_cg_band_flags(const CgBuild* __restrict__ bp, const unsigned char* __restrict__ band,
+__global__ __launch_bounds__(256) void k_cg_band_flags(const CgBuild* __restrict__ bp, const int* __restrict__ band,
                                                        unsigned char* __restrict__ flags, long nblocked) {
   const CgBuild& b = *bp;
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -356,7 +386,7 @@ __global__ __launch_bounds__(256) void k_cg_band_flags(const CgBuild* __restrict
   const int bz = (int)(blk % nbz), by = (int)((blk / nbz) % nby), bx = (int)(blk / ((long)nbz * nby));
   const int cx = 4 * bx + (w >> 4), cy = 4 * by + ((w >> 2) & 3), cz = 4 * bz + (w & 3);
   unsigned char f = 0;
-  if (cx < b.nx && cy < b.ny && cz < b.nz) f = band[((long)cx * b.ny + cy) * b.nz + cz];
+  if (cx < b.nx && cy < b.ny && cz < b.nz) f = band[((long)cx * b.ny + cy) * b.nz + cz] != kRepNone;
   flags[id] = f;
 }
 
@@ -371,9 +401,9 @@ __global__ __launch_bounds__(256) void k_cg_centers(CgBuild* __restrict__ bp, in
   const int w = (int)(id & 63);
   const int bz = (int)(blk % nbz), by = (int)((blk / nbz) % nby), bx = (int)(blk / ((long)nbz * nby));
   const int cx = 4 * bx + (w >> 4), cy = 4 * by + ((w >> 2) & 3), cz = 4 * bz + (w & 3);
-  b.band[k] = (int)(((long)cx * b.ny + cy) * b.nz + cz);
-  b.centers[k] = make_float4((float)(b.ox + (cx + 0.5) * b.s), (float)(b.oy + (cy + 0.5) * b.s),
-                             (float)(b.oz + (cz + 0.5) * b.s), 0.f);
+  const long cell = ((long)cx * b.ny + cy) * b.nz + cz;
+  b.band[k] = (int)cell;
+  b.cnn[k] = b.rep_final[cell];   // sorted position of a near target point
 }
 
 // ---------------------------------------------------------------------------
@@ -395,17 +425,15 @@ __global__ __launch_bounds__(64 * kCgWaves) void k_cg_coarse(const CgBuild* __re
     int cx, cy, cz;
     cell_coords(b, cell, cx, cy, cz);
     const CgBox B = fine_box(b, cx, cy, cz, 0, 0, 0, 0);
-    // no target point within the bound of any point of the cell
-    const double u = sqrt((double)b.cnd[bi] / (1.0 + 1e-6)) - 1e-5;
-    if (u - 1.7320509 * B.hb - 1e-5 > b.capm) {
+    const float4 p0 = ldg4(c.pts, b.cnn[bi]);
+    const int n = direct_list(b, B, p0, cand);
+    if (n == kNoMatchList) {   // no target point within the bound of any point of the cell
       if (lane == 0) {
         b.dir[cell] = kCgNoMatch;
         L0.hdr[bi] = make_uint2(0u, kHdrSkip);
       }
       continue;
     }
-    const float4 p0 = ldg4(c.pts, c.inv_perm[b.cnn[bi]]);
-    const int n = direct_list(b, B, p0, cand);
     if (n < 0) {   // more than kCgCandMax points: the cell is split (level 1, direct)
       if (lane == 0) {
         L0.hdr[bi] = make_uint2(0u, kHdrOverflow);
@@ -446,7 +474,6 @@ __global__ __launch_bounds__(256) void k_cg_decide(CgBuild* __restrict__ bp, int
       x = 1;
     } else if (h.y == 0u) {
       b.dir[b.band[s]] = kCgNoMatch;
-      atomicAdd(b.ctr + kCtrNoMatch * 32, 1u);
     } else if ((int)h.y <= b.lmax) {
       f = 1;
     } else {
@@ -507,13 +534,14 @@ __global__ __launch_bounds__(64 * kCgWaves) void k_cg_refine(const CgBuild* __re
     const float hq = 0.5f * hp;   // child centre offset
     if (ph.y == kHdrOverflow) {
       // the parent kept more than kCgCandMax points: each child straight from the target
-      const float4 p0w = ldg4(c.pts, c.inv_perm[b.cnn[bi]]);
+      const float4 p0w = ldg4(c.pts, b.cnn[bi]);
       int cmx = 0;
 #pragma unroll 1
       for (int o = 0; o < 8; ++o) {
         const int fx = 2 * px + ((o >> 2) & 1), fy = 2 * py + ((o >> 1) & 1), fz = 2 * pz + (o & 1);
         const CgBox CB = fine_box(b, cx, cy, cz, level, fx, fy, fz);
-        const int nk = direct_list(b, CB, p0w, cand);
+        int nk = direct_list(b, CB, p0w, cand);
+        if (nk == kNoMatchList) nk = 0;   // no point within the bound: an empty list
         uint2 h = make_uint2(0u, kHdrOverflow);
         if (nk < 0) {
           cmx = 0x7fffffff;
@@ -541,9 +569,13 @@ __global__ __launch_bounds__(64 * kCgWaves) void k_cg_refine(const CgBuild* __re
     for (int o = 0; o < 8; ++o) cnt[o] = 0;
     if (n > 0 && n <= kCgCandMax) {
       // nearest list point of the 27 lattice points (children's corners) and the 8 child centres
-      unsigned long long lk[35];
+      // keys: the squared distance's bits with the low 11 replaced by the list
+      // index (n <= kCgCandMax = 2^11): a dominator need not be the exact
+      // nearest point, and a 32-bit key reduces with DPP
+      static_assert(kCgCandMax <= 2048, "11-bit list index in the keys");
+      unsigned lk[35];
 #pragma unroll
-      for (int q = 0; q < 35; ++q) lk[q] = ~0ull;
+      for (int q = 0; q < 35; ++q) lk[q] = 0xffffffffu;
       for (int k = lane; k < n; k += 64) {
         const float4 p = ldg4(c.pts, P.pool[ph.x + k]);
         const Rel a = rel(PB, p.x, p.y, p.z);
@@ -561,16 +593,17 @@ __global__ __launch_bounds__(64 * kCgWaves) void k_cg_refine(const CgBuild* __re
             qz = (o & 1) ? hq : -hq;
           }
           const float dx = a.x - qx, dy = a.y - qy, dz = a.z - qz;
-          lk[q] = umin64(lk[q], dkey(dx * dx + dy * dy + dz * dz, k));
+          lk[q] = min(lk[q], (__float_as_uint(dx * dx + dy * dy + dz * dz) & ~0x7ffu) | (unsigned)k);
         }
       }
       // the 35 nearest points, parent-centred, in LDS (wave-uniform reads)
       Rel* const lat = lat_all[wib];
 #pragma unroll
       for (int q = 0; q < 35; ++q) {
-        const unsigned long long kq = wave_umin64(lk[q]);
+        // non-negative float bit patterns order like unsigned ints (all ones: NaN, ignored by fminf)
+        const unsigned kq = __float_as_uint(wave_min(__uint_as_float(lk[q])));
         if (lane == q) {
-          const float4 p = ldg4(c.pts, P.pool[ph.x + (int)(unsigned)kq]);
+          const float4 p = ldg4(c.pts, P.pool[ph.x + (int)(kq & 0x7ffu)]);
           lat[q] = rel(PB, p.x, p.y, p.z);
         }
       }
@@ -754,19 +787,16 @@ __global__ __launch_bounds__(64 * kCgWaves) void k_cg_emit_write(const CgBuild* 
 // launchers
 static int cdiv_l(long a, long b) { return (int)((a + b - 1) / b); }
 
-void launch_cg_occ(hipStream_t s, const CgBuild* db, int n, long ncells) {
-  (void)ncells;
+void launch_cg_occ(hipStream_t s, const CgBuild* db, int n) {
   k_cg_occ<<<cdiv_l(n, 256), 256, 0, s>>>(db, n);
 }
-void launch_cg_dilate(hipStream_t s, const CgBuild* db, int axis, const unsigned char* in, unsigned char* out,
-                      long ncells) {
-  k_cg_dilate<<<cdiv_l(ncells, 256), 256, 0, s>>>(db, axis, in, out, ncells);
+void launch_cg_prop(hipStream_t s, const CgBuild* db, int axis, const int* in, int* out, long ncells) {
+  k_cg_prop<<<cdiv_l(ncells, 256), 256, 0, s>>>(db, axis, in, out, ncells);
 }
-void launch_cg_dir_fill(hipStream_t s, unsigned* dir, const unsigned char* band, long ncells, unsigned outside) {
+void launch_cg_dir_fill(hipStream_t s, unsigned* dir, const int* band, long ncells, unsigned outside) {
   k_cg_dir_fill<<<cdiv_l(ncells, 256), 256, 0, s>>>(dir, band, ncells, outside);
 }
-void launch_cg_band_flags(hipStream_t s, const CgBuild* db, const unsigned char* band, unsigned char* flags,
-                          long nblocked) {
+void launch_cg_band_flags(hipStream_t s, const CgBuild* db, const int* band, unsigned char* flags, long nblocked) {
   k_cg_band_flags<<<cdiv_l(nblocked, 256), 256, 0, s>>>(db, band, flags, nblocked);
 }
 void launch_cg_centers(hipStream_t s, CgBuild* db, int nband) {

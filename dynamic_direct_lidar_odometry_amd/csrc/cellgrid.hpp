@@ -58,13 +58,12 @@ struct CgBuild {
   double nomatch_dist;      // a non-band cell has no target point within this distance
   int lmax;                 // a level is final when all its lists have <= lmax points
   int lcap;                 // finest level: a longer list is not stored (walk)
-  unsigned char* occ;       // [ncells] occupancy, then the band flags
-  unsigned char* tmp;       // [ncells] dilation scratch
+  int* rep;                 // [ncells] a target point of each occupied cell (sorted position; INT_MAX: none)
+  int* rep_tmp;             // [ncells] propagation scratch
+  int* rep_final;           // [ncells] a near target point within r cells (Chebyshev), INT_MAX: none (= not band)
   unsigned* dir;            // [ncells] output
   int* band;                // [ncells] band cell ids, 4x4x4-blocked order
-  float4* centers;          // [nband] centre queries of the nearest-point pass
-  int* cnn;                 // [nband] nearest target point (original index)
-  float* cnd;               // [nband] its squared distance
+  int* cnn;                 // [nband] the band cell's near target point (sorted position)
   unsigned* ctr;            // [kCgCounters]
   CgLevel lv[kCgMaxLevel + 1];
   int2* finals;             // (level, slot)
@@ -80,10 +79,10 @@ struct CgBuild {
 constexpr int kCgShardsHost = 16;
 constexpr size_t kCgCtrWords = (size_t)(kCgCounters + (kCgMaxLevel + 1) * kCgShardsHost) * 32;
 
-void launch_cg_occ(hipStream_t s, const CgBuild* db, int n, long ncells);
-void launch_cg_dilate(hipStream_t s, const CgBuild* db, int axis, const unsigned char* in, unsigned char* out, long ncells);
-void launch_cg_dir_fill(hipStream_t s, unsigned* dir, const unsigned char* band, long ncells, unsigned outside);
-void launch_cg_band_flags(hipStream_t s, const CgBuild* db, const unsigned char* band, unsigned char* flags, long nblocked);
+void launch_cg_occ(hipStream_t s, const CgBuild* db, int n);
+void launch_cg_prop(hipStream_t s, const CgBuild* db, int axis, const int* in, int* out, long ncells);
+void launch_cg_dir_fill(hipStream_t s, unsigned* dir, const int* band, long ncells, unsigned outside);
+void launch_cg_band_flags(hipStream_t s, const CgBuild* db, const int* band, unsigned char* flags, long nblocked);
 void launch_cg_centers(hipStream_t s, CgBuild* db, int nband);
 void launch_cg_coarse(hipStream_t s, const CgBuild* db, int nband);
 void launch_cg_decide(hipStream_t s, CgBuild* db, int level, int nslots, unsigned char* fl_final, unsigned char* fl_next);

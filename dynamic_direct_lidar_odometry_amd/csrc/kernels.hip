@@ -970,15 +970,17 @@ __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_d
 // exceeded the cap) marks its 16-query sub-group for the walk (fb_mask bit,
 // fb_list entry); the walk then searches only those queries.
 __global__ __launch_bounds__(256) void k_cell_lookup(const AlignJob* __restrict__ job) {
+  constexpr int Q = kTaskQ;   // queries per wavefront; 64 / Q lanes (slices) scan each list
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
   const CloudDev src = job->src;
   const CellGridDev G = job->grid;
   const float cap2 = job->cap2;
   const int lane = lane_id();
+  const int qi = lane % Q, sl = lane / Q;
   const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
-  const int n64 = (src.n + 63) >> 6;
+  const int ngroups = (src.n + Q - 1) / Q;
   const int own_axis = job->own_axis;
   const float own_lo = job->own_lo, own_hi = job->own_hi;
   const int own_mod = job->own_mod, own_rem = job->own_rem;
@@ -986,14 +988,13 @@ __global__ __launch_bounds__(256) void k_cell_lookup(const AlignJob* __restrict_
   float Rf[9], tf[3];
   for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
   for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
-  for (int w = wave; w < n64; w += nwaves) {
-    const int i = w * 64 + lane;
+  for (int g = wave; g < ngroups; g += nwaves) {
+    const int i = g * Q + qi;
     const bool inrange = i < src.n;
     const float4 a = ldg4(src.pts, inrange ? i : src.n - 1);
     const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
     const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
     const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
-    const int g = i >> 4;
     const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
     const bool owned = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi)) &&
                        (own_mod == 0 || (g % own_mod) == own_rem);
@@ -1023,18 +1024,21 @@ __global__ __launch_bounds__(256) void k_cell_lookup(const AlignJob* __restrict_
         }
       }
     }
-    // the list's (distance, position) minimum and the smallest other distance
+    // this slice's part of the list: the (distance, position) minimum and the
+    // smallest distance of its other points
     unsigned long long bk = ~0ull;
     float d2 = INFINITY;
-    for (unsigned k = 0; k < cnt; k += 4) {
-      float4 p[4];
+    constexpr int kU = 4;   // loads in flight per lane
+    for (unsigned k = sl; k < cnt; k += kU * (64 / Q)) {
+      float4 pp[kU];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) p[j] = ldg4(G.ent, off + min(k + j, cnt - 1));
+      for (int j = 0; j < kU; ++j) pp[j] = ldg4(G.ent, off + min(k + j * (64 / Q), cnt - 1));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (k + j < cnt) {
-          const float dd = dist2(qx, qy, qz, p[j].x, p[j].y, p[j].z);
-          const unsigned long long kk = dkey(dd, __float_as_int(p[j].w));
+      for (int j = 0; j < kU; ++j) {
+        const float4 p = pp[j];
+        if (k + j * (64 / Q) < cnt) {
+          const float dd = dist2(qx, qy, qz, p.x, p.y, p.z);
+          const unsigned long long kk = dkey(dd, __float_as_int(p.w));
           if (kk < bk) {
             if (bk != ~0ull) d2 = fminf(d2, __uint_as_float((unsigned)(bk >> 32)));
             bk = kk;
@@ -1044,7 +1048,19 @@ __global__ __launch_bounds__(256) void k_cell_lookup(const AlignJob* __restrict_
         }
       }
     }
-    if (inrange && !walk) {
+    // merge the slices: the loser's distance joins the others'
+    static_assert(Q == 16, "slice merge over lanes l ^ 16, l ^ 32");
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const unsigned long long ob = h == 0 ? xor_min64<16>(bk) : xor_min64<32>(bk);   // min of the pair
+      const unsigned long long other = h == 0 ? __shfl_xor(bk, 16) : __shfl_xor(bk, 32);
+      const float od2 = h == 0 ? __shfl_xor(d2, 16) : __shfl_xor(d2, 32);
+      const unsigned long long lose = bk < other ? other : bk;
+      d2 = fminf(d2, od2);
+      if (lose != ~0ull) d2 = fminf(d2, __uint_as_float((unsigned)(lose >> 32)));
+      bk = ob;
+    }
+    if (sl == 0 && inrange && !walk) {
       job->qstate[i] = make_float4(qx, qy, qz, -1.f);
       const unsigned long long key = owned ? umin64(bk, dkey(cap2, -1)) : dkey(INFINITY, -1);
       job->key[i] = key;
@@ -1055,23 +1071,13 @@ __global__ __launch_bounds__(256) void k_cell_lookup(const AlignJob* __restrict_
       }
       if (job->tie_scan == 3) job->key2[i] = mirror_key(key);
     }
-    // sub-groups with a query for the walk
-    const unsigned long long wb = __ballot(walk);
-    if (wb) {
-      const int r = lane >> 4;
-      const unsigned m16 = (unsigned)(wb >> (16 * r)) & 0xffffu;
-      const int nz = ((wb & 0xffffull) != 0) + ((wb & 0xffff0000ull) != 0) + ((wb & 0xffff00000000ull) != 0) +
-                     ((wb >> 48) != 0);
-      const int seg = w & (kFbSegs - 1);
-      int base = 0;
-      if (lane == 0) base = (int)atomicAdd(job->fb_count + seg * 32, (unsigned)nz);
-      base = __builtin_amdgcn_readfirstlane(base);
-      if ((lane & 15) == 0 && m16) {
-        int rank = 0;
-        for (int t = 0; t < r; ++t) rank += ((wb >> (16 * t)) & 0xffffull) != 0;
-        job->fb_list[seg * job->fb_seg_cap + base + rank] = g;
-        job->fb_mask[g] = (unsigned short)m16;
-      }
+    // a sub-group with a query for the walk
+    const unsigned m16 = (unsigned)__ballot(walk && sl == 0) & 0xffffu;
+    if (m16 && lane == 0) {
+      const int seg = g & (kFbSegs - 1);
+      const int slot = (int)atomicAdd(job->fb_count + seg * 32, 1u);
+      job->fb_list[seg * job->fb_seg_cap + slot] = g;
+      job->fb_mask[g] = (unsigned short)m16;
     }
   }
 }
@@ -1138,12 +1144,9 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   TaskLds* const TL = reinterpret_cast<TaskLds*>(dsm) + __builtin_amdgcn_readfirstlane(wib);   // scalar base
   f4v* const upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kTaskLdsBytes);
-  if constexpr (FUSED) {
-    fill_upper(tgt, upper);
-    __syncthreads();
-  }
   // candidate cells (k_cell_lookup): only the listed sub-groups, only their
-  // unanswered queries; the answered ones keep the lookup's outputs
+  // unanswered queries; the answered ones keep the lookup's outputs.  Their
+  // tasks are scanned inline (task_cap_r = 0: no k_nn_scan launch).
   const int grid_on = job->grid_on;
   int seg_end[kFbSegs];
   int nitems = ngroups;
@@ -1154,6 +1157,11 @@ __global__ __launch_bounds__(256, MINW) void k_nn_seed(const AlignJob* __restric
       nitems += (int)job->fb_count[sg * 32];
       seg_end[sg] = nitems;
     }
+    if ((int)blockIdx.x * kLinWaves >= nitems) return;   // the whole block (uniform): before the LDS prologue
+  }
+  if constexpr (FUSED) {
+    fill_upper(tgt, upper);
+    __syncthreads();
   }
   for (int item = wave; item < nitems; item += nwaves_total) {
     int g = item;
@@ -3209,7 +3217,7 @@ LinGeom linearize_geometry(int nsrc, int tgt_upper) {
   g.scan_blocks = scan_blocks(gcap * kSearchQ);                   // any grid is exact
   g.mom_blocks = moment_blocks(cdiv(std::max(nsrc, 1), 32768) * 32768);   // grid-stride; = the slab rows
   g.lds_boxes = std::min(2048, cdiv(std::max(tgt_upper, 1), 128) * 128);   // >= the target's upper boxes
-  g.lookup_blocks = std::max(1, gcap * kSearchQ / 256);                    // one query per lane
+  g.lookup_blocks = gcap / kLinWaves;                                      // one 16-query sub-group per wave
   return g;
 }
 
@@ -3222,20 +3230,27 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
                      occ_scan = env_knob("DDLO_OCC_SCAN", 5);
     static const int fused = env_knob("DDLO_FUSED_SEED", 1);   // 0: separate seed and collect kernels (A/B)
     const size_t lds = collect_lds_bytes(g.lds_boxes);
+    // with candidate cells the walk gets the few sub-groups without a list:
+    // small grids (the kernels are grid-stride loops), so that the usual
+    // empty launches cost little
+    const int seed_blocks = g.grid ? std::min(g.seed_blocks, 256) : g.seed_blocks;
+    const int scan_blocks = g.grid ? std::min(g.scan_blocks, 8 * kTaskRegions / kScanWaves) : g.scan_blocks;
     if (fused) {
       static const int occ_fused = env_knob("DDLO_OCC_FUSED", 4);
-      if (occ_fused == 2) k_nn_seed<2, true><<<g.seed_blocks, 64 * kLinWaves, lds, s>>>(job);
-      else if (occ_fused == 4) k_nn_seed<4, true><<<g.seed_blocks, 64 * kLinWaves, lds, s>>>(job);
-      else k_nn_seed<3, true><<<g.seed_blocks, 64 * kLinWaves, lds, s>>>(job);
+      if (occ_fused == 2) k_nn_seed<2, true><<<seed_blocks, 64 * kLinWaves, lds, s>>>(job);
+      else if (occ_fused == 4) k_nn_seed<4, true><<<seed_blocks, 64 * kLinWaves, lds, s>>>(job);
+      else k_nn_seed<3, true><<<seed_blocks, 64 * kLinWaves, lds, s>>>(job);
     } else {
       if (occ_seed == 6) k_nn_seed<6, false><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);
       else k_nn_seed<4, false><<<g.seed_blocks, 64 * kLinWaves, 0, s>>>(job);
       if (occ_col == 4) k_nn_collect<4><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
       else k_nn_collect<3><<<g.collect_blocks, 64 * kLinWaves, lds, s>>>(job);
     }
-    if (occ_scan == 6) k_nn_scan<6><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
-    else if (occ_scan == 5) k_nn_scan<5, 6><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);   // 6-task batches: 7.5 KB LDS per wave
-    else k_nn_scan<4><<<g.scan_blocks, 64 * kScanWaves, 0, s>>>(job);
+    if (g.grid && fused) {
+      // the walk scanned its (few) sub-groups' tasks inline (AlignJob::task_cap_r = 0)
+    } else if (occ_scan == 6) k_nn_scan<6><<<scan_blocks, 64 * kScanWaves, 0, s>>>(job);
+    else if (occ_scan == 5) k_nn_scan<5, 6><<<scan_blocks, 64 * kScanWaves, 0, s>>>(job);   // 6-task batches: 7.5 KB LDS per wave
+    else k_nn_scan<4><<<scan_blocks, 64 * kScanWaves, 0, s>>>(job);
   }
   if (g.fuse_lm) k_moments<true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
   else k_moments<false><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);

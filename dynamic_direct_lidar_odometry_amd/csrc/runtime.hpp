@@ -432,6 +432,7 @@ struct gicp_ctx {
   hipEvent_t st_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool st_tree = false;          // the last compute_cov built a tree (events 2, 3 recorded)
   bool st_resolve = false;       // ... and ran the tie resolvers (events 4, 5)
+  bool st_in_cov = false;        // a profiled compute_cov is running: only its own tree build is timed
 };
 
 namespace ddlo {
@@ -582,7 +583,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   }
   if (!t->ready) HIP_TRY(hipEventCreateWithFlags(&t->ready, hipEventDisableTiming));
   t->n = n;
-  const bool timed = c->profiling && c->st_ev[2] && stop < 0 && !off;
+  const bool timed = c->profiling && c->st_in_cov && c->st_ev[2] && stop < 0 && !off;
   if (timed) HIP_TRY(hipEventRecord(c->st_ev[2], s));
   // grids sized for a bucket of 16k points: one captured build graph serves
   // every cloud of the bucket (the kernels read the descriptor, and n, from
@@ -808,7 +809,15 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   HIP_TRY(cv->cov6.ensure(sizeof(double) * 6 * (size_t)cv->n));
   if (c->profiling && !c->st_ev[0])
     for (auto& e : c->st_ev) HIP_TRY(hipEventCreate(&e));
+  // stage times: only what this pass records (a tree built earlier, e.g. with
+  // the index, is not this pass's; nothing is reported from an older pass)
   c->st_tree = false;
+  c->st_resolve = false;
+  struct InCov {
+    gicp_ctx* c;
+    ~InCov() { c->st_in_cov = false; }
+  } in_cov{c};
+  c->st_in_cov = c->profiling;
   // DDLO_COV_TASKS=1: the task-based kNN (knn_tasks.hip) — exact, but not
   // faster than the lane-per-query kernel on the cfg 5 clouds
   const char* tv = std::getenv("DDLO_COV_TASKS");
@@ -897,7 +906,7 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     return fail(GICP_EINVAL, "unsupported k");
   }
   if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[1], c->stream));
-  c->st_resolve = c->tie_exact;
+  c->st_resolve = c->tie_exact && c->profiling;
   if (c->tie_exact) {
     if (lazy) {
       const int n = side.cloud->n;
@@ -911,8 +920,9 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
       const NfTreeData& tp = gated ? *c->nf_gated : *side.cloud->nfp;
       HIP_TRY(nftree_join(tp, c->stream));
       if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[4], c->stream));
-      launch_nf_lazy(c->stream, tp.dev(), cd, nullptr, tl, k, c->params.regularization, cv->cov6.as<double>(), nullptr,
-                     nullptr, c->lazy_buf.p, wgs, tp.status.as<int>(), c->nf_err.as<int>());
+      if (!launch_nf_lazy(c->stream, tp.dev(), cd, nullptr, tl, k, c->params.regularization, cv->cov6.as<double>(),
+                          nullptr, nullptr, c->lazy_buf.p, wgs, tp.status.as<int>(), c->nf_err.as<int>()))
+        return fail(GICP_EINVAL, "nanoflann tie order: the lazy tie search cannot run (k > 64 or no partial tree)");
       if (c->profiling) HIP_TRY(hipEventRecord(c->st_ev[5], c->stream));
       c->lazy_wgs_last = wgs;
     } else {

@@ -307,8 +307,10 @@ gicp_status gicp_set_shard(struct gicp_ctx* ctx, int axis, float lo, float hi);
  * point i (the cloud of the last gicp_set_target), its index local_index[i]
  * in that whole cloud: tied correspondences are then re-run through the WHOLE
  * target's nanoflann tree, as the unsharded reference resolves them.  The
- * tree is built here, once per submap; gicp_set_target drops it.  n = 0
- * removes it. */
+ * tree is built here, once per submap; gicp_set_target, gicp_clear_target
+ * and gicp_swap_source_target drop it.  local_index must be one-to-one and map
+ * every local point onto an identical point of the whole cloud (checked:
+ * GICP_EINVAL otherwise).  n = 0 removes it. */
 gicp_status gicp_set_tie_target(struct gicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes,
                                 const int32_t* local_index, size_t n_local);
 /* Interleaved sharding, for a target that fits every GPU (it is replicated):

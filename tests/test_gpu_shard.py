@@ -191,3 +191,51 @@ def test_slab_shards_tied_target(knn_golden, world):
         seen |= mine
         c.close()
     assert seen.all()
+
+
+@pytest.mark.parametrize("op", ["swap", "clear"])
+def test_tie_target_dropped_with_its_target(knn_golden, op):
+    """The whole-target tie order belongs to the target it was given for:
+    gicp_swap_source_target / gicp_clear_target drop it (the old index map
+    would re-map a tied correspondence into the wrong cloud).  After a swap
+    the ctx aligns the former target (a tied lattice) like a plain ctx; a bad
+    index map is rejected at gicp_set_tie_target."""
+    tgt = np.ascontiguousarray(knn_golden["lat_pts"])
+    src = np.ascontiguousarray(knn_golden["lat_q"])
+    par = dict(S2M, k_correspondences=10)
+    idx = np.arange(len(tgt), dtype=np.int32)[: len(tgt) // 2]
+    sub = np.ascontiguousarray(tgt[idx])
+    c = P.Context(0)
+    c.set_params(P.default_params(**par))
+    c.set_target(sub)
+    c.compute_covariances(TARGET)
+    with pytest.raises(P.GicpError):
+        c.set_tie_target(tgt, idx[::-1].copy())   # not the local points
+    with pytest.raises(P.GicpError):
+        bad = idx.copy()
+        bad[1] = bad[0]
+        c.set_tie_target(tgt, bad)                # not one-to-one
+    c.set_tie_target(tgt, idx)
+    c.set_source(src)
+    c.compute_covariances(SOURCE)
+    if op == "swap":
+        c.swap_source_target()   # the lattice queries become the target, the half lattice the source
+    else:
+        c.clear_target()
+        c.set_target(src)
+        c.compute_covariances(TARGET)
+        c.set_source(sub)
+        c.compute_covariances(SOURCE)
+    plain = P.Context(0)
+    plain.set_params(P.default_params(**par))
+    plain.set_target(src)
+    plain.compute_covariances(TARGET)
+    plain.set_source(sub)
+    plain.compute_covariances(SOURCE)
+    H, b, cost, nc = c.linearize(np.eye(4))
+    Hp, bp, costp, ncp = plain.linearize(np.eye(4))
+    np.testing.assert_array_equal(c.correspondences()[0], plain.correspondences()[0])
+    np.testing.assert_array_equal(H, Hp)
+    assert nc == ncp
+    c.close()
+    plain.close()
