@@ -101,13 +101,12 @@ int env_int(const char* name, int dflt) {
 // process, not on every align (host time between aligns).
 struct SearchKnobs {
   float split_extent, hard_extent, probe, probe_d, tri_mv, reuse_gap, reuse_gap0, reuse_rec_eps, reuse_rec_conv;
-  int list_flush, xcd_scan, pf_ratio, hard_blocks, prev_window, reuse, reuse_rec0, tie_scan, tie_ab;
+  int xcd_scan, pf_ratio, hard_blocks, prev_window, reuse, reuse_rec0, tie_scan, tie_ab;
 };
 const SearchKnobs& search_knobs() {
   static const SearchKnobs k = [] {
     SearchKnobs v;
     v.split_extent = env_float("DDLO_SPLIT_EXTENT", kSplitExtentDefault);
-    v.list_flush = (int)env_float("DDLO_LIST_FLUSH", 16.f);
     v.xcd_scan = env_int("DDLO_XCD_SCAN", 1);
     v.pf_ratio = env_int("DDLO_PF_RATIO", 2);
     v.hard_extent = env_float("DDLO_HARD_EXTENT", 4.0f);
@@ -116,7 +115,7 @@ const SearchKnobs& search_knobs() {
     v.tri_mv = env_float("DDLO_TRI_MV", 0.2f);
     v.probe = env_float("DDLO_PROBE", 1.0f);
     v.probe_d = env_float("DDLO_PROBE_D", 0.5f);
-    v.reuse = search_uses_tasks() ? env_int("DDLO_REUSE", 1) : 0;
+    v.reuse = env_int("DDLO_REUSE", 1);
     v.reuse_gap = env_float("DDLO_REUSE_GAP", 0.05f);
     v.reuse_gap0 = env_float("DDLO_REUSE_GAP0", 0.f);
     v.reuse_rec0 = env_int("DDLO_REUSE_REC0", 0);
@@ -161,7 +160,7 @@ float search_cap2(const gicp_params& p) {
 
 // The target's candidate cells answer this ctx's searches (same bound)
 bool grid_active(const gicp_ctx* c) {
-  if (!c->grid_mode || !c->tgt.cloud || !search_uses_tasks()) return false;
+  if (!c->grid_mode || !c->tgt.cloud) return false;
   const auto& g = c->tgt.cloud->grid;
   return g && g->ok && g->cap2 == search_cap2(c->params);
 }
@@ -187,7 +186,7 @@ struct FbLayout {
 constexpr double kGridCell = 0.4;
 constexpr double kGridMaxReach = 4.0;     // bounds beyond this: cells farther than it use the walk
 constexpr int kGridListMax = 32;
-constexpr int kGridListCap = 256;         // finest level: longer lists are not stored (the walk)
+constexpr int kGridListCap = kCgCandMax;  // finest level: longer lists are not stored (the walk)
 constexpr long kGridMaxCells = 48L << 20; // coarse cells (the directory is 4 B per cell)
 
 gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_ptr<CellGridData>* out) {
@@ -431,6 +430,7 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   d.ny = b.ny;
   d.nz = b.nz;
   d.outside_nomatch = outside_nomatch ? 1 : 0;
+  d.has_fallback = (g->info.fallback_fine > 0 || !outside_nomatch) ? 1 : 0;
   g->ok = true;
   return GICP_OK;
 }
@@ -438,7 +438,7 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
 // gicp_set_target_grid policy: build the target's candidate cells for this
 // ctx's bound (auto: at the second align against the same target and bound)
 gicp_status maybe_build_grid(gicp_ctx* c) {
-  if (!c->grid_mode || !c->tgt.cloud || !search_uses_tasks()) return GICP_OK;
+  if (!c->grid_mode || !c->tgt.cloud) return GICP_OK;
   CloudData& t = *c->tgt.cloud;
   const float cap2 = search_cap2(c->params);
   if (t.grid && t.grid->cap2 == cap2) return GICP_OK;   // built (or found too large) for this bound
@@ -453,6 +453,23 @@ gicp_status maybe_build_grid(gicp_ctx* c) {
   if (s) return s;
   t.grid = g;
   return GICP_OK;
+}
+
+// Just before k_align_init reads the pinned job: whole (job_full = 1) unless
+// only the guess changed since the job it last copied whole, whose device copy
+// is still in place (k_align_init alone writes the device job).
+void finalize_job(gicp_ctx* c) {
+  AlignJob& j = *c->job_host;
+  j.job_full = 0;
+  AlignJob probe = j;
+  std::memcpy(probe.guess_R, c->job_last.guess_R, sizeof(probe.guess_R));
+  std::memcpy(probe.guess_t, c->job_last.guess_t, sizeof(probe.guess_t));
+  probe.job_full = c->job_last.job_full;
+  if (!c->job_last_valid || std::memcmp(&probe, &c->job_last, sizeof(AlignJob)) != 0) {
+    j.job_full = 1;
+    c->job_last = j;
+    c->job_last_valid = true;
+  }
 }
 
 gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
@@ -509,7 +526,6 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
     j.sec = reinterpret_cast<unsigned*>(u + sl.sec);
     j.key2 = reinterpret_cast<unsigned long long*>(u + sl.key2);
   }
-  j.list_flush = kn.list_flush;
   j.xcd_scan = kn.xcd_scan;
   j.pf_ratio = kn.pf_ratio;
   j.hard_extent = kn.hard_extent;
@@ -532,7 +548,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   // search tracks the examined points' second distance; the target's tree,
   // when it exists, re-runs the tied queries.  Slab shards hold a subset of
   // the target, whose tree orders ties differently: Morton order there.
-  j.tie_detect = (c->tie_exact && search_uses_tasks() && (c->own_axis < 0 || c->tie_ref)) ? 1 : 0;
+  j.tie_detect = (c->tie_exact && (c->own_axis < 0 || c->tie_ref)) ? 1 : 0;
   j.tgt_nf = NfTreeDev{nullptr, nullptr, nullptr, 0};
   j.tgt_nf_status = nullptr;
   j.tie_map = nullptr;
@@ -567,6 +583,7 @@ LinGeom geometry(const gicp_ctx* c) {
   LinGeom g = linearize_geometry(c->src.cloud->n, c->tgt.cloud->upper_count());
   g.fuse_lm = !c->comm && lm_fusion_enabled();   // a sharded align all-reduces between the moments and the LM step
   g.grid = grid_active(c);
+  g.grid_walk = !g.grid || c->tgt.cloud->grid->dev.has_fallback != 0;
   return g;
 }
 
@@ -604,7 +621,7 @@ gicp_status prepare_align(gicp_ctx* c) {
   // front (every rank the same tree, so no rank ever re-runs alone and the
   // collectives stay matched); otherwise it is built only when an align
   // meets a tie (gicp_align).  The stream waits once for a tree's build.
-  if (c->tie_exact && (c->own_axis < 0 || c->tie_ref) && search_uses_tasks()) {
+  if (c->tie_exact && (c->own_axis < 0 || c->tie_ref)) {
     CloudData& tc = c->tie_ref ? *c->tie_ref : *c->tgt.cloud;
     if ((c->comm || c->tie_ref) && !tc.nf) {
       gicp_status s = ensure_nftree(c, tc, c->stream);
@@ -722,7 +739,8 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   const LinGeom g = geometry(c);
   (void)nblocks;   // = g.mom_blocks
   const std::array<long long, 8> key{{c->comm ? 1 : 0, (long long)(uintptr_t)jd, g.seed_blocks, g.collect_blocks,
-                                      g.scan_blocks, g.mom_blocks, g.lds_boxes, g.grid ? g.lookup_blocks : 0}};
+                                      g.scan_blocks, g.mom_blocks, g.lds_boxes,
+                                      g.grid ? (g.grid_walk ? 2L : 1L) * g.lookup_blocks : 0}};
   const bool use_graph = !c->comm || c->comm_graphs;
   const int first = std::max(1, std::min({c->predicted_iters, max_it, kMaxFirstChunk}));
   GraphSet* gs = nullptr;
@@ -1162,6 +1180,7 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
   for (;;) {
     s = fill_job(c, guess16, nblocks);
     if (s) return s;
+    finalize_job(c);
     const int max_it = c->job_host->max_iterations;
     end_ev = c->ev1;
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
@@ -1361,6 +1380,7 @@ gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, doubl
     c->job_host->optimizer = GICP_OPT_GAUSS_NEWTON;
     c->job_host->max_iterations = 1;
     c->job_host->fixed_iterations = 1;
+    finalize_job(c);
     AlignJob* jd = c->job_dev.as<AlignJob>();
     launch_align_init(c->stream, jd, c->job_host_dev);
     s = enqueue_iteration(c, jd, nblocks, nullptr);

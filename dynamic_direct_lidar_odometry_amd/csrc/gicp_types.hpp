@@ -109,6 +109,7 @@ struct CellGridDev {
   float ox, oy, oz, inv_s; // grid origin, 1 / coarse cell size
   int nx, ny, nz;
   int outside_nomatch;     // a query outside the grid box has no target point within the bound (else the walk)
+  int has_fallback;        // some cell has no list (or outside_nomatch is 0): the walk kernel stays in the graph
 };
 
 // Per-align device state (one per ctx, lives in device memory).
@@ -154,6 +155,8 @@ struct AlignJob {
   unsigned int* stats;     // optional per-wave diagnostics [wave][kStatFields] (nullptr = off)
   double guess_R[9];
   double guess_t[3];
+  long long job_full;      // k_align_init copies the whole job (1) or, when nothing else changed since the
+                           // previous align of the ctx, only guess_R / guess_t and this word (0)
   double max_corr2;        // max_correspondence_distance^2 (double compare)
   float cap2;              // nextafter(float(max_corr2), +inf), the search bound
   // fp64 copies of the seed kernel's float knobs (scalar loads where they are
@@ -182,7 +185,6 @@ struct AlignJob {
   int premom;
   double* mom;             // [kSlabStride]
   float split_extent;      // sub-range split threshold of a wave's union box (m)
-  int list_flush;          // search (collect-scan variant): leaf-list length that triggers an early scan
   // task-based correspondence search (nn_tasks.hpp)
   float4* qstate;                // [n_src] transformed query (x, y, z) + seed bound (< 0: inactive)
   unsigned long long* key;       // [n_src] (squared distance, sorted target position) of the best match

@@ -4,8 +4,9 @@
 //                       k_leaf_boxes, k_level_boxes   (radix sort: hipcub, capi.hip)
 //   K2 kNN-k covariance k_covariances<KCAP,EXACT>        calculate_covariances
 //                                                       nano_gicp_impl.hpp:373-441
-//   K3 correspondences  k_nn_search<Q>                  update_correspondences
-//                                                       :234-275 (1-NN part)
+//   K3 correspondences  k_cell_lookup (candidate cells,  update_correspondences
+//                       cellgrid.hip), k_nn_seed +      :234-275 (1-NN part)
+//                       k_nn_scan (the walk)
 //   K4 moments          k_moments                       update_correspondences
 //                                                       (M) + linearize :277-336
 //   K5 LM / GN step     k_lm_step                       lsq_registration_impl.hpp:95-232
@@ -17,6 +18,7 @@
 // not be contracted into FMAs so that correspondences equal the oracle's.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 
@@ -904,19 +906,43 @@ constexpr int kSeedW = 8;           // Morton-window seed points per slice lane
 __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_dev,
                                                     const AlignJob* __restrict__ job_src) {
   static_assert(sizeof(AlignJob) % 8 == 0, "AlignJob is copied in 8-byte words");
+  static_assert(offsetof(AlignJob, guess_R) % 8 == 0 && offsetof(AlignJob, guess_t) == offsetof(AlignJob, guess_R) + 72 &&
+                    offsetof(AlignJob, job_full) == offsetof(AlignJob, guess_R) + 96,
+                "guess_R, guess_t, job_full: 13 consecutive 8-byte words");
+  constexpr int kHdr0 = (int)(offsetof(AlignJob, guess_R) / 8), kHdrN = 13;
   __shared__ unsigned long long job_lds[sizeof(AlignJob) / 8];
+  __shared__ int full_s;
   const AlignJob* job = job_dev;
+  double gR[9], gt[3];
   if (job_src) {
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(job_src);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(job_dev);
-    for (int w = threadIdx.x; w < (int)(sizeof(AlignJob) / 8); w += blockDim.x) {
-      // system scope: read past every GPU cache (the host rewrites this buffer per align)
-      const unsigned long long v = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      job_lds[w] = v;
-      dst[w] = v;
+    // system scope: read past every GPU cache (the host rewrites this buffer per align).
+    // First the guess and the full-copy flag (one round trip); the rest of the
+    // job only when the host changed more than the guess since the last align.
+    if ((int)threadIdx.x < kHdrN) {
+      const unsigned long long v = __hip_atomic_load(src + kHdr0 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      job_lds[kHdr0 + threadIdx.x] = v;
+      dst[kHdr0 + threadIdx.x] = v;
+      if (threadIdx.x == kHdrN - 1) full_s = v != 0ull;
     }
     __syncthreads();
-    job = reinterpret_cast<const AlignJob*>(job_lds);
+    if (full_s) {
+      for (int w = threadIdx.x; w < (int)(sizeof(AlignJob) / 8); w += blockDim.x) {
+        if (w >= kHdr0 && w < kHdr0 + kHdrN) continue;
+        const unsigned long long v = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        job_lds[w] = v;
+        dst[w] = v;
+      }
+      __syncthreads();
+      job = reinterpret_cast<const AlignJob*>(job_lds);
+    }
+    const AlignJob* jh = reinterpret_cast<const AlignJob*>(job_lds);
+    for (int i = 0; i < 9; ++i) gR[i] = jh->guess_R[i];
+    for (int i = 0; i < 3; ++i) gt[i] = jh->guess_t[i];
+  } else {
+    for (int i = 0; i < 9; ++i) gR[i] = job->guess_R[i];
+    for (int i = 0; i < 3; ++i) gt[i] = job->guess_t[i];
   }
   AlignState* st = job->state;
   if (threadIdx.x <= kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;   // + the moment kernel's arrival counter
@@ -940,8 +966,8 @@ __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_d
     }
   }
   if (threadIdx.x == 0) {
-    for (int i = 0; i < 9; ++i) st->R[i] = job->guess_R[i];
-    for (int i = 0; i < 3; ++i) st->t[i] = job->guess_t[i];
+    for (int i = 0; i < 9; ++i) st->R[i] = gR[i];
+    for (int i = 0; i < 3; ++i) st->t[i] = gt[i];
     st->lambda = -1.0;
     st->iter = 0;
     st->done = job->max_iterations <= 0 ? 1 : 0;
@@ -1899,220 +1925,6 @@ __global__ __launch_bounds__(64 * kScanWaves, MINW) void k_nn_scan(const AlignJo
   else resolve();
 }
 
-template <int Q, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_nn_search(const AlignJob* __restrict__ job) {
-  AlignState* st = job->state;
-  if (__builtin_amdgcn_readfirstlane(st->done)) return;
-  const CloudDev src = job->src;
-  const CloudDev tgt = job->tgt;
-  const auto corr = gpw(job->corr);
-  const auto sqd = gpw(job->sqd);
-  unsigned int* const stats = job->stats;
-  const float cap2 = job->cap2;
-  const double max_corr2 = job->max_corr2;
-  const int have_prev = st->have_prev;
-  const int prev_window = job->prev_window;
-  const double tri_mv = job->tri_mv_d;
-  const int own_axis = job->own_axis;
-  const float own_lo = job->own_lo, own_hi = job->own_hi;
-  const int own_mod = job->own_mod, own_rem = job->own_rem;
-  float Rf[9], tf[3];
-  for (int e = 0; e < 9; ++e) Rf[e] = (float)st->R[e];
-  for (int e = 0; e < 3; ++e) tf[e] = (float)st->t[e];
-
-  const int lane = lane_id();
-  const int qi = lane % Q;
-  const int wib = threadIdx.x >> 6;
-  // dynamic LDS: [kLinWaves x CollectLds][upper-level box cache]
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  CollectLds* CL = reinterpret_cast<CollectLds*>(dsm) + wib;
-  f4v* upper = reinterpret_cast<f4v*>(dsm + kLinWaves * kCollectLdsBytes);
-  fill_upper(tgt, upper);
-  __syncthreads();
-  const int wave = (int)blockIdx.x * kLinWaves + wib;
-  const int nwaves_total = gridDim.x * kLinWaves;
-  const int ngroups = (src.n + Q - 1) / Q;
-  // previous linearization pose (for the triangle-inequality bound)
-  float Rp[9], tp[3];
-  for (int e = 0; e < 9; ++e) Rp[e] = (float)st->last_lin_R[e];
-  for (int e = 0; e < 3; ++e) tp[e] = (float)st->last_lin_t[e];
-  for (int g = wave; g < ngroups; g += nwaves_total) {
-    const unsigned long long tm0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
-    const int i = g * Q + qi;
-    const bool inrange = i < src.n;
-    const int ic = inrange ? i : src.n - 1;
-    // every independent per-query load of the prologue in one round trip
-    const float4 a = ldg4(src.pts, ic);
-    const int jprev = have_prev ? corr[ic] : -1;
-    const float sqprev = have_prev ? sqd[ic] : 0.f;
-    const unsigned long long skey = gp(src.keys)[ic];
-    // fp32 query transform, Eigen lazy-product order (see oracle/cpu_ref.cpp)
-    const float qx = (Rf[0] * a.x + Rf[1] * a.y) + (Rf[2] * a.z + tf[0]);
-    const float qy = (Rf[3] * a.x + Rf[4] * a.y) + (Rf[5] * a.z + tf[1]);
-    const float qz = (Rf[6] * a.x + Rf[7] * a.y) + (Rf[8] * a.z + tf[2]);
-    // spatial sharding: search only the queries this rank owns
-    const float qa = own_axis == 0 ? qx : own_axis == 1 ? qy : qz;
-    const bool active = inrange && (own_axis < 0 || (qa >= own_lo && qa < own_hi)) &&
-                        (own_mod == 0 || ((i >> 4) % own_mod) == own_rem);
-    if (!__any(active)) {
-      if (inrange && lane < Q) {
-        corr[i] = -1;
-        sqd[i] = INFINITY;
-        job->key[i] = dkey(INFINITY, -1);
-      }
-      if (stats && lane == 0) {
-        unsigned int* o = stats + (size_t)g * kStatFields;
-        for (int f = 0; f < kStatFields; ++f) o[f] = 0;
-      }
-      continue;
-    }
-    NNVisitor<Q> vis;
-    vis.qx = qx;
-    vis.qy = qy;
-    vis.qz = qz;
-    vis.active = active;
-    vis.best = active ? cap2 : -1.f;
-    vis.bestj = -1;
-    vis.skip_lo = 1;
-    vis.skip_hi = 0;
-    bool seeded = false;
-    bool large_step = false;   // previous match exists but the pose moved >= 2 cm since
-    // coordinates of the point behind vis.bestj when it is already in registers
-    float bpx = 0.f, bpy = 0.f, bpz = 0.f;
-    bool have_bp = true;
-    if (have_prev && active) {
-      const int j = jprev;
-      if (j >= 0) {
-        // NN(q) <= |q - p_prev| <= sqrt(sqd_prev) + |q - q_prev| (triangle
-        // inequality; fp64 with an upward margin covers fp32 rounding), so
-        // the bound needs no load of the previous match.
-        const float qpx = (Rp[0] * a.x + Rp[1] * a.y) + (Rp[2] * a.z + tp[0]);
-        const float qpy = (Rp[3] * a.x + Rp[4] * a.y) + (Rp[5] * a.z + tp[1]);
-        const float qpz = (Rp[6] * a.x + Rp[7] * a.y) + (Rp[8] * a.z + tp[2]);
-        const double ddx = (double)qx - qpx, ddy = (double)qy - qpy, ddz = (double)qz - qpz;
-        const double mv = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
-        if (mv < tri_mv) {
-          const double r = sqrt((double)sqprev) + mv;
-          const double b2 = r * r * (1.0 + 1e-5) + 1e-12;
-          if (b2 < job->cap2_d) {
-            vis.best = __uint_as_float(__float_as_uint((float)b2) + 1);  // round up
-            seeded = true;
-          }
-        } else if (prev_window) {
-          large_step = true;   // exact distances to the Morton window around p_prev (below)
-        } else {  // large pose step: the exact distance to the previous match
-          const float4 p = ldg4(tgt.pts, j);
-          const float d = dist2(qx, qy, qz, p.x, p.y, p.z);
-          if (d < cap2) {
-            vis.best = d;
-            vis.bestj = j;
-            bpx = p.x;
-            bpy = p.y;
-            bpz = p.z;
-            seeded = true;
-          }
-        }
-      }
-    }
-    // Exact seeding for queries without a usable previous correspondence:
-    // the real target points around the query's Morton position give an
-    // upper bound, so the single search below stays exact.  After a large
-    // pose step the window is centred on the previous match instead (its
-    // sorted position IS a Morton position next to the new nearest point,
-    // and no key search is needed); the window contains the previous match.
-    const bool need_seed = active && !seeded && !large_step;
-    const bool use_window = need_seed || large_step;
-    bool again = false;
-    if (__any(use_window)) {
-      // Morton window of kSeedW points per slice lane (64/Q * kSeedW per query)
-      int pos = large_step ? jprev : 0;
-      if (__any(need_seed)) {
-        const unsigned long long qk = morton_key(qx, qy, qz, tgt.quant);
-        int dlo, dhi;
-        dir_range(tgt.dir, qk, dlo, dhi);   // one load instead of ~5 dependent search steps
-        const int lb = group_lower_bound<Q>(tgt.keys, tgt.n, qk, dlo, dhi);
-        if (need_seed) pos = lb;
-      }
-      const int s = lane / Q;
-      const int w0 = pos - (64 / Q) * kSeedW / 2 + s * kSeedW;
-      unsigned long long bk = dkey(vis.best, vis.bestj);
-      float4 p[kSeedW];
-#pragma unroll
-      for (int k = 0; k < kSeedW; ++k) p[k] = ldg4(tgt.pts, min(max(w0 + k, 0), tgt.n - 1));
-      if (use_window) {
-#pragma unroll
-        for (int k = 0; k < kSeedW; ++k) {
-          const int cand = min(max(w0 + k, 0), tgt.n - 1);
-          bk = umin64(bk, dkey(dist2(qx, qy, qz, p[k].x, p[k].y, p[k].z), cand));
-        }
-      }
-      vis.merge_slices(bk);
-      if (use_window) {
-        const float bd = __uint_as_float((unsigned)(bk >> 32));
-        if (bd < cap2) {
-          vis.best = bd;
-          vis.bestj = (int)(unsigned)bk;
-          have_bp = false;   // the winning window point may sit in another slice lane
-        }
-      }
-      again = need_seed;
-    }
-    // Group sharing: every query also takes the exact distance to the other
-    // queries' candidate points (Morton-adjacent queries are spatially
-    // adjacent, so a neighbour's candidate is often far closer than the
-    // query's own).  Valid (distance, position) pairs only: exactness kept.
-    {
-      const unsigned long long donors = __ballot(lane < Q && active && vis.bestj >= 0);
-      if (donors && __any(active)) {
-        float4 bp = make_float4(bpx, bpy, bpz, 0.f);
-        if (__any(!have_bp && vis.bestj >= 0)) {
-          if (!have_bp) bp = ldg4(tgt.pts, max(vis.bestj, 0));
-        }
-        unsigned long long bk = dkey(vis.best, vis.bestj);
-        unsigned long long m = donors;
-        while (m) {
-          const int k = __builtin_ctzll(m);
-          m &= m - 1;
-          const float sx = readlane_f(bp.x, k), sy = readlane_f(bp.y, k), sz = readlane_f(bp.z, k);
-          const int sj = readlane_i(vis.bestj, k);
-          bk = umin64(bk, dkey(dist2(qx, qy, qz, sx, sy, sz), sj));
-        }
-        if (active) {
-          vis.best = __uint_as_float((unsigned)(bk >> 32));
-          vis.bestj = (int)(unsigned)bk;
-        }
-      }
-    }
-    unsigned cst[6] = {0, 0, 0, 0, 0, 0};
-    const unsigned tm_pro = stats ? (unsigned)__builtin_amdgcn_s_memtime() : 0u;
-    collect_scan_nn<Q>(tgt, CL, upper, qx, qy, qz, active, vis.best, vis.bestj, skey, cst, job->split_extent,
-                       job->list_flush);
-    vis.st_blocks = cst[0];
-    vis.st_box = min((tm_pro - (unsigned)tm0) >> 4, 65535u) | (min((cst[1] - (unsigned)tm0) >> 4, 65535u) << 16);
-    vis.st_exact = cst[2];
-    vis.st_scan = cst[3];
-    vis.st_splits = cst[4];
-    const bool valid = active && vis.bestj >= 0 && (double)vis.best < max_corr2;
-    if (inrange && lane < Q) {
-      corr[i] = valid ? vis.bestj : -1;
-      sqd[i] = active && vis.bestj >= 0 ? vis.best : INFINITY;
-      job->key[i] = active && vis.bestj >= 0 ? dkey(vis.best, vis.bestj) : dkey(INFINITY, -1);
-    }
-    if (stats && lane == 0) {
-      const unsigned long long tm1 = __builtin_amdgcn_s_memtime();
-      unsigned int* o = stats + (size_t)g * kStatFields;
-      o[0] = vis.st_blocks;
-      o[1] = vis.st_box;
-      o[2] = vis.st_exact;
-      o[3] = vis.st_scan;
-      o[4] = (unsigned)(tm1 - tm0);
-      o[5] = cst[5] - (unsigned)tm0;  // cycles until the end of the collect phase
-      o[6] = (unsigned)__popcll(__ballot(again)) | (vis.st_splits << 16);
-      o[7] = 1;
-    }
-  }
-}
-
 // K3b: Mahalanobis + normal-equation moments of the matched pairs
 // (update_correspondences :265-273 + linearize :292-328), 64 points per
 // wavefront, in-register transpose reduction, one slab row per block.
@@ -2133,7 +1945,8 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job);
 // builds it and runs the align again.  Not inlined: the rare path keeps its
 // registers out of the moment loop.
 __device__ __forceinline__ void resolve_tied_corr(const AlignJob* __restrict__ job, AlignState* st, const CloudDev& tgt,
-                                               bool tied, int i, float kd, int& j, NfWaveStack* S) {
+                                               bool tied, int i, float kd, int& j, NfWaveStack* S,
+                                               bool q_in_regs = false, float qx = 0.f, float qy = 0.f, float qz = 0.f) {
   unsigned long long tm = __ballot(tied);
   const int lane = lane_id();
   const NfTreeDev t = job->tgt_nf;
@@ -2151,7 +1964,9 @@ __device__ __forceinline__ void resolve_tied_corr(const AlignJob* __restrict__ j
     tm &= tm - 1;
     const int il = __builtin_amdgcn_readlane(i, l);
     const float dl = __uint_as_float((unsigned)__builtin_amdgcn_readlane((int)__float_as_uint(kd), l));
-    const float4 q = ldg4(job->qstate, il);   // the search's fp32 query (trans_f * a_i, :240,253)
+    // the search's fp32 query (trans_f * a_i, :240,253)
+    const float4 q = q_in_regs ? make_float4(readlane_f(qx, l), readlane_f(qy, l), readlane_f(qz, l), 0.f)
+                               : ldg4(job->qstate, il);
     float rd;
     int rix;
     int err = 0, jn = -1;
@@ -2177,7 +1992,11 @@ __device__ __forceinline__ void resolve_tied_corr(const AlignJob* __restrict__ j
 // an arrival counter (memory-side atomic); the block that arrives last takes
 // one agent-scope acquire and reads the slab with plain loads
 // (MI355X_MICROARCH.md "visibility", the split-K form of Guideline 16).
-template <bool FUSE_LM>
+// LOOKUP (candidate cells without any fallback cell): the correspondence
+// lookup of k_cell_lookup is done here, one query per lane, and the match's
+// coordinates come from its list entry -- no lookup kernel, no key / sec
+// round trip.  Same keys, ties and moments as k_cell_lookup + k_moments.
+template <bool FUSE_LM, bool LOOKUP = false>
 __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __restrict__ job) {
   AlignState* st = job->state;
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
@@ -2227,17 +2046,83 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     // checks, so those loads overlap them; a re-run query reloads its b
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
     double ca[6] = {0, 0, 0, 0, 0, 0}, cb[6] = {0, 0, 0, 0, 0, 0};
+    float lqx = 0.f, lqy = 0.f, lqz = 0.f;   // LOOKUP: the fp32 query
+    unsigned long long lkey = 0ull;
+    unsigned lsec = 0xffffffffu;
+    if constexpr (LOOKUP) {
+      // k_cell_lookup's arithmetic, one lane per query
+      const CellGridDev G = job->grid;
+      a = ldg4(src.pts, active ? i : src.n - 1);
+      const float Rf0 = (float)R[0], Rf1 = (float)R[1], Rf2 = (float)R[2], Rf3 = (float)R[3], Rf4 = (float)R[4],
+                  Rf5 = (float)R[5], Rf6 = (float)R[6], Rf7 = (float)R[7], Rf8 = (float)R[8];
+      const float tf0 = (float)t[0], tf1 = (float)t[1], tf2 = (float)t[2];
+      lqx = (Rf0 * a.x + Rf1 * a.y) + (Rf2 * a.z + tf0);
+      lqy = (Rf3 * a.x + Rf4 * a.y) + (Rf5 * a.z + tf1);
+      lqz = (Rf6 * a.x + Rf7 * a.y) + (Rf8 * a.z + tf2);
+      const int g16 = i >> 4;
+      const float qa = job->own_axis == 0 ? lqx : job->own_axis == 1 ? lqy : lqz;
+      const bool owned = active && (job->own_axis < 0 || (qa >= job->own_lo && qa < job->own_hi)) &&
+                         (job->own_mod == 0 || (g16 % job->own_mod) == job->own_rem);
+      unsigned off = 0, cnt = 0;
+      if (owned) {
+        const float tx = (lqx - G.ox) * G.inv_s, ty = (lqy - G.oy) * G.inv_s, tz = (lqz - G.oz) * G.inv_s;
+        if (tx >= 0.f && tx < (float)G.nx && ty >= 0.f && ty < (float)G.ny && tz >= 0.f && tz < (float)G.nz) {
+          const int cx = min((int)tx, G.nx - 1), cy = min((int)ty, G.ny - 1), cz = min((int)tz, G.nz - 1);
+          const unsigned d = gp(G.dir)[((long)cx * G.ny + cy) * G.nz + cz];
+          if (d != kCgNoMatch) {   // (no fallback cell in LOOKUP mode)
+            const int lvl = (int)(d >> 30), m = 1 << lvl;
+            const int fx = min((int)((tx - (float)cx) * (float)m), m - 1);
+            const int fy = min((int)((ty - (float)cy) * (float)m), m - 1);
+            const int fz = min((int)((tz - (float)cz) * (float)m), m - 1);
+            const unsigned long long e = gp(reinterpret_cast<const unsigned long long*>(
+                G.fine))[(d & 0x3fffffffu) + (unsigned)((fx * m + fy) * m + fz)];
+            off = (unsigned)e;
+            cnt = (unsigned)(e >> 32);
+          }
+        }
+      }
+      unsigned long long bk = ~0ull;
+      float d2 = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
+      constexpr int kU = 8;   // loads in flight
+      for (unsigned k = 0; k < cnt; k += kU) {
+        float4 pp[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) pp[u] = ldg4(G.ent, off + min(k + u, cnt - 1));
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          if (k + u < cnt) {
+            const float dd = dist2(lqx, lqy, lqz, pp[u].x, pp[u].y, pp[u].z);
+            const unsigned long long kk = dkey(dd, __float_as_int(pp[u].w));
+            if (kk < bk) {
+              if (bk != ~0ull) d2 = fminf(d2, __uint_as_float((unsigned)(bk >> 32)));
+              bk = kk;
+              bx = pp[u].x;
+              by = pp[u].y;
+              bz = pp[u].z;
+            } else {
+              d2 = fminf(d2, dd);
+            }
+          }
+        }
+      }
+      lkey = owned ? umin64(bk, dkey(job->cap2, -1)) : dkey(INFINITY, -1);
+      const float lkd = __uint_as_float((unsigned)(lkey >> 32));
+      lsec = (owned && (unsigned)lkey != 0xffffffffu && d2 == lkd) ? (unsigned)(lkey >> 32) : 0xffffffffu;
+      b = make_float4(bx, by, bz, 0.f);
+    }
     if (active) {
-      const unsigned long long k = key[i];
+      const unsigned long long k = LOOKUP ? lkey : key[i];
       // independent of the key: issued with it
-      const unsigned sv = tie_detect ? job->sec[i] : 0xffffffffu;
-      const unsigned k2lo = tie3m ? (unsigned)job->key2[i] : 0u;
+      const unsigned sv = !tie_detect ? 0xffffffffu : LOOKUP ? lsec : job->sec[i];
+      const unsigned k2lo = (tie3m && !LOOKUP) ? (unsigned)job->key2[i] : 0u;
       kj = (unsigned)k;
       kd = __uint_as_float((unsigned)(k >> 32));
       j = (kj != 0xffffffffu && (double)kd < max_corr2) ? (int)kj : -1;
       if (j >= 0) {
-        a = ldg4(src.pts, i);
-        b = ldg4(tgt.pts, j);
+        if constexpr (!LOOKUP) {   // (LOOKUP: a and b are in registers already)
+          a = ldg4(src.pts, i);
+          b = ldg4(tgt.pts, j);
+        }
         load_sym6(src_cov + 6 * (size_t)i, ca);
         load_sym6(tgt_cov + 6 * (size_t)j, cb);
       }
@@ -2247,7 +2132,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       // the key's); tie_scan 3 also: the mirrored key names another point
       const bool searched = tie_detect && j >= 0 && sv != 0xffffffffu;
       tied = searched && sv <= (unsigned)(k >> 32);
-      if (tie3m && searched) tied = tied || k2lo != ((unsigned)k ^ 0xffffffffu);
+      if (tie3m && searched && !LOOKUP) tied = tied || k2lo != ((unsigned)k ^ 0xffffffffu);
       // tie_scan >= 2: the scan compares only the 8-point slices' bests, so a
       // second point at the distance inside the winner's own slice (the 8
       // aligned sorted positions one lane scanned; the same 128-B line as the
@@ -2268,7 +2153,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     // nanoflann's choice among the tied points (wave-uniform, rare)
     if (tie_detect && __any(tied)) {
       const int j0 = j;
-      resolve_tied_corr(job, st, tgt, tied, i, kd, j, &tie_stk[wib]);
+      resolve_tied_corr(job, st, tgt, tied, i, kd, j, &tie_stk[wib], LOOKUP, lqx, lqy, lqz);
       if (tied) kj = (unsigned)j;
       if (j != j0) {   // another point of the same distance: its coordinates and covariance
         b = ldg4(tgt.pts, j);
@@ -2283,7 +2168,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       // walk radius) — every unexamined point lies in a leaf farther than the
       // walk radius — and its match.  A reference stays a valid proof for
       // the rest of the align (same target), so other iterations keep it.
-      if (rec) {
+      if (rec && !LOOKUP) {   // (LOOKUP: no walk, so no reference is ever checked)
         const float4 qs = ldg4(job->qstate, i);
         if (qs.w >= 0.f) {
           job->ref[i] = make_float4(qs.x, qs.y, qs.z, fminf(__uint_as_float(job->sec[i]), qs.w));
@@ -2381,6 +2266,8 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
 }
 template __global__ void k_moments<false>(const AlignJob*);
 template __global__ void k_moments<true>(const AlignJob*);
+template __global__ void k_moments<false, true>(const AlignJob*);
+template __global__ void k_moments<true, true>(const AlignJob*);
 
 // ---------------------------------------------------------------------------
 // K5: slab reduction + LM/GN step on one workgroup.
@@ -3181,9 +3068,6 @@ void launch_tie_map(hipStream_t s, const int* local_index, const int* inv_perm, 
 void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src) {
   k_align_init<<<1, 128, 0, s>>>(job, job_src);
 }
-size_t search_lds_bytes(int upper_count) {
-  return (size_t)kLinWaves * kCollectLdsBytes + 2 * sizeof(f4v) * (size_t)upper_count;
-}
 size_t collect_lds_bytes(int upper_count) {
   return (size_t)kLinWaves * kTaskLdsBytes + 2 * sizeof(f4v) * (size_t)upper_count;
 }
@@ -3197,13 +3081,6 @@ static int scan_blocks(int nsrc) {
   int waves = std::min(std::max(groups, kTaskRegions), cap);
   waves = (waves + 8 * kTaskRegions - 1) / (8 * kTaskRegions) * (8 * kTaskRegions);
   return waves / kScanWaves;
-}
-bool search_uses_tasks() {
-  static const bool old_search = [] {   // DDLO_SEARCH=collect: the single-kernel collect-then-scan search (A/B)
-    const char* v = std::getenv("DDLO_SEARCH");
-    return v && std::strcmp(v, "collect") == 0;
-  }();
-  return !old_search;
 }
 // Bucketed launch geometry: scans of similar size (cfg 5: +-1k points per
 // frame) share one captured chunk graph, and a graph never runs with a grid
@@ -3222,9 +3099,16 @@ LinGeom linearize_geometry(int nsrc, int tgt_upper) {
 }
 
 void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
+  static const int fused_lookup = env_knob("DDLO_GRID_FUSED", 1);   // 0: separate lookup kernel (A/B)
+  if (g.grid && !g.grid_walk && fused_lookup) {
+    // every query is answered by its cell: the lookup runs inside the moment kernel
+    if (g.fuse_lm) k_moments<true, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
+    else k_moments<false, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
+    return;
+  }
   if (g.grid) k_cell_lookup<<<g.lookup_blocks, 256, 0, s>>>(job);
-  if (!search_uses_tasks()) {
-    k_nn_search<kSearchQ, 3><<<g.seed_blocks, 64 * kLinWaves, search_lds_bytes(g.lds_boxes), s>>>(job);
+  if (g.grid && !g.grid_walk) {
+    // every query is answered by its cell (or provably unmatched): no walk
   } else {
     static const int occ_seed = env_knob("DDLO_OCC_SEED", 4), occ_col = env_knob("DDLO_OCC_COLLECT", 3),
                      occ_scan = env_knob("DDLO_OCC_SCAN", 5);

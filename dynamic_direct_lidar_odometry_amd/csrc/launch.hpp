@@ -52,12 +52,12 @@ struct LinGeom {
   int seed_blocks, collect_blocks, scan_blocks, mom_blocks, lds_boxes, lookup_blocks;
   bool fuse_lm = false;   // the LM step runs in the moment kernel's last block (no k_lm_step launch)
   bool grid = false;      // the target's candidate cells answer the search first (k_cell_lookup)
+  bool grid_walk = true;  // ... and some of its cells have no list: the walk kernel follows the lookup
 };
 bool lm_fusion_enabled();   // DDLO_FUSE_LM (unsharded graph aligns)
 LinGeom linearize_geometry(int nsrc, int tgt_upper);
 void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g);
 int search_queries_per_wave();
-bool search_uses_tasks();   // false under DDLO_SEARCH=collect (the single-kernel search)
 int task_cap_per_region(int nsrc);   // task-list slots per region for nsrc source points
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
 void launch_lm_step(hipStream_t s, const AlignJob* job, AlignState* publish);

@@ -328,6 +328,8 @@ struct gicp_ctx {
   DevBuf corr, sqd, slab, job_dev, state_dev, tmp_out, stats;
   bool stats_on = false;
   AlignJob* job_host = nullptr;   // pinned
+  AlignJob job_last{};            // the job k_align_init last copied whole (AlignJob::job_full)
+  bool job_last_valid = false;
   AlignJob* job_host_dev = nullptr;     // its device-side address (read by k_align_init)
   AlignState* state_host_dev = nullptr; // state_host's device-side address (written by k_lm_step)
   // pinned, two slots: chunk k publishes its end state to slot k % 2, so the

@@ -698,42 +698,8 @@ using NN1Visitor = NNVisitor<64>;
 
 namespace ddlo {
 
-// ===========================================================================
-// Collect-then-scan exact 1-NN for Q-query groups (the correspondence search
-// of the GICP loop).
-//
-// The per-leaf traversal above pays one dependent global round trip per
-// node and per leaf.  Here a wavefront
-//   1. walks the upper levels (levels >= 1, cached in LDS per workgroup) with
-//      the union box of its queries' balls -> candidate level-1 blocks;
-//   2. loads the leaf boxes of up to 4 candidate blocks at once (lane = leaf)
-//      and tests every leaf EXACTLY against all Q queries (broadcast from
-//      LDS) -> per-wave leaf list;
-//   3. streams the listed leaves through LDS in batches with global_load_lds
-//      (one instruction moves two 32-point leaves), one wait per batch, and
-//      every lane scans its slice of each leaf.
-// Exactness: a leaf is dropped only if its box is farther than the query's
-// bound, and bounds only shrink while scanning.
-// ===========================================================================
-constexpr int kListMax = 288;       // leaf list capacity per wavefront (>= kListFlush + 4 blocks x 64 leaves)
-constexpr int kListFlush = 16;      // scan once this many leaves are listed: early
-                                    // scans tighten the bounds that filter later blocks
-constexpr int kBlkMax = 32;         // candidate level-1 blocks per wavefront
-constexpr int kBatch = 8;           // leaves per LDS-DMA batch
-constexpr int kQMax = 32;           // queries per wavefront (collect path)
-
-struct CollectLds {
-  f4v q[kQMax];                     // per query: x, y, z, bound (bound < 0: inactive)
-  int leaves[kListMax];
-  int blocks[kBlkMax];
-  int nleaves, nblocks, pad0, pad1;
-  f4v pts[kBatch * kLeafSize];      // streamed leaves (AoS float4)
-  f4v sb_lo[kFanout], sb_hi[kFanout];  // boxes of a block's leaves that pass the union test
-  int sb_leaf[kFanout];
-  int sr_lo[4], sr_hi[4], nsr, pad2;     // query sub-ranges of a split wave
-};
-constexpr int kCollectLdsBytes = (int)sizeof(CollectLds);
-
+// Upper levels of a cloud's hierarchy, cached in LDS by the correspondence
+// walk (nn_tasks.hpp).
 __device__ __forceinline__ int upper_count(const CloudDev& c) {
   return c.nlevels <= 1 ? 0 : (lvl_off(c, c.nlevels - 1) + lvl_cnt(c, c.nlevels - 1) - c.off1);
 }
@@ -754,300 +720,5 @@ __device__ __forceinline__ bool box_overlap_v(const WaveBox& w, f4v lo, f4v hi) 
   return lo.x <= w.hx && hi.x >= w.lx && lo.y <= w.hy && hi.y >= w.ly && lo.z <= w.hz && hi.z >= w.lz;
 }
 
-template <int Q>
-struct NNCollector {
-  static constexpr int S = 64 / Q;
-  static constexpr int P = kLeafSize / S;
-  CollectLds* L;
-  const f4v* U;     // upper-level cache
-  int nup;          // its size
-  WaveBox box;
-  // per-lane query state; bk = (best, bestj) key, identical in the S lanes of a query
-  float qx, qy, qz;
-  bool active;
-  unsigned long long bk;
-  unsigned st_blocks = 0, st_exact = 0, st_scan = 0, st_splits = 0;
-  int list_flush = kListFlush;   // leaf-list length that triggers an early scan
-
-  __device__ __forceinline__ float bound() const { return __uint_as_float((unsigned)(bk >> 32)); }
-
-  __device__ __forceinline__ void publish_bounds() {
-    if (lane_id() < Q) L->q[lane_id()].w = active ? bound() : -1.f;
-    __builtin_amdgcn_wave_barrier();
-  }
-
-  // Stream the listed leaves through LDS and scan them.
-  __device__ __forceinline__ void flush_leaves(const CloudDev& c) {
-    const int lane = lane_id();
-    const int n = L->nleaves;
-    if (n == 0) return;
-    const int s = lane / Q;
-    const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
-    unsigned long long k = bk;
-    for (int b0 = 0; b0 < n; b0 += kBatch) {
-      const int nb = min(kBatch, n - b0);
-      // one global_load_lds_dwordx4 moves two leaves: lanes 0-31 -> leaf 2t, 32-63 -> leaf 2t+1
-#pragma unroll
-      for (int t = 0; t < kBatch / 2; ++t) {
-        if (2 * t < nb) {
-          const int lf = L->leaves[b0 + min(2 * t + (lane >> 5), nb - 1)];
-          const float4* src = c.pts + (size_t)lf * kLeafSize + (lane & 31);
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                           (__attribute__((address_space(3))) void*)&L->pts[2 * t * kLeafSize], 16, 0, 0);
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the batch has landed in LDS
-      __builtin_amdgcn_wave_barrier();
-      for (int t = 0; t < nb; ++t) {
-        const int start = L->leaves[b0 + t] * kLeafSize + s * P;
-        const f4v* pp = &L->pts[t * kLeafSize + s * P];
-#pragma unroll
-        for (int h = 0; h < P; h += 2) {
-          const f4v p0 = pp[h], p1 = pp[h + 1];
-          const f2v dx = qx2 - f2v{p0.x, p1.x};
-          const f2v dy = qy2 - f2v{p0.y, p1.y};
-          const f2v dz = qz2 - f2v{p0.z, p1.z};
-          const f2v d = (dx * dx + dy * dy) + dz * dz;
-          k = umin64(k, dkey(d.x, start + h));
-          k = umin64(k, dkey(d.y, start + h + 1));
-        }
-      }
-      st_scan += nb;
-      __builtin_amdgcn_wave_barrier();
-    }
-    for (int m = Q; m < 16; m <<= 1) k = umin64(k, __shfl_xor(k, m));
-    if constexpr (Q <= 16) k = xor_min64<16>(k);
-    if constexpr (Q <= 32) k = xor_min64<32>(k);
-    if (active) bk = k;
-    if (lane == 0) L->nleaves = 0;
-    __builtin_amdgcn_wave_barrier();
-    publish_bounds();
-  }
-
-  // Exact leaf filter of the listed blocks (4 blocks per round trip).
-  // (1) lane = leaf: one test of the leaf box against the union box of the
-  //     wave's current balls; (2) only the survivors are tested against the
-  //     individual queries, as (leaf, query) pairs spread over the lanes
-  //     (64/Q leaves per round) instead of every leaf against all Q queries.
-  // The leaf list is scanned (bounds tightened) between groups of 4 blocks;
-  // the scan sits outside the unrolled block loop so that its code exists
-  // once (the kernel must stay small for the instruction cache).
-  __device__ __forceinline__ void flush_blocks(const CloudDev& c) {
-    const int lane = lane_id();
-    const int nb = L->nblocks;
-    for (int b0 = 0; b0 < nb; b0 += 4) {
-      float4 lo[4], hi[4];
-      int base[4], cnt[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int bi = min(b0 + u, nb - 1);
-        base[u] = L->blocks[bi] * kFanout;
-        cnt[u] = (b0 + u < nb) ? min(kFanout, c.cnt0 - base[u]) : 0;
-        const int li = min(base[u] + lane, c.cnt0 - 1);
-        lo[u] = ldg4(c.box_lo, li);
-        hi[u] = ldg4(c.box_hi, li);
-      }
-      // union of the current balls (bounds only shrink: a superset)
-      const WaveBox wb = make_wave_box(active, qx, qy, qz, bound());
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (cnt[u] == 0) continue;
-        st_blocks += 1;
-        const bool pass = lane < cnt[u] && box_overlap(wb, lo[u], hi[u]);
-        const unsigned long long m = __ballot(pass);
-        const int cm = __popcll(m);
-        if (cm == 0) continue;
-        if (pass) {
-          const int slot = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-          L->sb_lo[slot] = f4v{lo[u].x, lo[u].y, lo[u].z, 0.f};
-          L->sb_hi[slot] = f4v{hi[u].x, hi[u].y, hi[u].z, 0.f};
-          L->sb_leaf[slot] = base[u] + lane;
-        }
-        __builtin_amdgcn_wave_barrier();
-        pair_filter(cm);
-      }
-      if (L->nleaves > list_flush) flush_leaves(c);  // tightens bounds; list empties
-    }
-    if (lane == 0) L->nblocks = 0;
-    __builtin_amdgcn_wave_barrier();
-  }
-
-  // (leaf, query) pair tests of the cm staged leaves; listed leaves appended
-  __device__ __forceinline__ void pair_filter(int cm) {
-    const int lane = lane_id();
-    constexpr int LPR = 64 / Q;
-    for (int r0 = 0; r0 < cm; r0 += LPR) {
-      const int li = r0 + lane / Q;
-      bool need = false;
-      if (li < cm) {
-        const f4v qk = L->q[lane % Q];
-        const f4v blo = L->sb_lo[li], bhi = L->sb_hi[li];
-        need = qk.w >= 0.f && box_dist2(qk.x, qk.y, qk.z, make_float4(blo.x, blo.y, blo.z, 0.f),
-                                        make_float4(bhi.x, bhi.y, bhi.z, 0.f)) <= qk.w;
-      }
-      const unsigned long long bal = __ballot(need);
-      // the first lane of each Q-lane segment lists the segment's leaf
-      const unsigned long long segm = Q >= 64 ? ~0ull : ((1ull << Q) - 1ull);
-      const bool lead = (lane % Q) == 0 && li < cm && ((bal >> (lane & ~(Q - 1))) & segm) != 0ull;
-      const unsigned long long lm = __ballot(lead);
-      const int cl = __popcll(lm);
-      if (cl == 0) continue;
-      st_exact += cl;
-      const int n0 = L->nleaves;
-      if (lead) {
-        const int slot =
-            n0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(lm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)lm, 0u));
-        L->leaves[slot] = L->sb_leaf[li];
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) L->nleaves = n0 + cl;
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-
-  __device__ __forceinline__ bool upper_ov(const CloudDev& c, int level, int idx) const {
-    const int k = lvl_off(c, level) - c.off1 + idx;
-    return box_overlap_v(box, U[k], U[nup + k]);
-  }
-
-  // Depth-first walk of the upper levels with the wave box: an explicit
-  // per-level stack of 64-bit child masks (uniform values: scalar registers),
-  // so the block push (and the block flush it may trigger) has a single call
-  // site whatever the depth.
-  __device__ __forceinline__ void collect_blocks(const CloudDev& c) {
-    const int T = c.nlevels - 1;
-    const int lane = lane_id();
-    if (T == 0) {  // a single leaf block
-      if (lane == 0) {
-        L->blocks[L->nblocks] = 0;
-        L->nblocks = L->nblocks + 1;
-      }
-      __builtin_amdgcn_wave_barrier();
-      return;
-    }
-    unsigned long long m1 = 0, m2 = 0, m3 = 0, m4 = 0;
-    int b1 = 0, b2 = 0, b3 = 0;
-    {
-      const bool ov = lane < lvl_cnt(c, T) && upper_ov(c, T, lane);
-      const unsigned long long m = __ballot(ov);
-      if (T == 1) m1 = m; else if (T == 2) m2 = m; else if (T == 3) m3 = m; else m4 = m;
-    }
-    int lv = T;
-    while (true) {
-      unsigned long long m = lv == 1 ? m1 : lv == 2 ? m2 : lv == 3 ? m3 : m4;
-      if (m == 0ull) {
-        if (lv == T) break;
-        ++lv;
-        continue;
-      }
-      const int base = lv == 1 ? b1 : lv == 2 ? b2 : lv == 3 ? b3 : 0;
-      const int node = base + __builtin_ctzll(m);
-      m &= m - 1;
-      if (lv == 1) m1 = m; else if (lv == 2) m2 = m; else if (lv == 3) m3 = m; else m4 = m;
-      if (lv == 1) {  // a level-1 node is a block of 64 leaves
-        if (L->nblocks >= kBlkMax) flush_blocks(c);
-        if (lane == 0) {
-          L->blocks[L->nblocks] = node;
-          L->nblocks = L->nblocks + 1;
-        }
-        __builtin_amdgcn_wave_barrier();
-        continue;
-      }
-      const int cb = node * kFanout;
-      const int cnt = min(kFanout, lvl_cnt(c, lv - 1) - cb);
-      const bool ov = lane < cnt && upper_ov(c, lv - 1, cb + lane);
-      const unsigned long long cm = __ballot(ov);
-      --lv;
-      if (lv == 1) { m1 = cm; b1 = cb; } else if (lv == 2) { m2 = cm; b2 = cb; } else { m3 = cm; b3 = cb; }
-    }
-  }
-};
-
-// Full exact bounded 1-NN for a Q-query group: split the group at Morton
-// jumps (<= 4 compact sub-ranges), collect per sub-range, filter, scan.
-template <int Q>
-__device__ __forceinline__ void collect_scan_nn(const CloudDev& c, CollectLds* L, const f4v* U, float qx, float qy,
-                                                float qz, bool active, float& best, int& bestj,
-                                                unsigned long long key, unsigned (&st)[6],
-                                                float split_extent = kSplitExtent, int list_flush = kListFlush) {
-  const int lane = lane_id();
-  const int qi = lane % Q;
-  if (lane < Q) L->q[lane] = f4v{qx, qy, qz, active ? best : -1.f};
-  if (lane == 0) {
-    L->nleaves = 0;
-    L->nblocks = 0;
-  }
-  __builtin_amdgcn_wave_barrier();
-  NNCollector<Q> col;
-  col.L = L;
-  col.U = U;
-  col.nup = upper_count(c);
-  col.qx = qx;
-  col.qy = qy;
-  col.qz = qz;
-  col.active = active;
-  col.bk = dkey(best, bestj);
-  col.list_flush = list_flush;
-  // Query sub-ranges: the whole group, or — when the union box of its balls
-  // is wider than kSplitExtent — up to 4 Morton-jump sub-ranges, each walked
-  // with its own (smaller) box.  A runtime worklist keeps one walk site.
-  const WaveBox whole = make_wave_box(active, qx, qy, qz, best);
-  if (lane == 0) {
-    L->sr_lo[0] = 0;
-    L->sr_hi[0] = Q;
-    L->nsr = 1;
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (box_extent(whole) > split_extent) {
-    col.st_splits += 1;
-    const int sp = morton_jump_split<Q>(key, 0, Q);
-    int nsr = 0;
-    for (int h = 0; h < 2; ++h) {
-      const int lo = h == 0 ? 0 : sp, hi = h == 0 ? sp : Q;
-      if (lo >= hi) continue;
-      const bool act = active && qi >= lo && qi < hi;
-      const WaveBox hb = make_wave_box(act, qx, qy, qz, col.bound());
-      if (box_extent(hb) > split_extent && hi - lo > 4) {
-        col.st_splits += 1;
-        const int s2 = morton_jump_split<Q>(key, lo, hi);
-        if (lane == 0) {
-          L->sr_lo[nsr] = lo; L->sr_hi[nsr] = s2;
-          L->sr_lo[nsr + 1] = s2; L->sr_hi[nsr + 1] = hi;
-        }
-        nsr += 2;
-      } else {
-        if (lane == 0) {
-          L->sr_lo[nsr] = lo; L->sr_hi[nsr] = hi;
-        }
-        nsr += 1;
-      }
-    }
-    if (lane == 0) L->nsr = nsr;
-    __builtin_amdgcn_wave_barrier();
-  }
-  for (int r = 0; r < L->nsr; ++r) {
-    const int lo = L->sr_lo[r], hi = L->sr_hi[r];
-    if (lo >= hi) continue;
-    const bool act = active && qi >= lo && qi < hi;
-    if (!__any(act)) continue;
-    col.box = make_wave_box(act, qx, qy, qz, col.bound());
-    col.collect_blocks(c);
-  }
-  // a block listed by two sub-ranges is filtered twice: harmless (a leaf
-  // scanned twice leaves the minimum unchanged)
-  const unsigned tm_trav = (unsigned)__builtin_amdgcn_s_memtime();
-  col.flush_blocks(c);
-  st[5] = (unsigned)__builtin_amdgcn_s_memtime();
-  col.flush_leaves(c);
-  st[0] = col.st_blocks;
-  st[1] = tm_trav;
-  st[2] = col.st_exact;
-  st[3] = col.st_scan;
-  st[4] = col.st_splits;
-  if (active) {
-    best = col.bound();
-    bestj = (int)(unsigned)col.bk;
-  }
-}
 
 }  // namespace ddlo

@@ -45,9 +45,11 @@ def main():
         c.synchronize()
         t0 = time.perf_counter()
         it = 0
+        dev = []
         for _ in range(args.aligns):
             _, r = c.align(guess)
             it += r.iterations_run
+            dev.append(r.device_ms)
         c.synchronize()
         el = time.perf_counter() - t0
         walk = c.lookup_walk_groups()
@@ -59,6 +61,7 @@ def main():
             nit += r.iterations_run
         c.set_profiling(False)
         out[name] = {"ms_per_scan": 1e3 * el / args.aligns, "iters_per_scan": it / args.aligns,
+                     "device_ms_median": float(np.median(dev)),
                      "linearize_us_per_iter": 1e3 * lin / max(nit, 1), "first_align_ms": 1e3 * first,
                      "walk_groups_last_align": walk, "pose": pose.tolist(), "grid": info}
         print(name, json.dumps({k: v for k, v in out[name].items() if k != "pose"}), flush=True)
