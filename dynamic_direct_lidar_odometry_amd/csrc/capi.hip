@@ -186,6 +186,7 @@ struct FbLayout {
 constexpr double kGridCell = 0.4;
 constexpr double kGridMaxReach = 4.0;     // bounds beyond this: cells farther than it use the walk
 constexpr int kGridListMax = 32;
+constexpr int kGridAutoAligns = 32;       // GICP_GRID_AUTO: built at this align against the same target and bound
 constexpr int kGridListCap = kCgCandMax;  // finest level: longer lists are not stored (the walk)
 constexpr long kGridMaxCells = 48L << 20; // coarse cells (the directory is 4 B per cell)
 
@@ -238,7 +239,11 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   b.delta = 1e-4 + 4e-6 * (amax + M + S);
   b.capm = capm;
   b.nomatch_dist = (r - 1) * S - 1e-3;
-  b.lmax = kGridListMax;
+  static const int lmax_env = [] {   // development A/B of the list length (DDLO_GRID_LMAX)
+    const char* v = std::getenv("DDLO_GRID_LMAX");
+    return v && *v ? std::atoi(v) : 0;
+  }();
+  b.lmax = lmax_env > 0 ? lmax_env : kGridListMax;
   b.lcap = kGridListCap;
   const bool outside_nomatch = capm <= b.nomatch_dist;
   // scratch
@@ -447,7 +452,10 @@ gicp_status maybe_build_grid(gicp_ctx* c) {
     t.grid_aligns = 0;
   }
   ++t.grid_aligns;
-  if (c->grid_mode == GICP_GRID_AUTO && t.grid_aligns < 2) return GICP_OK;
+  // auto: only a target aligned against many times pays for its cells (a
+  // ~16 ms build for a 500k-point submap against ~0.15 ms saved per align);
+  // OdomNode's submaps live ~20 scans (DESIGN.md §4 "Candidate cells")
+  if (c->grid_mode == GICP_GRID_AUTO && t.grid_aligns < kGridAutoAligns) return GICP_OK;
   std::shared_ptr<CellGridData> g;
   const gicp_status s = cellgrid_build(c, t, cap2, &g);
   if (s) return s;

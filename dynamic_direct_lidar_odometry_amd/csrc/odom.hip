@@ -677,6 +677,7 @@ gicp_status ddlo_odom_default_params(ddlo_odom_params* p) {
   p->vf_submap_use = 1;
   p->vf_submap_res = 0.1;
   p->skip_first_scan = 1;
+  p->s2m_target_grid = GICP_GRID_OFF;
   return GICP_OK;
 }
 
@@ -697,6 +698,8 @@ gicp_status ddlo_odom_create(int device, const ddlo_odom_params* p, ddlo_odom** 
   if (!st) st = gicp_ctx_create(device, &o->s2m);
   if (!st) st = gicp_set_params(o->s2s, &o->p.s2s);
   if (!st) st = gicp_set_params(o->s2m, &o->p.s2m);
+  if (!st) st = gicp_set_target_grid(o->s2m, o->p.s2m_target_grid);
+  if (!st) st = gicp_set_target_grid(o->s2s, GICP_GRID_OFF);   // S2S targets live one scan
   if (st) {
     if (o->s2s) gicp_ctx_destroy(o->s2s);
     if (o->s2m) gicp_ctx_destroy(o->s2m);

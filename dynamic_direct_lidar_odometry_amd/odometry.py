@@ -38,6 +38,7 @@ class OdomParams(C.Structure):
         ("vf_submap_use", C.c_int32),
         ("vf_submap_res", C.c_double),
         ("skip_first_scan", C.c_int32),
+        ("s2m_target_grid", C.c_int32),
     ]
 
 

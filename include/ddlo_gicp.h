@@ -223,8 +223,8 @@ gicp_status gicp_set_tie_order(struct gicp_ctx* ctx, int nanoflann_order);
  * order); only the time differs.  It pays for a target that is aligned
  * against several times (the S2M submap: OdomNode keeps a submap for many
  * scans, odom.cc:1215-1315).  mode: 0 = off; 1 = auto (default): built at the
- * second align against the same target and bound; 2 = built at the next
- * align.  The structure belongs to the target cloud (it follows
+ * 32nd align against the same target and bound (a long-lived target; the
+ * build costs about a hundred aligns' savings); 2 = built at the next align.  The structure belongs to the target cloud (it follows
  * gicp_swap_source_target). */
 #define GICP_GRID_OFF 0
 #define GICP_GRID_AUTO 1

@@ -45,6 +45,9 @@ typedef struct ddlo_odom_params {
   int32_t skip_first_scan;         /* 1 (reference): the first scan with >= min_num_points points only
                                       initialises (initializeDDLO, odom.cc:641-646), so keyframe 0 is
                                       the second one; 0: the first scan becomes the target at once */
+  int32_t s2m_target_grid;         /* candidate cells of the S2M submap (gicp_set_target_grid): 0 off
+                                      (default: a submap lives ~20 scans, fewer than the build pays for),
+                                      1 auto, 2 on */
 } ddlo_odom_params;
 
 typedef enum ddlo_odom_status {

@@ -126,12 +126,15 @@ def test_grid_align_equals_walk_and_oracle(pair):
     cw.close()
 
 
-def test_grid_auto_builds_at_second_align(pair):
+def test_grid_auto_builds_for_a_long_lived_target(pair):
+    """GRID_AUTO builds the cells at the 32nd align against one target and bound."""
     tgt, src, T, tcov, scov = pair
     kw = dict(k_correspondences=10, max_correspondence_distance=2.0)
     c = make(tgt, src, tcov, scov, P.GRID_AUTO, **kw)
     G = perturbed(T, 0.2, 0.01).astype(np.float32)
     p1, r1 = c.align(G)
+    for _ in range(30):
+        c.align(G)
     assert c.grid_info()["built"] == 0
     p2, r2 = c.align(G)
     assert c.grid_info()["built"] == 1
