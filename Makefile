@@ -8,7 +8,7 @@ PKG := dynamic_direct_lidar_odometry_amd
 CSRC := $(PKG)/csrc
 LIBDIR := $(PKG)/_lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
-OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/nftree.o $(LIBDIR)/cellgrid.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o $(LIBDIR)/segment.o
+OBJS := $(LIBDIR)/kernels.o $(LIBDIR)/knn_tasks.o $(LIBDIR)/nftree.o $(LIBDIR)/cellgrid.o $(LIBDIR)/tietree.o $(LIBDIR)/capi.o $(LIBDIR)/preprocess.o $(LIBDIR)/odom.o $(LIBDIR)/segment.o
 
 all: lib oracle facade raycast
 
@@ -30,7 +30,11 @@ $(LIBDIR)/cellgrid.o: $(CSRC)/cellgrid.hip $(CSRC)/cellgrid.hpp $(CSRC)/search.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/runtime.hpp $(CSRC)/cellgrid.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h
+$(LIBDIR)/tietree.o: $(CSRC)/tietree.hip $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/capi.o: $(CSRC)/capi.hip $(CSRC)/nftree.hpp $(CSRC)/runtime.hpp $(CSRC)/cellgrid.hpp $(CSRC)/gicp_types.hpp $(CSRC)/launch.hpp include/ddlo_gicp.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -85,3 +89,11 @@ statsprof: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/statsprof/libddlo_gicp.so $(LIBDIR)/statsprof/kernels.o $(filter-out $(LIBDIR)/kernels.o,$(OBJS))
 
 .PHONY: statsprof
+
+# development build: the A/B environment knobs (devknobs.hpp) are read
+dev:
+	@mkdir -p $(LIBDIR)/dev
+	for f in $(notdir $(OBJS:.o=)); do $(HIPCC) $(HIPFLAGS) -DDDLO_DEV -c $(CSRC)/$$f.hip -o $(LIBDIR)/dev/$$f.o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/dev/libddlo_gicp.so $(addprefix $(LIBDIR)/dev/,$(notdir $(OBJS)))
+
+.PHONY: dev

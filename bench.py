@@ -204,7 +204,9 @@ def sharded_leg(dist, rank, world, local_rank, args):
     guess = prob["guess"].astype(np.float32)
     sh = ShardedGicp(local_rank, rank, world, uid, params, mode=args.shard_mode)
     sh.ctx.set_target_grid(P.GRID_ON)   # each rank's target's candidate cells, built at the first align
+    t_st = time.perf_counter()
     slab = sh.set_target(sub, tcov, source=src, guess=guess)
+    set_target_ms = 1e3 * (time.perf_counter() - t_st)
     sh.set_source(src, scov)
     log(f"[rank {rank}] sharded setup {time.time() - t0:.1f}s: src {len(src)} tgt {len(sub)} "
         f"local {len(sh.local_index)} mode {args.shard_mode}" +
@@ -235,6 +237,7 @@ def sharded_leg(dist, rank, world, local_rank, args):
     graphs = sh.ctx.comm_info()[2]
     # per-rank linearize roofline (eager profiled aligns: the all-reduce sits outside the timed kernels)
     roof = lin_roofline(sh.ctx, guess, len(src) / world, reps=3)
+    dev_bytes = sh.ctx.device_bytes()
     sh.close()
     out_leg = {"workload": "cfg4 S2M: 262,144-pt 128x2048 scan -> 2,000,000-pt 8-keyframe submap, LM, maxCorr 2.0 m",
                "n_gpus": world, "ms_per_scan": round(1e3 * elapsed / args.sharded_steps, 4),
@@ -246,7 +249,9 @@ def sharded_leg(dist, rank, world, local_rank, args):
                "collective": "RCCL all-reduce, 80 fp64 per outer iteration" + (" (in graph)" if graphs else " (eager)"),
                "scaling": "strong", "roofline_rank0": roof,
                "target_grid_rank0": {"built": grid["built"], "build_ms": round(grid["build_ms"], 3),
-                                     "bytes": grid["bytes"], "first_align_ms": round(first_align_ms, 3)}}
+                                     "bytes": grid["bytes"], "first_align_ms": round(first_align_ms, 3)},
+               "set_target_ms_rank0": round(set_target_ms, 2),
+               "device_mib_rank0": {k: round(v / 2**20, 2) for k, v in dev_bytes.items()}}
     if dist is not None:
         import torch
         t = torch.tensor([local_pts], dtype=torch.int64, device=f"cuda:{local_rank}")
@@ -403,21 +408,10 @@ def cfg5_stage_rooflines(frames, params, device, nframes=24):
                                             "linearize = k_nn_seed + k_nn_scan + k_moments", "B_lin = 76 B x N_s")}
 
 
-class tie_order_env:
-    """Contexts created inside the block use the Morton tie order (DDLO_TIE_EXACT=0; read at ctx creation)."""
-
-    def __init__(self, v):
-        self.v = v
-
-    def __enter__(self):
-        self.old = os.environ.get("DDLO_TIE_EXACT")
-        os.environ["DDLO_TIE_EXACT"] = self.v
-
-    def __exit__(self, *a):
-        if self.old is None:
-            os.environ.pop("DDLO_TIE_EXACT", None)
-        else:
-            os.environ["DDLO_TIE_EXACT"] = self.old
+def tie_order_env(v):
+    """Contexts created inside the block use the given tie order ("0": Morton, no nanoflann trees)."""
+    import dynamic_direct_lidar_odometry_amd as P
+    return P.default_option(P.OPT_TIE_ORDER, int(v))
 
 
 def s2s_gn_leg(local_rank, args):

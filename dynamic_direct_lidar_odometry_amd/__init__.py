@@ -117,6 +117,16 @@ def load():
     path = lib_path()
     if not os.path.exists(path):
         raise RuntimeError(f"HIP library not built: {path} (run __graft_entry__.build() or `make lib`)")
+    # PyTorch-ROCm ships its own libamdhip64.so.7 and librccl.so.1 under the
+    # same sonames as /opt/rocm's: whichever loads first serves the whole
+    # process.  Loading this library (ROCm's) first and torch afterwards (e.g.
+    # torch.distributed for the shard ranks' unique id) leaves torch's other
+    # bundled libraries on ROCm's runtime, and the process aborts in its exit
+    # teardown.  So torch, when installed, loads first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(path)
     P, S, I, D = C.c_void_p, C.c_size_t, C.c_int, C.c_double
     sig = {
@@ -159,6 +169,16 @@ def load():
         "gicp_s2s_batch": (I, [I, C.POINTER(GicpParams), P, P, S, I, I, P, P]),
         "gicp_residual_image": (I, [P, D, D, I, I, P, P]),
         "gicp_set_tie_order": (I, [P, I]),
+        "gicp_get_tie_order": (I, [P, C.POINTER(C.c_int)]),
+        "gicp_set_option": (I, [P, I, I]),
+        "gicp_get_option": (I, [P, I, C.POINTER(C.c_int)]),
+        "gicp_set_default_option": (I, [I, I]),
+        "gicp_get_default_option": (I, [I, C.POINTER(C.c_int)]),
+        "gicp_tie_builder_set": (I, [P, P, C.c_size_t, C.c_size_t]),
+        "gicp_tie_builder_export": (I, [P, P, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+        "gicp_set_tie_tree": (I, [P, P, C.c_size_t]),
+        "gicp_set_tie_trees_from_root": (I, [P, I, P, P]),
+        "gicp_get_device_bytes": (I, [P, C.POINTER(C.c_int64), I]),
         "gicp_debug_nftree": (I, [P, I, P, P, P, S, C.POINTER(S)]),
         "gicp_debug_nfbuild": (I, [P, I, I, P, P, P, P, S]),
         "gicp_set_target_grid": (I, [P, I]),
@@ -191,6 +211,41 @@ def _xyz(points):
         return a, a.strides[0]
     a = np.ascontiguousarray(np.asarray(points, dtype=np.float32).reshape(-1, 3))
     return a, 12
+
+
+OPT_TIE_ORDER, OPT_TIE_LAZY, OPT_TIE_PARTIAL_LEVELS, OPT_COV_TASKS = 1, 2, 3, 4
+
+
+def set_default_option(option: int, value: int):
+    """The value contexts created from now on start with (gicp_set_default_option; process-wide)."""
+    L = load()
+    rc = L.gicp_set_default_option(int(option), int(value))
+    if rc != 0:
+        raise GicpError(rc, L.gicp_last_error().decode())
+
+
+def get_default_option(option: int) -> int:
+    L = load()
+    v = C.c_int(0)
+    rc = L.gicp_get_default_option(int(option), C.byref(v))
+    if rc != 0:
+        raise GicpError(rc, L.gicp_last_error().decode())
+    return int(v.value)
+
+
+class default_option:
+    """Context manager: contexts created inside the block start with option = value."""
+
+    def __init__(self, option: int, value: int):
+        self.option, self.value = option, value
+
+    def __enter__(self):
+        self.old = get_default_option(self.option)
+        set_default_option(self.option, self.value)
+        return self
+
+    def __exit__(self, *a):
+        set_default_option(self.option, self.old)
 
 
 def comm_unique_id() -> bytes:
@@ -449,14 +504,70 @@ class Context:
         self._check(self.L.gicp_set_shard_groups(self.h, int(nparts), int(part)))
 
     def set_tie_target(self, points, local_index):
-        """Slab shard: the whole target its local target was cut from and each local point's index in it
-        (exact ties resolve in the whole target's nanoflann order).  points=None removes it."""
+        """Slab shard, single process: the whole target its local target was cut from and each local
+        point's index in it.  Exact ties resolve through the whole target's nanoflann tree restricted to
+        the local points (the whole cloud is released before the call returns).  points=None removes it."""
         if points is None:
             self._check(self.L.gicp_set_tie_target(self.h, None, 0, 12, None, 0))
             return
         a, stride = _xyz(points)
         li = np.ascontiguousarray(local_index, np.int32)
         self._check(self.L.gicp_set_tie_target(self.h, _ptr(a), len(a), stride, _ptr(li), len(li)))
+
+    def set_option(self, option: int, value: int):
+        """gicp_set_option (OPT_TIE_ORDER, OPT_TIE_LAZY, OPT_TIE_PARTIAL_LEVELS, OPT_COV_TASKS)."""
+        self._check(self.L.gicp_set_option(self.h, int(option), int(value)))
+
+    def get_option(self, option: int) -> int:
+        v = C.c_int(0)
+        self._check(self.L.gicp_get_option(self.h, int(option), C.byref(v)))
+        return int(v.value)
+
+    def tie_order(self) -> bool:
+        """True: exact ties in nanoflann's order (default); False: Morton order."""
+        v = C.c_int(0)
+        self._check(self.L.gicp_get_tie_order(self.h, C.byref(v)))
+        return bool(v.value)
+
+    def tie_builder_set(self, points):
+        """Tie builder (one rank per submap): the whole submap and its nanoflann tree; None frees them."""
+        if points is None:
+            self._check(self.L.gicp_tie_builder_set(self.h, None, 0, 12))
+            return
+        a, stride = _xyz(points)
+        self._check(self.L.gicp_tie_builder_set(self.h, _ptr(a), len(a), stride))
+
+    def tie_builder_export(self, local_index) -> bytes:
+        """The builder's tree restricted to the points local_index names (whole-cloud indices, one per
+        local target point): the blob a slab rank installs with set_tie_tree."""
+        li = np.ascontiguousarray(local_index, np.int32)
+        p, n = C.c_void_p(), C.c_size_t(0)
+        self._check(self.L.gicp_tie_builder_export(self.h, _ptr(li), len(li), C.byref(p), C.byref(n)))
+        return C.string_at(p.value, n.value)
+
+    def set_tie_tree(self, blob: bytes | None):
+        """Slab shard: install the restriction of the whole submap's tree to this rank's target (None removes it)."""
+        if not blob:
+            self._check(self.L.gicp_set_tie_tree(self.h, None, 0))
+            return
+        self._check(self.L.gicp_set_tie_tree(self.h, blob, len(blob)))
+
+    def set_tie_trees_from_root(self, root: int, blobs: list[bytes] | None):
+        """Collective over this ctx's communicator: the root passes every rank's blob, the others None."""
+        if blobs is None:
+            self._check(self.L.gicp_set_tie_trees_from_root(self.h, int(root), None, None))
+            return
+        bufs = [C.create_string_buffer(b, len(b)) for b in blobs]
+        ptrs = (C.c_void_p * len(bufs))(*[C.cast(b, C.c_void_p) for b in bufs])
+        sizes = (C.c_size_t * len(bufs))(*[len(b) for b in blobs])
+        self._check(self.L.gicp_set_tie_trees_from_root(self.h, int(root), ptrs, sizes))
+
+    def device_bytes(self) -> dict:
+        """Device bytes this ctx holds, by part (gicp_get_device_bytes)."""
+        v = (C.c_int64 * 7)()
+        self._check(self.L.gicp_get_device_bytes(self.h, v, 7))
+        keys = ("total", "target", "source", "covariances", "tie_tree", "tie_builder", "scratch")
+        return {k: int(x) for k, x in zip(keys, v)}
 
     def set_comm(self, unique_id: bytes | None, nranks: int, rank: int):
         buf = None

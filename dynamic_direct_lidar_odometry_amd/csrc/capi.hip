@@ -34,6 +34,8 @@
 #include "launch.hpp"
 #include "runtime.hpp"
 #include "cellgrid.hpp"
+#include "nftree.hpp"   // kNfStack: the search depth a tie tree must fit
+#include "devknobs.hpp"
 
 
 namespace {
@@ -47,6 +49,11 @@ struct Rccl {
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclBroadcast) broadcast = nullptr;   // gicp_set_tie_trees_from_root
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   bool ok = false;
   std::string why;
@@ -67,6 +74,11 @@ const Rccl& rccl() {
     x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
     x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
     x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+    x.broadcast = (decltype(x.broadcast))dlsym(h, "ncclBroadcast");
+    x.send = (decltype(x.send))dlsym(h, "ncclSend");
+    x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
+    x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+    x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
     x.ok = x.get_unique_id && x.comm_init_rank && x.comm_destroy && x.all_reduce && x.error_string;
     if (!x.ok) x.why = "RCCL is missing an entry point";
     return x;
@@ -85,7 +97,7 @@ const Rccl& rccl() {
 // Tuning knob of the search (development; the default is the tuned value)
 constexpr float kSplitExtentDefault = 5.0f;
 float env_float(const char* name, float dflt) {
-  const char* v = std::getenv(name);
+  const char* v = dev_getenv(name);
   if (!v || !*v) return dflt;
   char* end = nullptr;
   const float f = std::strtof(v, &end);
@@ -93,8 +105,30 @@ float env_float(const char* name, float dflt) {
 }
 
 int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
+  const char* v = dev_getenv(name);
   return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// Options (gicp_set_option): the values new contexts take.  A -DDDLO_DEV
+// build still reads the old A/B environment variables as the initial values.
+static std::atomic<int> g_opt_default[GICP_OPT_COUNT] = {{0}, {1}, {1}, {3}, {0}};
+static const bool g_opt_env_read = [] {
+  auto rd = [](const char* name, int opt, bool flag) {
+    const char* v = dev_getenv(name);
+    if (v && *v) g_opt_default[opt].store(flag ? (*v != '0') : std::max(0, std::atoi(v)));
+  };
+  rd("DDLO_TIE_EXACT", GICP_OPT_TIE_ORDER, true);
+  rd("DDLO_TIE_LAZY", GICP_OPT_TIE_LAZY, true);
+  rd("DDLO_TIE_PARTIAL_LEVELS", GICP_OPT_TIE_PARTIAL_LEVELS, false);
+  rd("DDLO_COV_TASKS", GICP_OPT_COV_TASKS, true);
+  return true;
+}();
+
+static gicp_status check_option(int option, int value) {
+  if (option <= 0 || option >= GICP_OPT_COUNT) return fail(GICP_EINVAL, "unknown option");
+  if (option == GICP_OPT_TIE_PARTIAL_LEVELS ? (value < 0 || value > 24) : (value != 0 && value != 1))
+    return fail(GICP_EINVAL, "option value out of range");
+  return GICP_OK;
 }
 
 // The search's development knobs, read from the environment once per
@@ -240,7 +274,7 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   b.capm = capm;
   b.nomatch_dist = (r - 1) * S - 1e-3;
   static const int lmax_env = [] {   // development A/B of the list length (DDLO_GRID_LMAX)
-    const char* v = std::getenv("DDLO_GRID_LMAX");
+    const char* v = dev_getenv("DDLO_GRID_LMAX");
     return v && *v ? std::atoi(v) : 0;
   }();
   b.lmax = lmax_env > 0 ? lmax_env : kGridListMax;
@@ -556,19 +590,17 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   // search tracks the examined points' second distance; the target's tree,
   // when it exists, re-runs the tied queries.  Slab shards hold a subset of
   // the target, whose tree orders ties differently: Morton order there.
-  j.tie_detect = (c->tie_exact && (c->own_axis < 0 || c->tie_ref)) ? 1 : 0;
+  j.tie_detect = (c->tie_exact && (c->own_axis < 0 || c->tie_tree)) ? 1 : 0;
   j.tgt_nf = NfTreeDev{nullptr, nullptr, nullptr, 0};
   j.tgt_nf_status = nullptr;
-  j.tie_map = nullptr;
   j.tie_scan = j.tie_detect ? kn.tie_scan : 0;
   j.tie_ab = kn.tie_ab;
   if (j.tie_detect) {
-    const CloudData* tc = c->tie_ref ? c->tie_ref.get() : c->tgt.cloud.get();
-    if (tc->nf) {
-      j.tgt_nf = tc->nf->dev();
-      j.tgt_nf_status = tc->nf->status.as<int>();
+    const NfTreeData* tt = c->tie_tree ? c->tie_tree.get() : c->tgt.cloud->nf.get();
+    if (tt) {
+      j.tgt_nf = tt->dev();
+      j.tgt_nf_status = tt->status.as<int>();
     }
-    if (c->tie_ref) j.tie_map = c->tie_map.as<int>();
   }
   // the target's candidate cells answer the search first (k_cell_lookup)
   j.grid_on = grid_active(c) ? 1 : 0;
@@ -629,13 +661,13 @@ gicp_status prepare_align(gicp_ctx* c) {
   // front (every rank the same tree, so no rank ever re-runs alone and the
   // collectives stay matched); otherwise it is built only when an align
   // meets a tie (gicp_align).  The stream waits once for a tree's build.
-  if (c->tie_exact && (c->own_axis < 0 || c->tie_ref)) {
-    CloudData& tc = c->tie_ref ? *c->tie_ref : *c->tgt.cloud;
-    if ((c->comm || c->tie_ref) && !tc.nf) {
+  if (c->tie_exact && (c->own_axis < 0 || c->tie_tree)) {
+    CloudData& tc = *c->tgt.cloud;
+    if (c->comm && !c->tie_tree && !tc.nf) {
       gicp_status s = ensure_nftree(c, tc, c->stream);
       if (s) return s;
     }
-    const auto& nf = tc.nf;
+    const auto& nf = c->tie_tree ? c->tie_tree : tc.nf;
     if (nf && c->nf_joined.lock() != nf) {
       HIP_TRY(nftree_join(*nf, c->stream));
       c->nf_joined = nf;
@@ -803,7 +835,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   // the host polls the chunk's event (hipEventQuery) instead of blocking in
   // hipEventSynchronize: 2 us less per align at cfg 3 (DDLO_SPIN_WAIT=0: block)
   static const bool spin = [] {
-    const char* v = std::getenv("DDLO_SPIN_WAIT");
+    const char* v = dev_getenv("DDLO_SPIN_WAIT");
     return !(v && *v == '0');
   }();
   for (;;) {
@@ -905,7 +937,7 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
 namespace ddlo {
 bool lm_fusion_enabled() {
   static const bool on = [] {
-    const char* v = std::getenv("DDLO_FUSE_LM");
+    const char* v = dev_getenv("DDLO_FUSE_LM");
     return v && *v && std::atoi(v) != 0;
   }();
   return on;
@@ -960,16 +992,16 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
+  // options (gicp_set_default_option: the process-wide values new contexts take)
+  c->tie_exact = g_opt_default[GICP_OPT_TIE_ORDER].load() != 0;
+  c->tie_lazy = g_opt_default[GICP_OPT_TIE_LAZY].load() != 0;
+  c->partial_levels = g_opt_default[GICP_OPT_TIE_PARTIAL_LEVELS].load();
+  c->cov_tasks = g_opt_default[GICP_OPT_COV_TASKS].load() != 0;
   {
-    const char* v = std::getenv("DDLO_TIE_EXACT");   // A/B of the tie resolution (default: nanoflann's order)
-    c->tie_exact = !(v && *v == '0');
-    const char* lz = std::getenv("DDLO_TIE_LAZY");   // 0: covariance ties through the whole tree (A/B)
-    c->tie_lazy = !(lz && *lz == '0');
-    const char* pl = std::getenv("DDLO_TIE_PARTIAL_LEVELS");
-    if (pl) c->partial_levels = std::max(0, std::atoi(pl));
-    // DDLO_NF_OWN_STREAM=1: every ctx builds its trees on its own stream, the
-    // partial tree gated on the tie count (the S2S batch's workers always do)
-    const char* os = std::getenv("DDLO_NF_OWN_STREAM");
+    // DDLO_NF_OWN_STREAM=1 (development): every ctx builds its trees on its
+    // own stream, the partial tree gated on the tie count (the S2S batch's
+    // workers always do)
+    const char* os = dev_getenv("DDLO_NF_OWN_STREAM");
     c->nf_same_stream = os && *os == '1';
   }
   *out = c.release();
@@ -978,7 +1010,7 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
 
 gicp_status gicp_ctx_destroy(gicp_ctx* c) {
   if (!c) return GICP_OK;
-  if (std::getenv("DDLO_GRAPH_DEBUG")) std::fprintf(stderr, "[graphs] ctx %p: %ld chunk captures\n", (void*)c, c->captures);
+  if (dev_getenv("DDLO_GRAPH_DEBUG")) std::fprintf(stderr, "[graphs] ctx %p: %ld chunk captures\n", (void*)c, c->captures);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->aux_stream);
@@ -1076,7 +1108,7 @@ gicp_status gicp_set_target(gicp_ctx* c, const float* xyz, size_t n, size_t stri
   if (s) return s;
   c->tgt.cloud = cd;
   c->tgt.cov.reset();  // (:154)
-  c->tie_ref.reset();  // a slab's whole-target tie order belongs to the previous target
+  c->tie_tree.reset();  // a slab's tie order belongs to the previous target
   invalidate_align(c);
   return GICP_OK;
 }
@@ -1090,7 +1122,7 @@ gicp_status gicp_clear_source(gicp_ctx* c) {
 gicp_status gicp_clear_target(gicp_ctx* c) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
   c->tgt = Side();
-  c->tie_ref.reset();   // a slab's whole-target tie order belongs to the cleared target
+  c->tie_tree.reset();   // a slab's tie order belongs to the cleared target
   invalidate_align(c);
   return GICP_OK;
 }
@@ -1159,7 +1191,7 @@ gicp_status gicp_has_covariances(const gicp_ctx* c, int side, int* has) {
 gicp_status gicp_swap_source_target(gicp_ctx* c) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
   std::swap(c->src, c->tgt);  // clouds, indices and covariances (:100-102)
-  c->tie_ref.reset();         // the whole-target tie order (and its index map) belonged to the old target
+  c->tie_tree.reset();        // a slab's tie order belonged to the old target
   invalidate_align(c);        // correspondences_.clear() (:104-105)
   return GICP_OK;
 }
@@ -1463,6 +1495,90 @@ gicp_status gicp_set_tie_order(gicp_ctx* c, int nanoflann_order) {
   return GICP_OK;
 }
 
+gicp_status gicp_set_option(gicp_ctx* c, int option, int value) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  gicp_status s = check_option(option, value);
+  if (s) return s;
+  switch (option) {
+    case GICP_OPT_TIE_ORDER: c->tie_exact = value != 0; break;
+    case GICP_OPT_TIE_LAZY: c->tie_lazy = value != 0; break;
+    case GICP_OPT_TIE_PARTIAL_LEVELS: c->partial_levels = value; break;
+    case GICP_OPT_COV_TASKS: c->cov_tasks = value != 0; break;
+  }
+  return GICP_OK;
+}
+
+gicp_status gicp_get_option(const gicp_ctx* c, int option, int* value) {
+  if (!c || !value) return fail(GICP_EINVAL, "null argument");
+  gicp_status s = check_option(option, 0);
+  if (s) return s;
+  switch (option) {
+    case GICP_OPT_TIE_ORDER: *value = c->tie_exact ? 1 : 0; break;
+    case GICP_OPT_TIE_LAZY: *value = c->tie_lazy ? 1 : 0; break;
+    case GICP_OPT_TIE_PARTIAL_LEVELS: *value = c->partial_levels; break;
+    case GICP_OPT_COV_TASKS: *value = c->cov_tasks ? 1 : 0; break;
+  }
+  return GICP_OK;
+}
+
+gicp_status gicp_set_default_option(int option, int value) {
+  gicp_status s = check_option(option, value);
+  if (s) return s;
+  g_opt_default[option].store(value);
+  return GICP_OK;
+}
+
+gicp_status gicp_get_default_option(int option, int* value) {
+  if (!value) return fail(GICP_EINVAL, "null argument");
+  gicp_status s = check_option(option, 0);
+  if (s) return s;
+  *value = g_opt_default[option].load();
+  return GICP_OK;
+}
+
+gicp_status gicp_get_tie_order(const gicp_ctx* c, int* nanoflann_order) {
+  if (!c || !nanoflann_order) return fail(GICP_EINVAL, "null argument");
+  *nanoflann_order = c->tie_exact ? 1 : 0;
+  return GICP_OK;
+}
+
+namespace {
+int64_t tree_bytes(const std::shared_ptr<NfTreeData>& t) {
+  return t ? (int64_t)(t->vpts.bytes + t->nodes.bytes + t->box.bytes + t->status.bytes + t->sbox.bytes) : 0;
+}
+int64_t cloud_bytes(const std::shared_ptr<CloudData>& cd) {
+  if (!cd) return 0;
+  const CloudData& d = *cd;
+  int64_t b = (int64_t)(d.pts.bytes + d.keys.bytes + d.perm.bytes + d.inv_perm.bytes + d.box_lo.bytes +
+                        d.box_hi.bytes + d.quant.bytes + d.soa.bytes + d.dir.bytes);
+  b += tree_bytes(d.nf) + tree_bytes(d.nfp);
+  if (d.grid) b += (int64_t)(d.grid->dir.bytes + d.grid->fine.bytes + d.grid->ent.bytes);
+  return b;
+}
+}  // namespace
+
+gicp_status gicp_get_device_bytes(const gicp_ctx* c, int64_t* out, int nout) {
+  if (!c || !out || nout < 1) return fail(GICP_EINVAL, "null argument");
+  int64_t v[7] = {0, 0, 0, 0, 0, 0, 0};
+  v[1] = cloud_bytes(c->tgt.cloud);
+  v[2] = c->src.cloud == c->tgt.cloud ? 0 : cloud_bytes(c->src.cloud);
+  v[3] = (c->tgt.cov ? (int64_t)c->tgt.cov->cov6.bytes : 0) + (c->src.cov && c->src.cov != c->tgt.cov ? (int64_t)c->src.cov->cov6.bytes : 0);
+  v[4] = tree_bytes(c->tie_tree);
+  v[5] = cloud_bytes(c->tie_whole) + (int64_t)(c->tie_scratch.bytes + c->tie_lidx.bytes + c->tie_out_nodes.bytes +
+                                               c->tie_out_pts.bytes + c->tie_counts.bytes);
+  const DevBuf* scratch[] = {&c->raw_bytes, &c->raw_pts, &c->partial, &c->nonfinite, &c->keys_tmp, &c->vals_tmp,
+                             &c->sort_tmp, &c->knn, &c->corr, &c->sqd, &c->slab, &c->job_dev, &c->state_dev,
+                             &c->tmp_out, &c->stats, &c->nf_desc, &c->mom, &c->search, &c->nf_scratch, &c->tie_buf,
+                             &c->nf_err, &c->lazy_buf, &c->fb};
+  for (const DevBuf* b : scratch) v[6] += (int64_t)b->bytes;
+  if (c->nf_gated) v[6] += (int64_t)(c->nf_gated->vpts.bytes + c->nf_gated->nodes.bytes + c->nf_gated->box.bytes +
+                                     c->nf_gated->status.bytes + c->nf_gated->sbox.bytes);
+  v[0] = v[1] + v[2] + v[3] + v[4] + v[5] + v[6];
+  for (int i = 0; i < nout && i < 7; ++i) out[i] = v[i];
+  for (int i = 7; i < nout; ++i) out[i] = 0;
+  return GICP_OK;
+}
+
 gicp_status gicp_set_target_grid(gicp_ctx* c, int mode) {
   if (!c) return fail(GICP_EINVAL, "null ctx");
   if (mode < GICP_GRID_OFF || mode > GICP_GRID_ON) return fail(GICP_EINVAL, "grid mode must be 0 (off), 1 (auto) or 2 (on)");
@@ -1623,53 +1739,264 @@ gicp_status gicp_set_shard(gicp_ctx* c, int axis, float lo, float hi) {
   return GICP_OK;
 }
 
-gicp_status gicp_set_tie_target(gicp_ctx* c, const float* xyz, size_t n, size_t stride, const int32_t* local_index,
-                                size_t n_local) {
-  if (!c) return fail(GICP_EINVAL, "null ctx");
-  if (n == 0) {
-    c->tie_ref.reset();
-    return GICP_OK;
-  }
-  if (!xyz || !local_index) return fail(GICP_EINVAL, "null argument");
-  if (!c->tgt.cloud || (int)n_local != c->tgt.cloud->n) return fail(GICP_ESTATE, "set the local target first (n_local = its size)");
+// ---- slab shards' tie order (tietree.hip, DESIGN.md §5 "Slab shards") ----
+// Blob: header, the restricted tree's nodes, its points (x, y, z, local index).
+struct TieBlobHeader {
+  uint32_t magic, version;
+  int32_t n_local, nnodes;
+  float box[8];   // root_bbox lo (x, y, z, 0), hi (x, y, z, 0): the whole submap's
+};
+constexpr uint32_t kTieBlobMagic = 0x31545444u;   // "DTT1"
+
+namespace {
+gicp_status check_local_index(const int32_t* local_index, size_t n_local, size_t n) {
   std::vector<unsigned char> seen(n, 0);
   for (size_t i = 0; i < n_local; ++i) {
     if (local_index[i] < 0 || (size_t)local_index[i] >= n) return fail(GICP_EINVAL, "local_index out of range");
     if (seen[(size_t)local_index[i]]++) return fail(GICP_EINVAL, "local_index is not one-to-one");
   }
+  return GICP_OK;
+}
+}  // namespace
+
+gicp_status gicp_tie_builder_set(gicp_ctx* c, const float* xyz, size_t n, size_t stride) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
   gicp_status s = set_device(c);
   if (s) return s;
-  {
-    // the local target's point i must be the whole cloud's point local_index[i]
-    // (a tied correspondence is remapped through this index)
-    std::vector<float4> lp((size_t)n_local);
-    HIP_TRY(hipMemcpyAsync(lp.data(), c->tgt.cloud->pts.p, sizeof(float4) * n_local, hipMemcpyDeviceToHost, c->stream));
+  if (n == 0) {
     HIP_TRY(hipStreamSynchronize(c->stream));
-    const unsigned char* base = reinterpret_cast<const unsigned char*>(xyz);
-    for (size_t j = 0; j < n_local; ++j) {
-      int orig;
-      std::memcpy(&orig, &lp[j].w, sizeof(int));
-      float w[3];
-      std::memcpy(w, base + (size_t)local_index[orig] * stride, sizeof(w));
-      if (w[0] != lp[j].x || w[1] != lp[j].y || w[2] != lp[j].z)
-        return fail(GICP_EINVAL, "local_index does not map the local target's points onto the whole cloud's");
-    }
+    c->tie_whole.reset();
+    c->tie_scratch.reset();
+    c->tie_lidx.reset();
+    c->tie_out_nodes.reset();
+    c->tie_out_pts.reset();
+    c->tie_counts.reset();
+    std::vector<unsigned char>().swap(c->tie_blob);
+    return GICP_OK;
   }
+  if (!xyz) return fail(GICP_EINVAL, "null argument");
   std::shared_ptr<CloudData> cd;
   s = build_cloud(c, xyz, n, stride, &cd);
   if (s) return s;
-  s = ensure_nftree(c, *cd, c->stream);
+  auto t = std::make_shared<NfTreeData>();
+  s = nftree_build(c, *cd, c->stream, *t, -1, nullptr, -1, nullptr, /*zero_nodes=*/true);
   if (s) return s;
-  HIP_TRY(c->tie_map.ensure(sizeof(int) * (n + n_local)));
-  int* map = c->tie_map.as<int>();
-  int* lidx = map + n;
-  HIP_TRY(hipMemcpyAsync(lidx, local_index, sizeof(int) * n_local, hipMemcpyHostToDevice, c->stream));
-  launch_tie_map(c->stream, lidx, c->tgt.cloud->inv_perm.as<int>(), (int)n_local, (int)n, map);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(nftree_join(*t, c->stream));
+  cd->nf = t;
+  c->tie_whole = cd;
+  return GICP_OK;
+}
+
+gicp_status gicp_tie_builder_export(gicp_ctx* c, const int32_t* local_index, size_t n_local, const void** blob,
+                                    size_t* bytes) {
+  if (!c || !blob || !bytes) return fail(GICP_EINVAL, "null argument");
+  *blob = nullptr;
+  *bytes = 0;
+  if (!c->tie_whole || !c->tie_whole->nf) return fail(GICP_ESTATE, "no whole cloud: gicp_tie_builder_set first");
+  if (n_local == 0 || !local_index) return fail(GICP_EINVAL, "empty local_index");
+  const CloudData& W = *c->tie_whole;
+  const NfTreeData& T = *W.nf;
+  gicp_status s = check_local_index(local_index, n_local, (size_t)W.n);
+  if (s) return s;
+  s = set_device(c);
+  if (s) return s;
+  HIP_TRY(c->tie_scratch.ensure(tie_prune_scratch_bytes(T.n, T.cap)));
+  HIP_TRY(c->tie_lidx.ensure(sizeof(int) * n_local));
+  HIP_TRY(c->tie_out_nodes.ensure(sizeof(NfNode) * (size_t)T.cap));
+  HIP_TRY(c->tie_out_pts.ensure(sizeof(float4) * n_local));
+  HIP_TRY(c->tie_counts.ensure(sizeof(unsigned) * 4 + 2 * sizeof(float4)));
+  HIP_TRY(hipMemcpyAsync(c->tie_lidx.p, local_index, sizeof(int) * n_local, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(launch_tie_prune(c->stream, T.dev(), T.cap, c->tie_lidx.as<int>(), (int)n_local, c->tie_scratch.p,
+                           c->tie_out_nodes.as<NfNode>(), c->tie_out_pts.as<float4>(), c->tie_counts.as<unsigned>()));
+  unsigned cnt[4];
+  float4 box[2];
+  int bstat = 0;
+  HIP_TRY(hipMemcpyAsync(cnt, c->tie_counts.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(box, T.box.p, sizeof(box), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(&bstat, T.status.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  c->tie_ref = cd;
+  if (bstat) return fail(GICP_EHIP, "the whole cloud's tree build failed");
+  if (cnt[2] || cnt[0] != (unsigned)n_local || cnt[1] == 0 || cnt[1] > (unsigned)T.cap)
+    return fail(GICP_EHIP, "tie tree restriction failed");
+  const size_t nb = sizeof(TieBlobHeader) + sizeof(NfNode) * cnt[1] + sizeof(float4) * n_local;
+  c->tie_blob.resize(nb);
+  TieBlobHeader h{};
+  h.magic = kTieBlobMagic;
+  h.version = 1;
+  h.n_local = (int32_t)n_local;
+  h.nnodes = (int32_t)cnt[1];
+  std::memcpy(h.box, box, sizeof(h.box));
+  std::memcpy(c->tie_blob.data(), &h, sizeof(h));
+  unsigned char* q = c->tie_blob.data() + sizeof(h);
+  HIP_TRY(hipMemcpyAsync(q, c->tie_out_nodes.p, sizeof(NfNode) * cnt[1], hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(q + sizeof(NfNode) * cnt[1], c->tie_out_pts.p, sizeof(float4) * n_local,
+                         hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  *blob = c->tie_blob.data();
+  *bytes = nb;
+  return GICP_OK;
+}
+
+gicp_status gicp_set_tie_tree(gicp_ctx* c, const void* blob, size_t bytes) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  if (bytes == 0) {
+    c->tie_tree.reset();
+    invalidate_align(c);
+    return GICP_OK;
+  }
+  if (!blob || bytes < sizeof(TieBlobHeader)) return fail(GICP_EINVAL, "tie tree blob too short");
+  TieBlobHeader h;
+  std::memcpy(&h, blob, sizeof(h));
+  if (h.magic != kTieBlobMagic || h.version != 1) return fail(GICP_EINVAL, "not a tie tree blob");
+  if (!c->tgt.cloud) return fail(GICP_ESTATE, "set the local target first");
+  const int nl = c->tgt.cloud->n;
+  if (h.n_local != nl) return fail(GICP_EINVAL, "tie tree is not for a target of this size");
+  if (h.nnodes < 1 || bytes != sizeof(h) + sizeof(NfNode) * (size_t)h.nnodes + sizeof(float4) * (size_t)nl)
+    return fail(GICP_EINVAL, "tie tree blob size mismatch");
+  const unsigned char* q = static_cast<const unsigned char*>(blob) + sizeof(h);
+  std::vector<NfNode> nodes((size_t)h.nnodes);
+  std::vector<float4> pts((size_t)nl);
+  std::memcpy(nodes.data(), q, sizeof(NfNode) * nodes.size());
+  std::memcpy(pts.data(), q + sizeof(NfNode) * nodes.size(), sizeof(float4) * pts.size());
+  // a tree: every node reached once from the root, within the search's depth;
+  // the leaves' point ranges partition [0, n_local)
+  {
+    std::vector<unsigned char> seen(nodes.size(), 0);
+    std::vector<std::pair<int, int>> st{{0, 0}};
+    long covered = 0;
+    std::vector<int> cover((size_t)nl + 1, 0);
+    while (!st.empty()) {
+      const auto [v, d] = st.back();
+      st.pop_back();
+      if (v < 0 || v >= h.nnodes || seen[(size_t)v]++ || d >= kNfStack) return fail(GICP_EINVAL, "tie tree is not a tree");
+      const NfNode& nd = nodes[(size_t)v];
+      if (nd.feat == -1) {
+        if (nd.c1 < 0 || nd.c2 > nl || nd.c1 > nd.c2) return fail(GICP_EINVAL, "tie tree leaf range out of bounds");
+        covered += nd.c2 - nd.c1;
+        cover[(size_t)nd.c1] += 1;
+        cover[(size_t)nd.c2] -= 1;
+      } else {
+        if (nd.feat < 0 || nd.feat > 2) return fail(GICP_EINVAL, "tie tree node has no cut dimension");
+        st.push_back({nd.c2, d + 1});
+        st.push_back({nd.c1, d + 1});
+      }
+    }
+    int run = 0;
+    for (int i = 0; i < nl; ++i)
+      if ((run += cover[(size_t)i]) != 1) return fail(GICP_EINVAL, "tie tree leaves do not partition the points");
+    if (covered != nl) return fail(GICP_EINVAL, "tie tree leaves do not partition the points");
+  }
+  gicp_status s = set_device(c);
+  if (s) return s;
+  {
+    // its points are the local target's, each once (point ids = local indices)
+    std::vector<float4> lp((size_t)nl);
+    HIP_TRY(hipMemcpyAsync(lp.data(), c->tgt.cloud->pts.p, sizeof(float4) * nl, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::vector<float4> by_orig((size_t)nl);
+    for (const float4& p : lp) {
+      int o;
+      std::memcpy(&o, &p.w, sizeof(int));
+      by_orig[(size_t)o] = p;
+    }
+    std::vector<unsigned char> seen((size_t)nl, 0);
+    for (const float4& p : pts) {
+      int w;
+      std::memcpy(&w, &p.w, sizeof(int));
+      if (w < 0 || w >= nl || seen[(size_t)w]++) return fail(GICP_EINVAL, "tie tree points are not the local target's");
+      const float4& l = by_orig[(size_t)w];
+      if (l.x != p.x || l.y != p.y || l.z != p.z)
+        return fail(GICP_EINVAL, "tie tree points are not the local target's (local_index does not map the local "
+                                 "target's points onto the whole cloud's)");
+    }
+  }
+  auto t = std::make_shared<NfTreeData>();
+  t->n = nl;
+  t->cap = h.nnodes;
+  HIP_TRY(t->vpts.ensure(sizeof(float4) * (size_t)nl));
+  HIP_TRY(t->nodes.ensure(sizeof(NfNode) * (size_t)h.nnodes));
+  HIP_TRY(t->box.ensure(2 * sizeof(float4)));
+  HIP_TRY(t->status.ensure(2 * sizeof(int)));
+  HIP_TRY(hipEventCreateWithFlags(&t->ready, hipEventDisableTiming));
+  const int status[2] = {0, h.nnodes};
+  HIP_TRY(hipMemcpyAsync(t->vpts.p, pts.data(), sizeof(float4) * (size_t)nl, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(t->nodes.p, nodes.data(), sizeof(NfNode) * nodes.size(), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(t->box.p, h.box, sizeof(h.box), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(t->status.p, status, sizeof(status), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipEventRecord(t->ready, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));   // the host vectors go out of scope
+  c->tie_tree = t;
   invalidate_align(c);
   return GICP_OK;
+}
+
+gicp_status gicp_set_tie_target(gicp_ctx* c, const float* xyz, size_t n, size_t stride, const int32_t* local_index,
+                                size_t n_local) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  if (n == 0) return gicp_set_tie_tree(c, nullptr, 0);
+  if (!xyz || !local_index) return fail(GICP_EINVAL, "null argument");
+  if (!c->tgt.cloud || (int)n_local != c->tgt.cloud->n) return fail(GICP_ESTATE, "set the local target first (n_local = its size)");
+  gicp_status s = check_local_index(local_index, n_local, n);
+  if (s) return s;
+  s = gicp_tie_builder_set(c, xyz, n, stride);
+  const void* blob = nullptr;
+  size_t nb = 0;
+  if (!s) s = gicp_tie_builder_export(c, local_index, n_local, &blob, &nb);
+  if (!s) s = gicp_set_tie_tree(c, blob, nb);
+  const gicp_status s2 = gicp_tie_builder_set(c, nullptr, 0, 0);   // the whole cloud does not stay
+  return s ? s : s2;
+}
+
+gicp_status gicp_set_tie_trees_from_root(gicp_ctx* c, int root, const void* const* blobs, const size_t* sizes) {
+  if (!c) return fail(GICP_EINVAL, "null ctx");
+  if (!c->comm) return fail(GICP_ESTATE, "no communicator (gicp_set_comm)");
+  if (root < 0 || root >= c->nranks) return fail(GICP_EINVAL, "root out of range");
+  const int R = c->nranks, me = c->rank;
+  if (me == root && (!blobs || !sizes)) return fail(GICP_EINVAL, "the root passes every rank's blob");
+  if (R == 1) return gicp_set_tie_tree(c, blobs[0], sizes[0]);   // nothing to send
+  const Rccl& r = rccl();
+  if (!r.ok || !r.broadcast || !r.send || !r.recv || !r.group_start || !r.group_end)
+    return fail(GICP_ECOMM, "RCCL point-to-point entry points missing");
+  gicp_status s = set_device(c);
+  if (s) return s;
+  s = drain_tail(c);
+  if (s) return s;
+  // every rank's blob size (one broadcast), then root -> rank point-to-point
+  DevBuf dsz;
+  HIP_TRY(dsz.ensure(sizeof(unsigned long long) * (size_t)R));
+  std::vector<unsigned long long> sz((size_t)R, 0);
+  if (me == root)
+    for (int k = 0; k < R; ++k) sz[(size_t)k] = sizes[k];
+  HIP_TRY(hipMemcpyAsync(dsz.p, sz.data(), sizeof(unsigned long long) * R, hipMemcpyHostToDevice, c->stream));
+  NCCL_TRY(r.broadcast(dsz.p, dsz.p, (size_t)R, ncclUint64, root, c->comm, c->stream));
+  HIP_TRY(hipMemcpyAsync(sz.data(), dsz.p, sizeof(unsigned long long) * R, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  DevBuf sendb, recvb;
+  std::vector<size_t> off((size_t)R + 1, 0);
+  for (int k = 0; k < R; ++k) off[(size_t)k + 1] = off[(size_t)k] + (k == root ? 0 : (size_t)sz[(size_t)k]);
+  if (me == root && off[(size_t)R] > 0) {
+    HIP_TRY(sendb.ensure(off[(size_t)R]));
+    for (int k = 0; k < R; ++k)
+      if (k != root && sz[(size_t)k])
+        HIP_TRY(hipMemcpyAsync(sendb.as<char>() + off[(size_t)k], blobs[k], sz[(size_t)k], hipMemcpyHostToDevice, c->stream));
+  }
+  if (me != root && sz[(size_t)me]) HIP_TRY(recvb.ensure(sz[(size_t)me]));
+  NCCL_TRY(r.group_start());
+  if (me == root) {
+    for (int k = 0; k < R; ++k)
+      if (k != root && sz[(size_t)k]) NCCL_TRY(r.send(sendb.as<char>() + off[(size_t)k], sz[(size_t)k], ncclUint8, k, c->comm, c->stream));
+  } else if (sz[(size_t)me]) {
+    NCCL_TRY(r.recv(recvb.p, sz[(size_t)me], ncclUint8, root, c->comm, c->stream));
+  }
+  NCCL_TRY(r.group_end());
+  std::vector<unsigned char> mine;
+  if (me != root && sz[(size_t)me]) {
+    mine.resize(sz[(size_t)me]);
+    HIP_TRY(hipMemcpyAsync(mine.data(), recvb.p, mine.size(), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (me == root) return gicp_set_tie_tree(c, blobs[root], sizes[root]);
+  return gicp_set_tie_tree(c, mine.data(), mine.size());
 }
 
 gicp_status gicp_set_shard_groups(gicp_ctx* c, int nparts, int part) {
@@ -1761,7 +2088,7 @@ gicp_status gicp_s2s_batch(int device, const gicp_params* p, const float* const*
     gicp_status s = gicp_ctx_create(device, &ctxs[w]);
     if (!s) s = gicp_set_params(ctxs[w], p);
     if (!s) {
-      const char* os = std::getenv("DDLO_NF_OWN_STREAM");   // 0: the second stream (A/B)
+      const char* os = dev_getenv("DDLO_NF_OWN_STREAM");   // 0: the second stream (A/B)
       ctxs[w]->nf_same_stream = !(os && *os == '0');
     }
     if (s) {

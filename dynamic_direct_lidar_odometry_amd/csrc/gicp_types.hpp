@@ -238,9 +238,8 @@ struct AlignJob {
                                  // flags at the merges + the mirrored key + the winner's slice check, 4 as 3 with
                                  // the key atomic's return instead of the mirrored key, 0 none (A/B)
   const int* tgt_nf_status;      // the tree build's error bits (device int; 0 = usable)
-  NfTreeDev tgt_nf;              // nodes == nullptr: no tree (yet)
-  const int* tie_map;            // tgt_nf is a whole cloud the target was cut from (slab shard): its original
-                                 // index -> the target's sorted position (-1: not in it); nullptr: tgt.inv_perm
+  NfTreeDev tgt_nf;              // nodes == nullptr: no tree (yet); a slab shard's: its restriction of the
+                                 // whole submap's tree (tietree.hip), point ids = the local target's
   // Candidate-cell lookup (k_cell_lookup, before the walk): grid_on = 1 when
   // the target has candidate cells built for this bound.  The lookup answers
   // every query whose cell has a list; the 16-query sub-groups left with an

@@ -28,6 +28,7 @@
 #include "nftree.hpp"
 #include "cov_math.hpp"
 #include "launch.hpp"
+#include "devknobs.hpp"
 
 #include <algorithm>
 
@@ -1976,7 +1977,7 @@ __device__ __forceinline__ void resolve_tied_corr(const AlignJob* __restrict__ j
     rix = __builtin_amdgcn_readfirstlane(rix);
     if (!ok) err = 1;
     else if (__float_as_uint(rd) != __float_as_uint(dl) || rix < 0 || rix >= t.n) err = 16;
-    else if ((jn = job->tie_map ? job->tie_map[rix] : tgt.inv_perm[rix]) < 0) err = 32;   // outside the slab + halo
+    else if ((jn = tgt.inv_perm[rix]) < 0) err = 32;
     if (lane == l) {
       if (jn >= 0) j = jn;
       else atomicOr(&st->tie_err, err);
@@ -3002,7 +3003,7 @@ void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int
   k_level_boxes<<<cdiv(nparent, 4), 256, 0, s>>>(clo, chi, nchild, nparent, plo, phi);
 }
 static int env_knob(const char* name, int dflt) {   // development knobs (A/B of launch shapes)
-  const char* v = std::getenv(name);
+  const char* v = dev_getenv(name);
   return v && *v ? std::atoi(v) : dflt;
 }
 bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo,
@@ -3050,21 +3051,6 @@ void launch_cov_remap(hipStream_t s, const double* old_cov6, const int* old_inv_
                       double* cov6) {
   k_cov_remap<<<cdiv(n, 256), 256, 0, s>>>(old_cov6, old_inv_perm, new_perm, n, cov6);
 }
-// slab shard tie order: whole-target original index -> local sorted position
-__global__ __launch_bounds__(256) void k_tie_map_clear(int n_full, int* __restrict__ map) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_full) map[i] = -1;
-}
-__global__ __launch_bounds__(256) void k_tie_map_scatter(const int* __restrict__ local_index,
-                                                         const int* __restrict__ inv_perm, int n_local,
-                                                         int* __restrict__ map) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_local) map[local_index[i]] = inv_perm[i];
-}
-void launch_tie_map(hipStream_t s, const int* local_index, const int* inv_perm, int n_local, int n_full, int* map) {
-  k_tie_map_clear<<<cdiv(n_full, 256), 256, 0, s>>>(n_full, map);
-  k_tie_map_scatter<<<cdiv(n_local, 256), 256, 0, s>>>(local_index, inv_perm, n_local, map);
-}
 void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src) {
   k_align_init<<<1, 128, 0, s>>>(job, job_src);
 }
@@ -3075,7 +3061,7 @@ size_t collect_lds_bytes(int upper_count) {
 static int scan_blocks(int nsrc) {
   const int groups = (nsrc + kTaskQ - 1) / kTaskQ;
   static const int cap = [] {   // development knob
-    const char* v = std::getenv("DDLO_SCAN_WAVES");
+    const char* v = dev_getenv("DDLO_SCAN_WAVES");
     return v && *v ? std::max(kTaskRegions, std::atoi(v)) : 8192;
   }();
   int waves = std::min(std::max(groups, kTaskRegions), cap);

@@ -43,7 +43,10 @@ bool launch_knn_query(hipStream_t s, const CloudDev& c, const float4* q, int nq,
                       TieList ties = TieList{nullptr, nullptr});
 void launch_cov_import(hipStream_t s, const double* in, int layout, int n, const int* inv_perm, double* cov6);
 void launch_cov_export(hipStream_t s, const double* cov6, int layout, int n, const int* perm, double* out);
-void launch_tie_map(hipStream_t s, const int* local_index, const int* inv_perm, int n_local, int n_full, int* map);
+// tietree.hip: a slab shard's restriction of the whole submap's nanoflann tree
+size_t tie_prune_scratch_bytes(int n, int cap);
+hipError_t launch_tie_prune(hipStream_t s, const NfTreeDev& t, int cap, const int* local_index, int n_local,
+                            void* scratch, NfNode* out_nodes, float4* out_pts, unsigned* counts);
 void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src);
 // tgt_upper: number of upper-level (>= 1) boxes of the target (LDS cache size)
 // Launch geometry of one linearize (grids, upper-box LDS cache), bucketed by

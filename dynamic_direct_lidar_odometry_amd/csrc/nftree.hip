@@ -30,6 +30,7 @@
 #include "gicp_types.hpp"
 #include "launch.hpp"
 #include "nftree.hpp"
+#include "devknobs.hpp"
 
 namespace ddlo {
 
@@ -2170,7 +2171,7 @@ bool launch_nf_lazy(hipStream_t s, const NfTreeDev& t, const CloudDev& c, const 
                     int method, double* cov6, int* out_idx, float* out_d, void* scratch, int wgs, const int* status,
                     int* err) {
   if (k > 64 || wgs < 1 || !t.partial) return false;
-  static const int prof = std::getenv("DDLO_LAZY_PROF") != nullptr;   // development: per-phase cycles (printf)
+  static const int prof = dev_getenv("DDLO_LAZY_PROF") != nullptr;   // development: per-phase cycles (printf)
   char* wg = static_cast<char*>(scratch);
   if (cov6)
     k_nf_lazy<true><<<wgs, kLzT, 0, s>>>(t, c, q, ties, k, method, cov6, out_idx, out_d, wg, lz_wg_bytes(c.n), status,

@@ -45,6 +45,7 @@
 #include "gicp_types.hpp"
 #include "launch.hpp"
 #include "runtime.hpp"
+#include "devknobs.hpp"
 
 namespace {
 
@@ -706,7 +707,7 @@ gicp_status ddlo_odom_create(int device, const ddlo_odom_params* p, ddlo_odom** 
     return st;
   }
   o->s = o->s2s->stream;  // one stream: the driver's work is one dependent chain
-  o->timing = std::getenv("DDLO_ODOM_TIMING") != nullptr;
+  o->timing = dev_getenv("DDLO_ODOM_TIMING") != nullptr;
   if (hipHostMalloc((void**)&o->median_pin, sizeof(float), hipHostMallocDefault) != hipSuccess) {
     gicp_ctx_destroy(o->s2s);
     gicp_ctx_destroy(o->s2m);

@@ -22,6 +22,7 @@
 #include "../../include/ddlo_gicp.h"
 #include "gicp_types.hpp"
 #include "launch.hpp"
+#include "devknobs.hpp"
 
 #define HIP_TRY(expr)                                                                       \
   do {                                                                                      \
@@ -404,8 +405,9 @@ struct gicp_ctx {
   // splits only the nodes it walks; a cloud with many ties gets the whole
   // tree instead (lazy_heavy: the previous pass listed more than 2 x the
   // lazy kernel's workgroups)
-  bool tie_lazy = true;    // DDLO_TIE_LAZY=0: the whole tree for covariance ties too
-  int partial_levels = 3;  // big levels of the partial tree the lazy search starts from (DDLO_TIE_PARTIAL_LEVELS)
+  bool tie_lazy = true;    // GICP_OPT_TIE_LAZY 0: the whole tree for covariance ties too
+  int partial_levels = 3;  // big levels of the partial tree the lazy search starts from (GICP_OPT_TIE_PARTIAL_LEVELS)
+  bool cov_tasks = false;  // GICP_OPT_COV_TASKS: the task-based kNN for covariances
   bool lazy_heavy = false;
   // nanoflann's tree on the ctx's own stream, not beside it (gicp_s2s_batch's
   // workers: the other workers fill the device, and a second stream per
@@ -423,10 +425,14 @@ struct gicp_ctx {
   bool nf_err_pending = false;
   long ties_resolved = 0;       // diagnostics
   std::weak_ptr<NfTreeData> nf_joined;   // the target tree c->stream last waited for
-  // slab shard: the whole target the slab was cut from (its nanoflann tree
-  // orders the ties) and its original index -> local sorted position
-  std::shared_ptr<CloudData> tie_ref;
-  DevBuf tie_map;
+  // slab shard: its restriction of the whole submap's nanoflann tree
+  // (tietree.hip; gicp_set_tie_tree), which orders the in-align ties
+  std::shared_ptr<NfTreeData> tie_tree;
+  // tie builder (gicp_tie_builder_set): the whole submap, its tree, and the
+  // buffers of the restrictions exported from it
+  std::shared_ptr<CloudData> tie_whole;
+  DevBuf tie_scratch, tie_lidx, tie_out_nodes, tie_out_pts, tie_counts;
+  std::vector<unsigned char> tie_blob;   // the last exported restriction (gicp_tie_builder_export)
   // candidate cells of the target (gicp_set_target_grid): 0 off, 1 auto, 2 on
   int grid_mode = GICP_GRID_AUTO;
   DevBuf fb;                      // the lookup's walk list: [counters][list segments][masks]
@@ -572,11 +578,12 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
 // off (optional, 16 entries) receives the sizes and the scratch offsets.
 // partial_levels >= 0: only that many big levels, then stubs (k_nf_stub).
 inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, NfTreeData& tr, int stop = -1,
-                                long long* off = nullptr, int partial_levels = -1, const int* gate = nullptr) {
+                                long long* off = nullptr, int partial_levels = -1, const int* gate = nullptr,
+                                bool zero_nodes = false) {
   NfTreeData* t = &tr;
   const int n = cd.n;
   // the cloud is ready on s_in; the build runs on the aux stream
-  static const bool same_env = std::getenv("DDLO_NF_SAME_STREAM") != nullptr;   // A/B, diagnostics
+  static const bool same_env = dev_getenv("DDLO_NF_SAME_STREAM") != nullptr;   // A/B, diagnostics
   const bool same_stream = same_env || c->nf_same_stream;
   const hipStream_t s = same_stream ? s_in : c->aux_stream;
   if (!same_stream) {
@@ -616,6 +623,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   t->cap = z.big_ids + 2 * n;   // big-level ids, then 2 per point for the small subtrees' ranges
   HIP_TRY(t->vpts.ensure(sizeof(float4) * (size_t)n));
   HIP_TRY(t->nodes.ensure(sizeof(NfNode) * (size_t)t->cap));
+  if (zero_nodes) HIP_TRY(hipMemsetAsync(t->nodes.p, 0, t->nodes.bytes, s));   // unwritten slots read as non-nodes (tietree.hip)
   HIP_TRY(t->box.ensure(2 * sizeof(float4)));   // root_bbox
   HIP_TRY(t->status.ensure(2 * sizeof(int)));
   t->partial = partial;
@@ -671,7 +679,7 @@ inline gicp_status nftree_build(gicp_ctx* c, CloudData& cd, hipStream_t s_in, Nf
   HIP_TRY(c->nf_desc.ensure(sizeof(NfBuild)));
   NfBuild* db = c->nf_desc.as<NfBuild>();
   launch_nf_set_desc(s, b, db);   // by value as a kernel argument: no host buffer has to outlive the call
-  static const bool no_graph = std::getenv("DDLO_NF_NO_GRAPH") != nullptr;   // A/B, diagnostics
+  static const bool no_graph = dev_getenv("DDLO_NF_NO_GRAPH") != nullptr;   // A/B, diagnostics
   if (stop >= 0 || no_graph || same_env) {
     launch_nf_build(s, b, db, stop);
     HIP_TRY(hipGetLastError());
@@ -820,10 +828,9 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     ~InCov() { c->st_in_cov = false; }
   } in_cov{c};
   c->st_in_cov = c->profiling;
-  // DDLO_COV_TASKS=1: the task-based kNN (knn_tasks.hip) — exact, but not
+  // GICP_OPT_COV_TASKS: the task-based kNN (knn_tasks.hip) — exact, but not
   // faster than the lane-per-query kernel on the cfg 5 clouds
-  const char* tv = std::getenv("DDLO_COV_TASKS");
-  const bool tasks = tv && *tv == '1';
+  const bool tasks = c->cov_tasks;
   const CloudDev cd = side.cloud->dev();
   // exact ties: the points whose k-th neighbour distance is tied get their
   // neighbourhood from nanoflann's own search (nftree.hip)
@@ -892,7 +899,7 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     if (!launch_knn_covariances(c->stream, j, side.cloud->upper_count()))
       return fail(GICP_EINVAL, "unsupported k");
     launch_covariances(c->stream, cd, k, c->params.regularization, cv->cov6.as<double>(), j.redo, tl);
-    if (std::getenv("DDLO_COV_DEBUG")) {   // development: how many groups needed the fallback
+    if (dev_getenv("DDLO_COV_DEBUG")) {   // development: how many groups needed the fallback
       std::vector<unsigned char> r((n + 63) / 64);
       std::vector<unsigned> cn(n);
       HIP_TRY(hipMemcpyAsync(r.data(), j.redo, r.size(), hipMemcpyDeviceToHost, c->stream));
@@ -943,13 +950,13 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
     }
     gicp_status st = publish_ties(c, c->stream);
     if (st) return st;
-    static const bool dbg = std::getenv("DDLO_TIE_DEBUG") != nullptr;   // development: tied queries per cloud
+    static const bool dbg = dev_getenv("DDLO_TIE_DEBUG") != nullptr;   // development: tied queries per cloud
     if (dbg) {
       int cnt = 0;
       HIP_TRY(hipMemcpyAsync(&cnt, tl.count, sizeof(int), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
       std::fprintf(stderr, "[ties] n %d k %d tied %d\n", side.cloud->n, k, cnt);
-      if (const char* path = std::getenv("DDLO_TIE_DUMP")) {   // the tied queries' original indices, one line per cloud
+      if (const char* path = dev_getenv("DDLO_TIE_DUMP")) {   // the tied queries' original indices, one line per cloud
         const int m = std::min(cnt, tl.cap);
         std::vector<int> pos(m), perm(side.cloud->n);
         HIP_TRY(hipMemcpyAsync(pos.data(), tl.list, sizeof(int) * m, hipMemcpyDeviceToHost, c->stream));

@@ -376,6 +376,8 @@ def _raycast_lib():
                         "libddlo_raycast.so")
     if not os.path.exists(path):
         return None
+    from . import load
+    load()   # torch's HIP runtime first (see load())
     L = C.CDLL(path)
     P = C.c_void_p
     L.ddlo_raycast.restype = C.c_int

@@ -153,18 +153,35 @@ class ShardedGicp:
         else:
             slabs = plan_slabs(points, self.nranks, axis)
         self.slab = slabs[self.rank]
-        idx = halo_indices(points, self.slab, self.params.max_correspondence_distance)
-        if len(idx) == 0:  # an empty rank still needs a valid cloud; it owns no queries
-            idx = np.zeros(1, np.int64)
-        self.local_index = idx
         whole = np.ascontiguousarray(np.asarray(points, np.float32)[:, :3])
+        idx = self._slab_index(whole, self.slab)
+        self.local_index = idx
         self.ctx.set_target(np.ascontiguousarray(whole[idx]))
         self.ctx.set_covariances(TARGET, np.ascontiguousarray(covs[idx]))
-        # exact ties in the whole submap's nanoflann order (its tree, built once per submap)
-        self.ctx.set_tie_target(whole, idx)
+        # exact ties in the whole submap's nanoflann order: each rank holds that
+        # tree restricted to its slab + halo, built and cut once per submap on
+        # rank 0 and sent to its rank (tietree.hip); nothing with Morton ties
+        if self.ctx.tie_order():
+            if self.nranks == 1:
+                self.ctx.set_tie_target(whole, idx)
+            else:
+                blobs = None
+                if self.rank == 0:
+                    self.ctx.tie_builder_set(whole)
+                    try:
+                        blobs = [self.ctx.tie_builder_export(self._slab_index(whole, s)) for s in slabs]
+                    finally:
+                        self.ctx.tie_builder_set(None)
+                self.ctx.set_tie_trees_from_root(0, blobs)
         self.ctx.set_shard_groups(0, 0)
         self.ctx.set_shard(self.slab.axis, self.slab.lo, self.slab.hi)
         return self.slab
+
+    def _slab_index(self, whole: np.ndarray, slab: Slab) -> np.ndarray:
+        idx = halo_indices(whole, slab, self.params.max_correspondence_distance)
+        if len(idx) == 0:  # an empty rank still needs a valid cloud; it owns no queries
+            idx = np.zeros(1, np.int64)
+        return idx
 
     def set_source(self, points: np.ndarray, covs: np.ndarray | None = None):
         from . import SOURCE

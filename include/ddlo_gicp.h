@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DDLO_GICP_ABI_VERSION 3
+#define DDLO_GICP_ABI_VERSION 4
 
 typedef enum gicp_status {
   GICP_OK = 0,
@@ -212,6 +212,24 @@ gicp_status gicp_knn_target(struct gicp_ctx* ctx, const float* q, size_t nq, siz
  * is built).  Distances are identical either way.  Applies to covariances
  * and gicp_knn_target. */
 gicp_status gicp_set_tie_order(struct gicp_ctx* ctx, int nanoflann_order);
+gicp_status gicp_get_tie_order(const struct gicp_ctx* ctx, int* nanoflann_order);
+
+/* Options of a context.  gicp_set_default_option sets the value contexts
+ * created afterwards start with (process-wide; also the contexts the
+ * odometry driver and gicp_s2s_batch create inside).  Results are identical
+ * under every value; only the work differs. */
+enum gicp_option {
+  GICP_OPT_TIE_ORDER = 1,           /* 1 (default): nanoflann's tie order; 0: Morton (= gicp_set_tie_order) */
+  GICP_OPT_TIE_LAZY = 2,            /* 1 (default): covariance ties searched on the partial tree, splitting
+                                       lazily; 0: on the whole tree */
+  GICP_OPT_TIE_PARTIAL_LEVELS = 3,  /* big levels of that partial tree (0..24, default 3) */
+  GICP_OPT_COV_TASKS = 4,           /* 1: the task-based k-NN for covariances (default 0: a lane per query) */
+  GICP_OPT_COUNT = 5
+};
+gicp_status gicp_set_option(struct gicp_ctx* ctx, int option, int value);
+gicp_status gicp_get_option(const struct gicp_ctx* ctx, int option, int* value);
+gicp_status gicp_set_default_option(int option, int value);
+gicp_status gicp_get_default_option(int option, int* value);
 
 /* Candidate cells of the target (DESIGN.md §4 "Candidate cells"): a
  * per-target structure built once per (target cloud, max correspondence
@@ -300,19 +318,43 @@ gicp_status gicp_get_stream(const struct gicp_ctx* ctx, void** stream);
  * max_corr of an owned query lies in the slab + halo. */
 /* Ownership slab of this ctx; axis -1 removes it. */
 gicp_status gicp_set_shard(struct gicp_ctx* ctx, int axis, float lo, float hi);
-/* Exact ties for a slab shard: a slab's target is a subset of the submap, and
- * nanoflann orders equidistant points by ITS tree, which differs from the
- * whole submap's (nanoflann_impl.hpp:1045-1143 cut the subset's boxes).
- * Give the ctx the whole target it was cut from and, for every local target
- * point i (the cloud of the last gicp_set_target), its index local_index[i]
- * in that whole cloud: tied correspondences are then re-run through the WHOLE
- * target's nanoflann tree, as the unsharded reference resolves them.  The
- * tree is built here, once per submap; gicp_set_target, gicp_clear_target
- * and gicp_swap_source_target drop it.  local_index must be one-to-one and map
- * every local point onto an identical point of the whole cloud (checked:
- * GICP_EINVAL otherwise).  n = 0 removes it. */
+/* Exact ties for a slab shard (DESIGN.md §5 "Slab shards"): a slab's target
+ * is a subset of the submap, and nanoflann orders equidistant points by ITS
+ * tree, which differs from the whole submap's (nanoflann_impl.hpp:1045-1143
+ * cut the subset's boxes).  A slab rank resolves its tied correspondences
+ * through the whole submap's tree RESTRICTED to its own points (every point
+ * outside the slab + halo removed, emptied subtrees as empty leaves): for a
+ * matched owned query every equidistant point lies in the halo and the walk
+ * meets them in the whole tree's order.  The restriction is O(slab + halo);
+ * the rank never holds the whole submap.  gicp_set_target,
+ * gicp_clear_target and gicp_swap_source_target drop it.
+ *
+ * Builder (one rank, e.g. rank 0, once per submap): gicp_tie_builder_set
+ * uploads the whole submap and builds its nanoflann tree (n = 0 frees them);
+ * gicp_tie_builder_export returns the restriction to one rank's points
+ * (local_index[i] = the whole-cloud index of that rank's local target point
+ * i; one-to-one) as a blob owned by the ctx, valid until its next builder
+ * call.  Rank: gicp_set_tie_tree installs a blob (bytes = 0 removes it); it
+ * is checked against the local target (same size, a tree whose leaves
+ * partition the points, each point the local target's point of that index:
+ * GICP_EINVAL otherwise).  gicp_set_tie_trees_from_root does the transport
+ * over the ctx's communicator (collective: the root passes every rank's
+ * blob, the others NULL; one broadcast of the sizes, then root -> rank
+ * point-to-point).  gicp_set_tie_target = builder + export + install on one
+ * ctx, the whole cloud released before it returns (single-process use). */
+gicp_status gicp_tie_builder_set(struct gicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
+gicp_status gicp_tie_builder_export(struct gicp_ctx* ctx, const int32_t* local_index, size_t n_local,
+                                    const void** blob, size_t* bytes);
+gicp_status gicp_set_tie_tree(struct gicp_ctx* ctx, const void* blob, size_t bytes);
+gicp_status gicp_set_tie_trees_from_root(struct gicp_ctx* ctx, int root, const void* const* blobs,
+                                         const size_t* sizes);
 gicp_status gicp_set_tie_target(struct gicp_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes,
                                 const int32_t* local_index, size_t n_local);
+/* Device bytes the ctx holds (pool size classes): out[0] total, [1] target
+ * cloud (points, index, trees, candidate cells), [2] source cloud (0 when
+ * shared with the target), [3] covariances, [4] slab tie tree, [5] tie
+ * builder, [6] scratch.  nout entries are written (up to 7). */
+gicp_status gicp_get_device_bytes(const struct gicp_ctx* ctx, int64_t* out, int nout);
 /* Interleaved sharding, for a target that fits every GPU (it is replicated):
  * rank `part` of `nparts` owns the source points whose 16-point group in the
  * device's spatial (Morton) order is congruent to part mod nparts, so every

@@ -98,6 +98,21 @@ def test_default_params_are_the_reference_defaults():
     assert P.load().gicp_abi_version() >= 1
 
 
+def test_default_options():
+    """Process-wide option defaults (gicp_set_default_option): the documented values, settable and
+    restorable, out-of-range values and unknown options rejected (no device needed)."""
+    assert P.get_default_option(P.OPT_TIE_ORDER) == 1
+    assert P.get_default_option(P.OPT_TIE_LAZY) == 1
+    assert P.get_default_option(P.OPT_TIE_PARTIAL_LEVELS) == 3
+    assert P.get_default_option(P.OPT_COV_TASKS) == 0
+    with P.default_option(P.OPT_TIE_ORDER, 0):
+        assert P.get_default_option(P.OPT_TIE_ORDER) == 0
+    assert P.get_default_option(P.OPT_TIE_ORDER) == 1
+    for opt, val in ((0, 1), (5, 1), (P.OPT_TIE_ORDER, 2), (P.OPT_TIE_PARTIAL_LEVELS, -1), (P.OPT_TIE_PARTIAL_LEVELS, 25)):
+        with pytest.raises(P.GicpError):
+            P.set_default_option(opt, val)
+
+
 def _gpu_present():
     n = C.c_void_p()
     rc = P.load().gicp_ctx_create(0, C.byref(n))

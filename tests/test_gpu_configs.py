@@ -83,18 +83,24 @@ def test_cfg4_group_shards_add_up(cfg4, world):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_cfg4_slab_shards_add_up(cfg4, world):
     """Slab mode at cfg 4 size (the spatial tiling of north_star / SURVEY.md §8(e)): N contexts on one device,
-    each with its slab + 2 m halo of the 2M-point submap (slabs cut on the source at the guess) and the
-    whole submap as its tie order (gicp_set_tie_target).  Moments add up (rel 1e-10), matched counts add
-    up, every owned correspondence equals the unsharded one exactly (ties included).  Prints the per-rank
-    linearize time (ranks run one after another here) for DESIGN.md's critical-path table."""
+    each with its slab + 2 m halo of the 2M-point submap (slabs cut on the source at the guess) and, as its
+    tie order, the whole submap's nanoflann tree restricted to its points (one builder ctx exports every
+    rank's restriction; a rank never holds the whole submap).  Moments add up (rel 1e-10), matched counts
+    add up, every owned correspondence equals the unsharded one exactly (ties included), and a rank's tie
+    tree is O(its points).  Prints the per-rank linearize time (ranks run one after another here) and
+    device bytes for DESIGN.md's slab table."""
     from dynamic_direct_lidar_odometry_amd.shard import halo_indices, owner_of, plan_slabs_by_source, transform_f32
     pose = cfg4["guess"].astype(np.float64)
     full = _ctx(cfg4)
     _, _, _, nc = full.linearize(pose)
     mom = full.moments()
     fcorr, fsqd = full.correspondences()
+    full_bytes = full.device_bytes()
     full.close()
     slabs = plan_slabs_by_source(cfg4["src"], pose, world)
+    builder = P.Context(0)
+    builder.tie_builder_set(cfg4["sub"])
+    builder_bytes = builder.device_bytes()["tie_builder"]
     own = owner_of(transform_f32(cfg4["src"], pose), slabs)
     tot = np.zeros(80)
     ntot = 0
@@ -108,7 +114,9 @@ def test_cfg4_slab_shards_add_up(cfg4, world):
         c.set_source(cfg4["src"])
         c.set_covariances(SOURCE, cfg4["scov"])
         c.set_shard(sl.axis, sl.lo, sl.hi)
-        c.set_tie_target(cfg4["sub"], idx)
+        c.set_tie_tree(builder.tie_builder_export(idx))
+        db = c.device_bytes()
+        assert db["tie_builder"] == 0 and db["tie_tree"] <= 40 * len(idx) + (1 << 20)
         _, _, _, n_r = c.linearize(pose)
         tot += c.moments()
         ntot += n_r
@@ -120,12 +128,18 @@ def test_cfg4_slab_shards_add_up(cfg4, world):
         c.set_profiling(True)
         _, res = c.align(cfg4["guess"])
         c.set_profiling(False)
-        rows.append((r, int(mine.sum()), len(idx), res.linearize_ms / max(res.iterations_run, 1) * 1e3))
+        rows.append((r, int(mine.sum()), len(idx), res.linearize_ms / max(res.iterations_run, 1) * 1e3, db))
         c.close()
+    builder.close()
     assert ntot == nc
     np.testing.assert_allclose(tot[:74], mom[:74], rtol=1e-10, atol=1e-10 * np.abs(mom[:74]).max())
-    for r, nq, nt, us in rows:
-        print(f"slab world {world} rank {r}: owned queries {nq}, target points {nt}, linearize {us:.1f} us")
+    mb = 1.0 / (1 << 20)
+    print(f"slab world {world}: unsharded ctx {full_bytes['total'] * mb:.1f} MiB (target {full_bytes['target'] * mb:.1f}), "
+          f"rank-0 builder transient {builder_bytes * mb:.1f} MiB")
+    for r, nq, nt, us, db in rows:
+        print(f"slab world {world} rank {r}: owned queries {nq}, target points {nt}, linearize {us:.1f} us, "
+              f"device {db['total'] * mb:.1f} MiB (target {db['target'] * mb:.1f}, tie tree {db['tie_tree'] * mb:.2f}, "
+              f"scratch {db['scratch'] * mb:.1f})")
 
 
 def test_cfg4_comm1_pose_vs_oracle(cfg4):

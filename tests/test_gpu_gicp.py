@@ -72,7 +72,7 @@ def test_covariances_ragged_sizes_vs_oracle(n, k):
 
 @pytest.mark.parametrize("k", [10, 20, 7, 32])
 def test_covariances_task_knn_matches(s2s_golden, k, monkeypatch):
-    """The opt-in task-based kNN (knn_tasks.hip, DDLO_COV_TASKS=1) and the
+    """The opt-in task-based kNN (knn_tasks.hip, OPT_COV_TASKS) and the
     lane-per-query kernel both give the reference's covariances, on the
     ray-cast scan (dense near range, sparse far range: exercises the second
     round) and on a sparse random cloud with exact ties and duplicates
@@ -85,8 +85,8 @@ def test_covariances_task_knn_matches(s2s_golden, k, monkeypatch):
         ref = O.covariances(cloud, k)
         scale = max(np.abs(ref).max(), 1.0)
         for flag in ("0", "1"):
-            monkeypatch.setenv("DDLO_COV_TASKS", flag)
             c = P.Context(0)
+            c.set_option(P.OPT_COV_TASKS, int(flag))
             c.set_params(P.default_params(k_correspondences=k))
             c.set_target(cloud)
             c.compute_covariances(TARGET)

@@ -1,7 +1,8 @@
 """The sharded S2M linearize across PROCESSES: each of two
 spawned processes opens a Context on device 0, takes its share of the source
 (interleaved 16-point groups, or a spatial slab of the source with the
-target's slab + halo and the whole submap's tie order), runs the library's
+target's slab + halo and its restriction of the whole submap's nanoflann
+tree, cut by rank 0 and sent over gloo), runs the library's
 linearize and all-reduces the library's 80 moments over gloo -- the one
 collective a sharded iteration makes (nano_gicp_impl.hpp:284-339 sums
 per-thread partials; here per rank).  The sums equal the unsharded
@@ -60,7 +61,17 @@ def _worker(rank, world, port, mode, grid, q):
             c.set_source(np.ascontiguousarray(g["src"]))
             c.set_covariances(SOURCE, np.ascontiguousarray(g["cov_src"]))
             c.set_shard(s.axis, s.lo, s.hi)
-            c.set_tie_target(np.ascontiguousarray(g["sub"]), idx)
+            # the whole submap's tie order: rank 0 builds it and cuts every rank's restriction, the blobs
+            # travel over gloo (ShardedGicp sends them over its RCCL communicator instead)
+            objs = [None]
+            if rank == 0:
+                c.tie_builder_set(np.ascontiguousarray(g["sub"]))
+                objs = [[c.tie_builder_export(halo_indices(g["sub"], sl, S2M["max_correspondence_distance"]))
+                         for sl in slabs]]
+                c.tie_builder_set(None)
+            dist.broadcast_object_list(objs, src=0)
+            c.set_tie_tree(objs[0][rank])
+            assert c.device_bytes()["tie_builder"] == 0
         c.linearize(pose)
         m = torch.from_numpy(c.moments().copy())
         own = torch.tensor([float(c.moments()[73])], dtype=torch.float64)

@@ -59,8 +59,8 @@ def test_covariance_ties_lattice(k, spacing, lazy, monkeypatch):
     lat = np.stack(np.meshgrid(np.arange(24), np.arange(24), np.arange(5), indexing="ij"), -1).reshape(-1, 3)
     pts = (lat.astype(np.float32) * np.float32(spacing))
     pts = pts + (np.arange(len(pts)) % 7 == 0)[:, None].astype(np.float32) * np.float32(0.04 * spacing)   # some irregularity
-    monkeypatch.setenv("DDLO_TIE_LAZY", lazy)   # the lazy search on the partial tree, or the whole tree
     c = P.Context(0)
+    c.set_option(P.OPT_TIE_LAZY, int(lazy))   # the lazy search on the partial tree, or the whole tree
     c.set_params(P.default_params(k_correspondences=k))
     c.set_target(pts)
     c.compute_covariances(TARGET)
@@ -76,7 +76,7 @@ def test_covariance_ties_lattice(k, spacing, lazy, monkeypatch):
 @pytest.mark.parametrize("levels", ["0", "3", "6"])
 @pytest.mark.parametrize("name", ["scan", "scan_duplicates", "lattice_sparse"])
 def test_lazy_tie_search_matches_oracle(name, levels, monkeypatch):
-    """Covariance ties resolved on a partial tree (DDLO_TIE_LAZY=1: the top
+    """Covariance ties resolved on a partial tree (OPT_TIE_LAZY 1: the top
     `levels` big levels built, every tied query's nanoflann search splitting
     the stubs below lazily) equal the oracle's covariances at every point; a
     second pass on the same ctx after a tie-heavy first one takes the whole
@@ -89,9 +89,9 @@ def test_lazy_tie_search_matches_oracle(name, levels, monkeypatch):
     else:
         lat = np.stack(np.meshgrid(np.arange(40), np.arange(40), np.arange(3), indexing="ij"), -1).reshape(-1, 3)
         pts = lat.astype(np.float32) * np.float32(0.5)
-    monkeypatch.setenv("DDLO_TIE_LAZY", "1")   # read at context creation
-    monkeypatch.setenv("DDLO_TIE_PARTIAL_LEVELS", levels)   # read once per process: the first value sticks
     c = P.Context(0)
+    c.set_option(P.OPT_TIE_LAZY, 1)
+    c.set_option(P.OPT_TIE_PARTIAL_LEVELS, int(levels))
     c.set_params(P.default_params(k_correspondences=10))
     ref = O.covariances(pts, 10)
     scale = max(np.abs(ref).max(), 1.0)

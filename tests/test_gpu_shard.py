@@ -193,6 +193,84 @@ def test_slab_shards_tied_target(knn_golden, world):
     assert seen.all()
 
 
+def test_slab_tie_tree_blobs(knn_golden):
+    """The builder / rank split of the slab tie order: one ctx holds the whole lattice and exports each
+    rank's restriction; the rank ctxs (which never see the whole cloud) install the blobs and resolve
+    every tie as the reference's nanoflann does.  A rank's blob holds its own points only; damaged or
+    foreign blobs are rejected."""
+    tgt = np.ascontiguousarray(knn_golden["lat_pts"])
+    src = np.ascontiguousarray(knn_golden["lat_q"])
+    par = dict(S2M, k_correspondences=10)
+    ref = knn_golden["lat_k1_idx"][:, 0]
+    world = 3
+    slabs = plan_slabs(tgt, world)
+    own = owner_of(NP.transform_f32(np.eye(4), src), slabs)
+    builder = P.Context(0)
+    with pytest.raises(P.GicpError):
+        builder.tie_builder_export(np.arange(4))   # no whole cloud yet
+    builder.tie_builder_set(tgt)
+    assert builder.device_bytes()["tie_builder"] > 0
+    seen = np.zeros(len(src), bool)
+    for r, s in enumerate(slabs):
+        idx = halo_indices(tgt, s, par["max_correspondence_distance"])
+        blob = builder.tie_builder_export(idx)
+        c = P.Context(0)
+        c.set_params(P.default_params(**par))
+        c.set_target(np.ascontiguousarray(tgt[idx]))
+        c.compute_covariances(TARGET)
+        with pytest.raises(P.GicpError):
+            c.set_tie_tree(blob[:-16])                         # truncated
+        bad = bytearray(blob)
+        bad[-16:-4] = np.float32([9e9, 9e9, 9e9]).tobytes()    # a point that is not the local target's
+        with pytest.raises(P.GicpError):
+            c.set_tie_tree(bytes(bad))
+        if r > 0:
+            with pytest.raises(P.GicpError):
+                c.set_tie_tree(builder.tie_builder_export(halo_indices(tgt, slabs[0], 2.0)))   # another rank's
+        c.set_tie_tree(blob)
+        db = c.device_bytes()
+        assert db["tie_tree"] > 0 and db["tie_builder"] == 0
+        c.set_source(src)
+        c.compute_covariances(SOURCE)
+        c.set_shard(s.axis, s.lo, s.hi)
+        c.linearize(np.eye(4))
+        corr, _ = c.correspondences()
+        mine = own == r
+        gc = np.where(corr >= 0, idx[np.maximum(corr, 0)], -1)
+        np.testing.assert_array_equal(gc[mine], ref[mine])
+        seen |= mine
+        c.close()
+    builder.tie_builder_set(None)
+    assert builder.device_bytes()["tie_builder"] == 0
+    builder.close()
+    assert seen.all()
+
+
+def test_tie_trees_from_root_one_rank(knn_golden):
+    """gicp_set_tie_trees_from_root over a one-rank communicator (the root sends to nobody and installs
+    its own blob); ShardedGicp's slab mode at world 1 resolves the lattice's ties exactly."""
+    tgt = np.ascontiguousarray(knn_golden["lat_pts"])
+    src = np.ascontiguousarray(knn_golden["lat_q"])
+    c = P.Context(0)
+    c.set_params(P.default_params(**dict(S2M, k_correspondences=10)))
+    c.set_comm(P.comm_unique_id(), 1, 0)
+    c.set_target(tgt)
+    c.compute_covariances(TARGET)
+    c.tie_builder_set(tgt)
+    blob = c.tie_builder_export(np.arange(len(tgt)))
+    c.tie_builder_set(None)
+    c.set_tie_trees_from_root(0, [blob])
+    assert c.device_bytes()["tie_tree"] > 0
+    c.set_source(src)
+    c.compute_covariances(SOURCE)
+    c.set_shard(0, -np.inf, np.inf)
+    c.linearize(np.eye(4))
+    corr, _ = c.correspondences()
+    np.testing.assert_array_equal(corr, knn_golden["lat_k1_idx"][:, 0])
+    c.set_comm(None, 0, 0)
+    c.close()
+
+
 @pytest.mark.parametrize("op", ["swap", "clear"])
 def test_tie_target_dropped_with_its_target(knn_golden, op):
     """The whole-target tie order belongs to the target it was given for:
