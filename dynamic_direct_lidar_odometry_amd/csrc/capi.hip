@@ -708,7 +708,9 @@ gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks, Alig
     launch_mom_reduce(c->stream, jd);
     NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
   }
-  if (!g.fuse_lm) launch_lm_step(c->stream, jd, publish);
+  if (!g.fuse_lm)
+    launch_lm_step(c->stream, jd, c->state_dev.as<AlignState>(), c->slab.as<double>(), g.mom_blocks,
+                   c->comm ? c->mom.as<double>() : nullptr, publish);
   else if (publish) HIP_TRY(hipMemcpyAsync(publish, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
   return GICP_OK;
 }
@@ -778,7 +780,9 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   // key: whether RCCL is in the chunk, the job buffer and the launch geometry
   const LinGeom g = geometry(c);
   (void)nblocks;   // = g.mom_blocks
-  const std::array<long long, 8> key{{c->comm ? 1 : 0, (long long)(uintptr_t)jd, g.seed_blocks, g.collect_blocks,
+  // (the slab buffer: k_lm_step takes it as an argument; pool blocks are 256-B aligned, bit 0 = RCCL)
+  const std::array<long long, 8> key{{(long long)(uintptr_t)c->slab.p | (c->comm ? 1 : 0), (long long)(uintptr_t)jd,
+                                      g.seed_blocks, g.collect_blocks,
                                       g.scan_blocks, g.mom_blocks, g.lds_boxes,
                                       g.grid ? (g.grid_walk ? 2L : 1L) * g.lookup_blocks : 0}};
   const bool use_graph = !c->comm || c->comm_graphs;
@@ -926,7 +930,8 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
       launch_mom_reduce(c->stream, jd);
       NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
     }
-    launch_lm_step(c->stream, jd, nullptr);
+    launch_lm_step(c->stream, jd, c->state_dev.as<AlignState>(), c->slab.as<double>(), g.mom_blocks,
+                   c->comm ? c->mom.as<double>() : nullptr, nullptr);
   }
   HIP_TRY(hipGetLastError());
   return GICP_OK;

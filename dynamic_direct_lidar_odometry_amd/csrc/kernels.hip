@@ -1934,7 +1934,9 @@ constexpr int kMomWaves = 8;    // waves per moment block (512 threads: 256 bloc
 // (A last-block-done fusion of k_lm_step into this kernel measured slower:
 // 27.3 us against 9 + 13.5 us — every block's agent-scope release writes
 // back its XCD's L2 before the completion counter.)
-__device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job);
+__device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, AlignState* __restrict__ st,
+                                             const double* __restrict__ slab, int nblocks,
+                                             const double* __restrict__ premom);
 
 // Exact ties of update_correspondences' 1-NN (nano_gicp_impl.hpp:255): the
 // reference keeps the equidistant point nanoflann's walk meets first
@@ -2084,6 +2086,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       }
       unsigned long long bk = ~0ull;
       float d2 = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
+      const bool track2 = tie_detect;   // the second distance only feeds the tie test
       constexpr int kU = 8;   // loads in flight
       for (unsigned k = 0; k < cnt; k += kU) {
         float4 pp[kU];
@@ -2095,12 +2098,12 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
             const float dd = dist2(lqx, lqy, lqz, pp[u].x, pp[u].y, pp[u].z);
             const unsigned long long kk = dkey(dd, __float_as_int(pp[u].w));
             if (kk < bk) {
-              if (bk != ~0ull) d2 = fminf(d2, __uint_as_float((unsigned)(bk >> 32)));
+              if (track2 && bk != ~0ull) d2 = fminf(d2, __uint_as_float((unsigned)(bk >> 32)));
               bk = kk;
               bx = pp[u].x;
               by = pp[u].y;
               bz = pp[u].z;
-            } else {
+            } else if (track2) {
               d2 = fminf(d2, dd);
             }
           }
@@ -2262,7 +2265,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       atomicExch(arrive, 0u);   // re-armed for the next iteration (k_align_init zeroes it per align)
     }
     __syncthreads();
-    lm_step_body(job);
+    lm_step_body(job, job->state, job->slab, job->nblocks, nullptr);
   }
 }
 template __global__ void k_moments<false>(const AlignJob*);
@@ -2282,8 +2285,10 @@ __device__ void so3_exp_d(const double w[3], double R[9]) {  // gicp/so3.hpp:101
   } else {
     const double theta = sqrt(theta_sq);
     const double half = 0.5 * theta;
-    imag = sin(half) / theta;
-    real = cos(half);
+    double sh, ch;
+    sincos(half, &sh, &ch);   // one argument reduction for both
+    imag = sh / theta;
+    real = ch;
   }
   const double qw = real, qx = imag * w[0], qy = imag * w[1], qz = imag * w[2];
   const double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
@@ -2517,10 +2522,9 @@ constexpr int kLmRowsPerPart = (kMomBlocksMax + kLmParts - 1) / kLmParts;  // sl
 // mom[kSlabStride] by one workgroup: thread (p, v2) sums column pair v2 of
 // rows p, p + 12, ... with 16-byte loads (kLmParts x 40 threads), then 80
 // threads add the 12 partials in order (fixed order => deterministic).
-__device__ __forceinline__ void reduce_slab(const AlignJob* job, double (*part)[kSlabStride], double* mom) {
+__device__ __forceinline__ void reduce_slab(const double* slab_in, int nb, double (*part)[kSlabStride], double* mom) {
   const int tid = threadIdx.x;
-  const int nb = job->nblocks;
-  const auto slab = (const __attribute__((address_space(1))) d2v*)gp(job->slab);
+  const auto slab = (const __attribute__((address_space(1))) d2v*)gp(slab_in);
   constexpr int kPairs = kSlabStride / 2;
   if (tid < kLmParts * kPairs) {
     // unconditional (clamped) loads, summed in row order; fully unrolled, so
@@ -2555,7 +2559,7 @@ __global__ __launch_bounds__(kLmThreads) void k_mom_reduce(const AlignJob* __res
   if (__builtin_amdgcn_readfirstlane(st->done)) return;
   __shared__ double part[kLmParts][kSlabStride];
   __shared__ double mom[kSlabStride];
-  reduce_slab(job, part, mom);
+  reduce_slab(job->slab, job->nblocks, part, mom);
   if (threadIdx.x < kSlabStride) gpw(job->mom)[threadIdx.x] = mom[threadIdx.x];
 }
 
@@ -2572,8 +2576,12 @@ __global__ __launch_bounds__(kLmThreads) void k_mom_reduce(const AlignJob* __res
 #else
 #define LM_PROF(i)
 #endif
-__device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job) {
-  AlignState* st = job->state;
+// st, slab, nblocks: job->state, job->slab, job->nblocks, passed as kernel
+// arguments so the slab loads need no job load first; premom: the moments
+// already reduced (and summed across shards: job->mom), else nullptr.
+__device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, AlignState* __restrict__ st,
+                                             const double* __restrict__ slab, int nblocks,
+                                             const double* __restrict__ premom) {
 #ifdef DDLO_LM_PROF
   unsigned long long lm_t[6];
 #endif
@@ -2604,11 +2612,11 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job) {
   const double rotation_epsilon = job->rotation_epsilon, transformation_epsilon = job->transformation_epsilon;
   const int reuse = job->reuse;
   const float reuse_rec_eps = job->reuse_rec_eps, reuse_rec_conv = job->reuse_rec_conv;
-  if (job->premom) {  // moments already reduced (and summed across shards)
-    if (tid < kSlabStride) mom[tid] = gp((const double*)job->mom)[tid];
+  if (premom) {  // moments already reduced (and summed across shards)
+    if (tid < kSlabStride) mom[tid] = gp(premom)[tid];
     __syncthreads();
   } else {
-    reduce_slab(job, part, mom);   // ends with a barrier: Rt_s is visible too
+    reduce_slab(slab, nblocks, part, mom);   // ends with a barrier: Rt_s is visible too
   }
   LM_PROF(1);
   const Moments mo{mom};
@@ -2638,12 +2646,16 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job) {
   __syncthreads();
   LM_PROF(2);
   const int ntr = lm ? min(lm_max_iterations, kMaxTrials) : 1;
+  // one trial per thread (one wavefront issues them all: a trial per
+  // wavefront with wave-uniform pivots measured 2x slower, the waves then
+  // share the SIMDs' fp64 issue)
   if (tid < ntr) {
+    const int trial = tid;
     double lambda = 0.0;
     if (lm) {
       lambda = lambda0_s;
       double nu = 2.0;
-      for (int k = 0; k < tid; ++k) {
+      for (int k = 0; k < trial; ++k) {
         lambda = nu * lambda;
         nu = 2 * nu;
       }
@@ -2659,34 +2671,34 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job) {
     td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
     double den = 0.0;
     for (int e = 0; e < 6; ++e) den += d[e] * (lambda * d[e] - bs[e]);
-    tr_den[tid] = den;
-    tr_lambda[tid] = lambda;
+    tr_den[trial] = den;
+    tr_lambda[trial] = lambda;
     // is_converged's measure max(|Rd - I| / rot_eps, |td| / trans_eps) (lsq_registration_impl.hpp:128-139)
     double cm = 0.0;
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) cm = fmax(cm, fabs(Rd[3 * i + j] - (i == j ? 1.0 : 0.0)) / rotation_epsilon);
     for (int i = 0; i < 3; ++i) cm = fmax(cm, fabs(td[i]) / transformation_epsilon);
-    tr_cm[tid] = cm;
-    tr_conv[tid] = fixed_iterations <= 0 && cm < 1;
+    tr_cm[trial] = cm;
+    tr_conv[trial] = fixed_iterations <= 0 && cm < 1;
     double fro = 0.0;
     for (int e = 0; e < 9; ++e) {
       const double dd = Rd[e] - ((e % 4 == 0) ? 1.0 : 0.0);
       fro += dd * dd;
     }
-    tr_fro[tid] = fro;
-    for (int e = 0; e < 9; ++e) tr_R[tid][e] = Rd[e];
-    for (int e = 0; e < 3; ++e) tr_t[tid][e] = td[e];
+    tr_fro[trial] = fro;
+    for (int e = 0; e < 9; ++e) tr_R[trial][e] = Rd[e];
+    for (int e = 0; e < 3; ++e) tr_t[trial][e] = td[e];
     // d = vec([Rd - I | td]), d[3k + a] = D[a][k] (cost_decrease)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int a = 0; a < 3; ++a) tr_d[tid][3 * k + a] = k < 3 ? Rd[3 * a + k] - (a == k ? 1.0 : 0.0) : td[a];
+      for (int a = 0; a < 3; ++a) tr_d[trial][3 * k + a] = k < 3 ? Rd[3 * a + k] - (a == k ? 1.0 : 0.0) : td[a];
   }
   __syncthreads();
   LM_PROF(3);
   // trial cost decrease y0 - y(delta) = 2 <g, d> - d^T W d (cost_decrease),
   // one row of the quadratic form per thread: (trial, row) = (x / 12, x % 12)
-  for (int x = tid; lm && x < 12 * ntr; x += kLmThreads) {
+  for (int x = tid; lm && x < 12 * ntr; x += (int)blockDim.x) {
     const int tr = x / 12, i = x % 12;
     double srow = 0.0;
 #pragma unroll
@@ -2819,14 +2831,16 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job) {
 // publish (optional): a host-mapped AlignState the block copies the final
 // state of this step to (also after an early exit), so the host reads a
 // chunk's result from pinned memory without a device-to-host copy.
-__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job,
+__global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restrict__ job, AlignState* __restrict__ st,
+                                                        const double* __restrict__ slab, int nblocks,
+                                                        const double* __restrict__ premom,
                                                         AlignState* __restrict__ publish) {
-  if (!__builtin_amdgcn_readfirstlane(job->state->done)) lm_step_body(job);
+  if (!__builtin_amdgcn_readfirstlane(st->done)) lm_step_body(job, st, slab, nblocks, premom);
   if (publish) {
     static_assert(sizeof(AlignState) % 16 == 0, "AlignState is copied in 16-byte words");
     __threadfence();   // this block's state stores, then an L1 invalidate before they are read back
     __syncthreads();
-    const int4* src = reinterpret_cast<const int4*>(job->state);
+    const int4* src = reinterpret_cast<const int4*>(st);
     int4* dst = reinterpret_cast<int4*>(publish);
     for (int w = threadIdx.x; w < (int)(sizeof(AlignState) / 16); w += blockDim.x) dst[w] = src[w];
   }
@@ -3134,8 +3148,9 @@ int moment_blocks(int nsrc) {
   const int groups = (nsrc + 63) / 64;
   return std::max(1, std::min((groups + kMomWaves - 1) / kMomWaves, kMomBlocksMax));
 }
-void launch_lm_step(hipStream_t s, const AlignJob* job, AlignState* publish) {
-  k_lm_step<<<1, kLmThreads, 0, s>>>(job, publish);
+void launch_lm_step(hipStream_t s, const AlignJob* job, AlignState* st, const double* slab, int nblocks,
+                    const double* premom, AlignState* publish) {
+  k_lm_step<<<1, kLmThreads, 0, s>>>(job, st, slab, nblocks, premom, publish);
 }
 void launch_mom_reduce(hipStream_t s, const AlignJob* job) { k_mom_reduce<<<1, kLmThreads, 0, s>>>(job); }
 void launch_residual_image(hipStream_t s, const float4* pts, const int* perm, const int* inv_perm, int n,

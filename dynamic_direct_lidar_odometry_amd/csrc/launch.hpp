@@ -63,7 +63,10 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g);
 int search_queries_per_wave();
 int task_cap_per_region(int nsrc);   // task-list slots per region for nsrc source points
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
-void launch_lm_step(hipStream_t s, const AlignJob* job, AlignState* publish);
+// st / slab / nblocks / premom: the job's state, slab rows and (sharded) all-reduced moments, as
+// kernel arguments (the state and slab loads then need no job load first)
+void launch_lm_step(hipStream_t s, const AlignJob* job, AlignState* st, const double* slab, int nblocks,
+                    const double* premom, AlignState* publish);
 void launch_mom_reduce(hipStream_t s, const AlignJob* job);  // sharded align: slab -> job->mom
 void launch_residuals(hipStream_t s, const AlignJob* job, int nsrc, double* out);
 void launch_residual_image(hipStream_t s, const float4* pts, const int* perm, const int* inv_perm, int n,

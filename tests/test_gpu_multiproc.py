@@ -120,3 +120,69 @@ def test_two_processes_sum_to_unsharded(mode, grid):
     np.testing.assert_allclose(m[:73], full[:73], rtol=1e-10, atol=1e-10 * np.abs(full[:73]).max())
     if grid:
         assert res[0][2] == 1 and res[1][2] == 1
+
+
+def _rccl_worker(rank, world, port, q):
+    """ShardedGicp in slab mode with its own RCCL communicator: rank 0 builds the whole submap's tree and
+    sends every rank its restriction over RCCL (gicp_set_tie_trees_from_root); then a sharded align."""
+    import torch.distributed as dist
+    import dynamic_direct_lidar_odometry_amd as P
+    from dynamic_direct_lidar_odometry_amd.shard import ShardedGicp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = load_golden("gicp_s2m.npz")
+        obj = [P.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        try:
+            sh = ShardedGicp(0, rank, world, obj[0], P.default_params(**S2M), mode="slabs")
+        except P.GicpError as e:   # e.g. RCCL refusing two ranks on one device
+            q.put((rank, "skip", str(e)))
+            return
+        guess = np.asarray(g["guess"], np.float32)
+        sh.set_target(np.ascontiguousarray(g["sub"]), np.ascontiguousarray(g["cov_sub"]),
+                      source=np.ascontiguousarray(g["src"]), guess=guess)
+        db = sh.ctx.device_bytes()
+        sh.set_source(np.ascontiguousarray(g["src"]), np.ascontiguousarray(g["cov_src"]))
+        T, r = sh.align(guess)
+        q.put((rank, "ok", (np.asarray(T), int(r.iterations_run), db["tie_tree"], db["tie_builder"], len(sh.local_index))))
+        sh.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_slab_tie_trees_over_rccl():
+    """Two processes, slab mode, the tie-tree blobs sent over the library's RCCL communicator: every rank
+    holds a tie tree of its own points only, and the sharded align equals the unsharded one (pose 1e-6,
+    same iteration count).  Skipped where RCCL will not open two ranks on one device."""
+    import dynamic_direct_lidar_odometry_amd as P
+    import torch.multiprocessing as mp
+    g = load_golden("gicp_s2m.npz")
+    c = _ctx(g, 0)
+    T0, r0 = c.align(np.asarray(g["guess"], np.float32))
+    c.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rccl_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            rank, kind, payload = q.get(timeout=200)
+            res[rank] = (kind, payload)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    if any(k == "skip" for k, _ in res.values()):
+        pytest.skip("RCCL: " + next(v for k, v in res.values() if k == "skip"))
+    for rank in (0, 1):
+        T, iters, tie_bytes, builder_bytes, nloc = res[rank][1]
+        assert iters == r0.iterations_run
+        np.testing.assert_allclose(T, T0, atol=1e-6)
+        assert tie_bytes > 0 and builder_bytes == 0 and nloc <= len(g["sub"])

@@ -46,11 +46,19 @@ def knn_only(ref, nk, k):
     return set(out)
 
 
-def run_chain(frames, params):
+def run_chain(frames, params, progress=False, stop=None):
+    """Both drivers over `frames`, every decision compared.  stop(i, stats, sub, kf_frame) -> True ends
+    the chain early; kf_frame[k] = the frame that added keyframe k."""
+    import time
     gpu = OD.Odometry(0, params)
     ref = R.OdomRef(params, threads=THREADS)
-    stats = dict(tracked=0, changes=0, hull_changes=0, dropped=0)
+    stats = dict(tracked=0, changes=0, hull_changes=0, dropped=0, frames=0)
+    kf_frame = []
+    t0 = time.time()
     for i, f in enumerate(frames):
+        stats["frames"] = i + 1
+        if progress and i % 25 == 0:
+            print(f"frame {i}: {time.time() - t0:.0f} s, keyframes {len(kf_frame)}, {stats}", flush=True)
         g = gpu.process(f)
         o = ref.process(f)
         assert g.status == o["status"], i
@@ -62,6 +70,7 @@ def run_chain(frames, params):
             continue
         stats["tracked"] += 1
         assert g.num_keyframes == o["num_keyframes"], i
+        kf_frame.extend([i] * max(int(g.num_keyframes) - len(kf_frame), 0))
         sub = gpu.submap().tolist()
         assert sub == o["submap"], i
         assert g.submap_changed == o["submap_changed"], i
@@ -76,7 +85,10 @@ def run_chain(frames, params):
                 stats["hull_changes"] += 1
             if len(sub) < nk:
                 stats["dropped"] += 1
+        if stop is not None and stop(i, stats, sub, kf_frame):
+            break
     gpu.close()
+    stats["kf_frame"] = kf_frame
     return stats, len(ref.keyframes)
 
 
@@ -94,3 +106,31 @@ def test_cfg5_chain_hull_driven_submaps(frames210):
     assert nk >= 5, nk
     assert stats["hull_changes"] >= 1, stats
     assert stats["dropped"] >= 1, stats
+
+
+LAP_FRAMES = 700   # frames per lap of cfg 5's loop (scene.loop_trajectory: ~1.4 laps in 1000 frames)
+
+
+@pytest.mark.skipif(not __import__("os").environ.get("DDLO_LONG_TESTS"),
+                    reason="about 10 minutes: DDLO_LONG_TESTS=1 (its log is committed under profiles/)")
+def test_cfg5_chain_through_loop_revisit():
+    """ddlo.yaml parameters from frame 0 until the second lap's submaps take first-lap keyframes (the loop
+    revisit of OdomNode::getSubmapKeyframes, odom.cc:1215-1315: the k-NN and convex-hull keyframes of the
+    current position include keyframes made one lap earlier), plus 30 frames: every decision exact,
+    poses within 1e-4, as in the 210-frame chain."""
+    frames = scene.loop_sequence(64, 2048, 0, 1000, device=0)[0]
+    seen = {}
+
+    def stop(i, stats, sub, kf_frame):
+        if sub and kf_frame and "revisit" not in seen:
+            early = [k for k in sub if k < len(kf_frame) and kf_frame[k] < 150]
+            late = [k for k in sub if k < len(kf_frame) and kf_frame[k] >= LAP_FRAMES - 150]
+            if early and late and i >= LAP_FRAMES - 150:
+                seen["revisit"] = (i, sorted(sub), [kf_frame[k] for k in sorted(sub)])
+                print(f"revisit at frame {i}: submap keyframes {seen['revisit'][1]}, made at frames "
+                      f"{seen['revisit'][2]}", flush=True)
+        return "revisit" in seen and i >= seen["revisit"][0] + 30
+
+    stats, nk = run_chain(frames, OD.default_odom_params(), progress=True, stop=stop)
+    print(f"chain: {stats['frames']} frames, {nk} keyframes, {stats['changes']} submap changes", flush=True)
+    assert "revisit" in seen, stats

@@ -1,5 +1,5 @@
-"""Per-launch HBM-side traffic of the linearize (k_nn_seed [+ k_nn_collect] +
-k_nn_scan + k_moments) from two rocprofv3 --pmc passes over bench.py
+"""Per-launch HBM-side traffic of the linearize (k_moments with the fused
+candidate-cell lookup, or k_cell_lookup / k_nn_seed + k_nn_scan + k_moments) from two rocprofv3 --pmc passes over bench.py
 (FETCH_SIZE, WRITE_SIZE; kB units), per kernel.
 
 Counters (MI355X_MICROARCH.md, HBM section): both count L2 -> fabric
@@ -12,7 +12,8 @@ x2; k_moments streams its own 16 B / 48 B per point but gathers the
 target's covariances, so it is reported raw too, with the x2 figure beside
 it as the upper bound.  `bytes_per_linearize` (what bench.py reports as
 roofline.traffic) is the raw sum.  Active iterations only: search
-dispatches that together ran >= 20 us (a no-op iteration exits at once).
+dispatches that together ran >= 20 us, or a k_moments >= MOM_NOOP_US (a no-op
+iteration exits at once).
 
 usage: python tools/pmc_traffic.py fetch.csv write.csv [out.json]
 """
@@ -21,7 +22,8 @@ import json
 import sys
 from collections import defaultdict
 
-SEARCH = ("k_nn_seed", "k_nn_collect", "k_nn_scan", "k_nn_search")
+SEARCH = ("k_cell_lookup", "k_nn_seed", "k_nn_collect", "k_nn_scan")
+MOM_NOOP_US = 6.0   # a k_moments that exits at once; the fused candidate-cell linearize has no search kernel
 
 
 def short(name):
@@ -42,10 +44,11 @@ def per_iteration(path, counter):
             continue
         val = float(r["Counter_Value"]) * 1024.0   # kB -> bytes
         cur[k] += val
+        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         if k in SEARCH:
-            dur_s += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            dur_s += dur
         else:   # k_moments closes the iteration
-            if dur_s >= 20.0:
+            if dur_s >= 20.0 or dur >= MOM_NOOP_US:
                 out.append(dict(cur))
             cur, dur_s = defaultdict(float), 0.0
     return out

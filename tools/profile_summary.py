@@ -3,10 +3,12 @@
 usage: python tools/profile_summary.py <rocprof dir> [prefix=run] > profiles/<name>.md
 
 Besides rocprof's own per-kernel stats it splits every align() into its outer
-iterations (k_align_init, then per iteration the search kernels — k_nn_collect +
-k_nn_scan, or the single-kernel k_nn_search — k_moments and k_lm_step)
-and separates ACTIVE iterations from no-op launches (an iteration after
-convergence exits at its first instruction: search kernels < NOOP_US).  No-ops
+iterations (k_align_init, then per iteration the search kernels — k_cell_lookup,
+k_nn_seed + k_nn_scan, or none when the candidate-cell lookup is fused into
+k_moments — k_moments, k_mom_reduce + RCCL's all-reduce (sharded) and
+k_lm_step) and separates ACTIVE iterations from no-op launches (an
+iteration after convergence exits at its first instruction: search kernels
+< NOOP_US and k_moments < MOM_NOOP_US).  No-ops
 are counted per origin: the eager profiled path (gicp_set_profiling)
 launches all max_iterations iterations of an align, a graph align launches
 at most one speculative chunk after the converged one.  The "linearize" average (search + k_moments of
@@ -18,6 +20,8 @@ import sys
 from collections import defaultdict
 
 NOOP_US = 20.0   # summed search kernels of an iteration that exits at once (three launches, ~4-6 us each)
+MOM_NOOP_US = 6.0   # k_moments of an iteration that exits at once (~3.5-4.7 us); the fused candidate-cell
+                    # linearize (k_moments<.., LOOKUP>) has no search kernel at all
 
 
 def short(name):
@@ -38,8 +42,10 @@ def main():
     trace = list(csv.DictReader(open(f"{d}/{pre}_kernel_trace.csv")))
     trace.sort(key=lambda x: int(x["Start_Timestamp"]))
     seq = [(short(x["Kernel_Name"]).split("<")[0], (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3) for x in trace]
-    SEARCH = ("k_nn_search", "k_nn_seed", "k_nn_collect", "k_nn_scan")
-    LOOP = SEARCH + ("k_moments", "k_lm_step")
+    SEARCH = ("k_cell_lookup", "k_nn_seed", "k_nn_collect", "k_nn_scan")
+    LOOP = SEARCH + ("k_moments", "k_lm_step", "k_mom_reduce")
+    # a sharded align's all-reduce sits between k_mom_reduce and k_lm_step (RCCL's own kernel)
+    SKIP = ("ncclDevKernel", "ncclKernel", "__amd_rocclr")
     aligns = []
     cur = None
     for n, us in seq:
@@ -48,6 +54,8 @@ def main():
             aligns.append(cur)
         elif cur is not None and n in LOOP:
             cur.append((n, us))
+        elif cur is not None and n.startswith(SKIP):
+            continue
         else:
             cur = None
     per_pos = defaultdict(lambda: defaultdict(list))
@@ -70,14 +78,16 @@ def main():
         for k in iters:
             s_us = sum(k[n] for n in SEARCH)
             m, l = k["k_moments"], k["k_lm_step"]
-            if s_us < NOOP_US:
+            if s_us < NOOP_US and m < MOM_NOOP_US:
                 (noop_eager if eager else noop).append(s_us + m + l)
                 continue
             per_pos[it]["search"].append(s_us)
             per_pos[it]["seed"].append(k["k_nn_seed"])
             per_pos[it]["collect"].append(k["k_nn_collect"])
             per_pos[it]["scan"].append(k["k_nn_scan"])
+            per_pos[it]["lookup"].append(k["k_cell_lookup"])
             per_pos[it]["moments"].append(m)
+            per_pos[it]["reduce"].append(k["k_mom_reduce"])
             per_pos[it]["lm"].append(l)
             active_lin.append(s_us + m)
             active_search.append(s_us)
@@ -88,12 +98,12 @@ def main():
     print(f"\n## Active outer iterations ({len(aligns)} aligns, {len(active_lin)} active iterations; no-op "
           f"iterations: {len(noop)} in {len(aligns) - eager_aligns} graph aligns (speculative chunk), "
           f"{len(noop_eager)} in {eager_aligns} eager profiled aligns)\n")
-    print("| iteration | n | search us (seed + collect + scan) | k_moments us | k_lm_step us |")
-    print("|---:|---:|---:|---:|---:|")
+    print("| iteration | n | search us (lookup + seed + scan) | k_moments us | k_mom_reduce us | k_lm_step us |")
+    print("|---:|---:|---:|---:|---:|---:|")
     for it in sorted(per_pos):
         p = per_pos[it]
-        print(f"| {it} | {len(p['search'])} | {avg(p['search']):.1f} ({avg(p['seed']):.1f} + {avg(p['collect']):.1f} + {avg(p['scan']):.1f}) | "
-              f"{avg(p['moments']):.1f} | {avg(p['lm']):.1f} |")
+        print(f"| {it} | {len(p['search'])} | {avg(p['search']):.1f} ({avg(p['lookup']):.1f} + {avg(p['seed']):.1f} + {avg(p['scan']):.1f}) | "
+              f"{avg(p['moments']):.1f} | {avg(p['reduce']):.1f} | {avg(p['lm']):.1f} |")
     print(f"\n- linearize (search kernels + k_moments) average over active iterations: **{avg(active_lin):.1f} us** "
           f"(search {avg(active_search):.1f} + moments {avg(active_mom):.1f})")
     print(f"- k_lm_step average over active iterations: {avg(active_lm):.1f} us")
