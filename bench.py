@@ -149,6 +149,15 @@ def roofline_block(bytes_per_launch, launch_s, kernel, unit_bytes):
             "algorithmic_bytes_per_launch": int(bytes_per_launch), "bytes_rule": unit_bytes}
 
 
+def lin_kernel_label(ctx):
+    g = ctx.grid_info()
+    if g["built"] and g["fallback_fine"] == 0 and g["overflow_cells"] == 0:
+        return "linearize = k_moments with the fused candidate-cell lookup (one kernel per outer iteration)"
+    if g["built"]:
+        return "linearize = k_cell_lookup + k_nn_seed (walk of the unlisted sub-groups) + k_moments (per outer iteration)"
+    return "linearize = k_nn_seed + k_nn_scan + k_moments (per outer iteration)"
+
+
 def lin_roofline(ctx, guess, n_owned, reps=5):
     """Linearize roofline of a ctx's align (HIP events on the library stream, gicp_set_profiling)."""
     ctx.set_profiling(True)
@@ -159,9 +168,33 @@ def lin_roofline(ctx, guess, n_owned, reps=5):
         launches += r.iterations_run
     ctx.set_profiling(False)
     ctx.synchronize()
-    return roofline_block(76.0 * n_owned, ms * 1e-3 / max(launches, 1),
-                          "linearize = k_nn_seed + k_nn_scan + k_moments (per outer iteration)",
+    return roofline_block(76.0 * n_owned, ms * 1e-3 / max(launches, 1), lin_kernel_label(ctx),
                           "B_lin = 76 B x owned source points")
+
+
+def cfg3_walk_leg(ctx, guess, args, result):
+    """The headline's aligns with the target's candidate cells off: the seed + walk + scan search."""
+    from dynamic_direct_lidar_odometry_amd import GRID_OFF, GRID_ON
+    ctx.set_target_grid(GRID_OFF)
+    for _ in range(3):
+        ctx.align(guess)
+    ctx.synchronize()
+    t_w = time.perf_counter()
+    nw = max(20, args.steps // 4)
+    for _ in range(nw):
+        ctx.align(guess)
+    ctx.synchronize()
+    walk_ms = 1e3 * (time.perf_counter() - t_w) / nw
+    ctx.set_profiling(True)
+    wl_ms, wl_n = 0.0, 0
+    for _ in range(5):
+        _, r = ctx.align(guess)
+        wl_ms += r.linearize_ms
+        wl_n += r.iterations_run
+    ctx.set_profiling(False)
+    ctx.set_target_grid(GRID_ON)
+    result["cfg3_walk"] = {"ms_per_scan": round(walk_ms, 4), "linearize_us": round(1e3 * wl_ms / max(wl_n, 1), 2),
+                           "note": "candidate cells off (gicp_set_target_grid 0): the seed + walk + scan search"}
 
 
 def rot_err(A, B):
@@ -563,6 +596,8 @@ def main():
     ap.add_argument("--gn-steps", type=int, default=10)
     ap.add_argument("--no-odom", action="store_true", help="skip the cfg5 odometry-driver (S2M chain) leg")
     ap.add_argument("--no-seg", action="store_true", help="skip the range-image segmentation leg")
+    ap.add_argument("--no-walk", action="store_true",
+                    help="skip the cfg3 comparison with the candidate cells off (counter / trace runs of the headline)")
     ap.add_argument("--seg-steps", type=int, default=50)
     args = ap.parse_args()
 
@@ -664,8 +699,7 @@ def main():
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_unit": "bytes per linearize launch (L2->fabric, Infinity-Cache hits included; counters as read)",
                      "traffic_source": traffic_src,
-                     "kernel": "linearize = k_cell_lookup (candidate cells) + k_nn_seed (walk of the sub-groups "
-                               "without a list; none here) + k_moments (per outer iteration)",
+                     "kernel": lin_kernel_label(ctx),
                      "avg_launch_us": round(avg_launch_s * 1e6, 2),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch)},
     }
@@ -675,26 +709,8 @@ def main():
                              "note": "candidate cells of the submap, built once per target (first align, outside "
                                      "ms/scan like the index build, SURVEY.md §8(d)); the odometry leg pays them"}
     # the same aligns with the cells off (the round-4 walk), for comparison
-    ctx.set_target_grid(GRID_OFF)
-    for _ in range(3):
-        ctx.align(guess)
-    ctx.synchronize()
-    t_w = time.perf_counter()
-    nw = max(20, args.steps // 4)
-    for _ in range(nw):
-        ctx.align(guess)
-    ctx.synchronize()
-    walk_ms = 1e3 * (time.perf_counter() - t_w) / nw
-    ctx.set_profiling(True)
-    wl_ms, wl_n = 0.0, 0
-    for _ in range(5):
-        _, r = ctx.align(guess)
-        wl_ms += r.linearize_ms
-        wl_n += r.iterations_run
-    ctx.set_profiling(False)
-    ctx.set_target_grid(GRID_ON)
-    result["cfg3_walk"] = {"ms_per_scan": round(walk_ms, 4), "linearize_us": round(1e3 * wl_ms / max(wl_n, 1), 2),
-                           "note": "candidate cells off (gicp_set_target_grid 0): the seed + walk + scan search"}
+    if not args.no_walk:
+        cfg3_walk_leg(ctx, guess, args, result)
 
     # the launch predictor's misses in the number: cycle 8 distinct guesses
     # (the headline repeats one, so its iteration count is always predicted)

@@ -222,7 +222,7 @@ constexpr double kGridMaxReach = 4.0;     // bounds beyond this: cells farther t
 constexpr int kGridListMax = 32;
 constexpr int kGridAutoAligns = 32;       // GICP_GRID_AUTO: built at this align against the same target and bound
 constexpr int kGridListCap = kCgCandMax;  // finest level: longer lists are not stored (the walk)
-constexpr long kGridMaxCells = 48L << 20; // coarse cells (the directory is 4 B per cell)
+constexpr long kGridMaxCells = 48L << 20; // coarse cells (the directory is 8 B per cell)
 
 gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_ptr<CellGridData>* out) {
   hipStream_t s = c->stream;
@@ -291,11 +291,11 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   HIP_TRY(band.ensure(sizeof(int) * (size_t)ncells));
   HIP_TRY(dnum.ensure(sizeof(int) * 8));
   HIP_TRY(db_buf.ensure(sizeof(CgBuild)));
-  HIP_TRY(g->dir.ensure(sizeof(unsigned) * (size_t)ncells));
+  HIP_TRY(g->dir.ensure(sizeof(unsigned long long) * (size_t)ncells));
   b.rep = rep.as<int>();
   b.rep_tmp = rep_tmp.as<int>();
   b.rep_final = rep.as<int>();   // x: rep -> tmp, y: tmp -> rep, z: rep -> tmp; see below
-  b.dir = g->dir.as<unsigned>();
+  b.dir = g->dir.as<unsigned long long>();
   b.band = band.as<int>();
   b.ctr = ctr.as<unsigned>();
   CgBuild* db = db_buf.as<CgBuild>();
@@ -458,7 +458,7 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   g->info.bytes = (int64_t)(g->dir.bytes + g->fine.bytes + g->ent.bytes);
   g->info.built = 1;
   CellGridDev& d = g->dev;
-  d.dir = g->dir.as<unsigned>();
+  d.dir = g->dir.as<unsigned long long>();
   d.fine = g->fine.as<uint2>();
   d.ent = g->ent.as<float4>();
   d.ox = b.fox;

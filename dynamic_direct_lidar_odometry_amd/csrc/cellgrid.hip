@@ -369,8 +369,8 @@ __global__ __launch_bounds__(256) void k_cg_prop(const CgBuild* __restrict__ bp,
   out[c] = best;
 }
 
-__global__ __launch_bounds__(256) void k_cg_dir_fill(unsigned* __restrict__ dir, const int* __restrict__ band,
-                                                     long ncells, unsigned outside) {
+__global__ __launch_bounds__(256) void k_cg_dir_fill(unsigned long long* __restrict__ dir, const int* __restrict__ band,
+                                                     long ncells, unsigned long long outside) {
   const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c < ncells) dir[c] = band[c] != kRepNone ? kCgFallback : outside;
 }
@@ -748,7 +748,8 @@ __global__ __launch_bounds__(64 * kCgWaves) void k_cg_emit_write(const CgBuild* 
   const uint2* hdr = L.hdr + (size_t)s * nf;
   const unsigned fb = fine_base + fine_off[wave];
   unsigned eb = ent_base + ent_off[wave];
-  if (lane == 0) b.dir[b.band[bi]] = ((unsigned)level << 30) | fb;
+  // level 0: the one list inline in the directory (no fine-table load in the lookup)
+  if (lane == 0 && level > 0) b.dir[b.band[bi]] = ((unsigned long long)level << 62) | fb;
   for (int f0 = 0; f0 < nf; f0 += 64) {
     const int f = f0 + lane;
     uint2 h = make_uint2(0u, 0u);
@@ -766,6 +767,7 @@ __global__ __launch_bounds__(64 * kCgWaves) void k_cg_emit_write(const CgBuild* 
     if (f < nf) {
       b.fine[fb + f] = stored ? make_uint2(eb + ex, k) : make_uint2(0u, kCgFineFallback);
       if (!stored) atomicAdd(b.ctr + kCtrFineFb * 32, 1u);
+      if (level == 0) b.dir[b.band[bi]] = stored ? (((unsigned long long)k << 32) | (eb + ex)) : kCgFallback;
     }
     // copies: this chunk's lists, one fine cell after another
     const unsigned tot = __shfl(incl, 63);
@@ -793,7 +795,7 @@ void launch_cg_occ(hipStream_t s, const CgBuild* db, int n) {
 void launch_cg_prop(hipStream_t s, const CgBuild* db, int axis, const int* in, int* out, long ncells) {
   k_cg_prop<<<cdiv_l(ncells, 256), 256, 0, s>>>(db, axis, in, out, ncells);
 }
-void launch_cg_dir_fill(hipStream_t s, unsigned* dir, const int* band, long ncells, unsigned outside) {
+void launch_cg_dir_fill(hipStream_t s, unsigned long long* dir, const int* band, long ncells, unsigned long long outside) {
   k_cg_dir_fill<<<cdiv_l(ncells, 256), 256, 0, s>>>(dir, band, ncells, outside);
 }
 void launch_cg_band_flags(hipStream_t s, const CgBuild* db, const int* band, unsigned char* flags, long nblocked) {

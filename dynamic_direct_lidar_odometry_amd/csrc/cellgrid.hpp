@@ -61,7 +61,7 @@ struct CgBuild {
   int* rep;                 // [ncells] a target point of each occupied cell (sorted position; INT_MAX: none)
   int* rep_tmp;             // [ncells] propagation scratch
   int* rep_final;           // [ncells] a near target point within r cells (Chebyshev), INT_MAX: none (= not band)
-  unsigned* dir;            // [ncells] output
+  unsigned long long* dir;  // [ncells] output (CellGridDev::dir)
   int* band;                // [ncells] band cell ids, 4x4x4-blocked order
   int* cnn;                 // [nband] the band cell's near target point (sorted position)
   unsigned* ctr;            // [kCgCounters]
@@ -81,7 +81,7 @@ constexpr size_t kCgCtrWords = (size_t)(kCgCounters + (kCgMaxLevel + 1) * kCgSha
 
 void launch_cg_occ(hipStream_t s, const CgBuild* db, int n);
 void launch_cg_prop(hipStream_t s, const CgBuild* db, int axis, const int* in, int* out, long ncells);
-void launch_cg_dir_fill(hipStream_t s, unsigned* dir, const int* band, long ncells, unsigned outside);
+void launch_cg_dir_fill(hipStream_t s, unsigned long long* dir, const int* band, long ncells, unsigned long long outside);
 void launch_cg_band_flags(hipStream_t s, const CgBuild* db, const int* band, unsigned char* flags, long nblocked);
 void launch_cg_centers(hipStream_t s, CgBuild* db, int nband);
 void launch_cg_coarse(hipStream_t s, const CgBuild* db, int nband);

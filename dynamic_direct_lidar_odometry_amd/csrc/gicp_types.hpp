@@ -97,13 +97,17 @@ struct NfTreeDev {
 // with it) for some point of C.  Coarse cells of size s tile the target's
 // box plus the bound; a coarse cell is split uniformly into (2^level)^3 fine
 // cells.
-constexpr unsigned kCgNoMatch = 0xffffffffu;    // dir: no target point within the bound of any point of the cell
-constexpr unsigned kCgFallback = 0xfffffffeu;   // dir: no list (the walk searches the cell's queries)
+// Directory entry (u64) of a coarse cell: kCgNoMatch, kCgFallback, a
+// level-0 list inline (bits 62-63 = 0: entry offset in bits 0-31, count in
+// 32-61: no fine-table load on the lookup's dependent chain), or a refined
+// cell (bits 62-63 = level 1..3, fine-table base in bits 0-31).
+constexpr unsigned long long kCgNoMatch = ~0ull;       // no target point within the bound of any point of the cell
+constexpr unsigned long long kCgFallback = ~0ull - 1;  // no list (the walk searches the cell's queries)
 constexpr unsigned kCgFineFallback = 0xffffffffu;   // fine entry count: no list (the walk)
 constexpr int kCgMaxLevel = 3;
 
 struct CellGridDev {
-  const unsigned* dir;     // [nx * ny * nz] (level << 30) | fine-table base, or kCgNoMatch / kCgFallback
+  const unsigned long long* dir;   // [nx * ny * nz] directory entries (above)
   const uint2* fine;       // per fine cell: (first entry, count)
   const float4* ent;       // list entries: x, y, z, sorted target position (int bits)
   float ox, oy, oz, inv_s; // grid origin, 1 / coarse cell size
@@ -111,6 +115,30 @@ struct CellGridDev {
   int outside_nomatch;     // a query outside the grid box has no target point within the bound (else the walk)
   int has_fallback;        // some cell has no list (or outside_nomatch is 0): the walk kernel stays in the graph
 };
+
+// The list of the cell holding a query at grid coordinates (tx, ty, tz) (in
+// range): 0 = no target point within the bound, 1 = the list (off, cnt),
+// 2 = no list (the walk).
+__device__ __forceinline__ int cg_cell_list(const CellGridDev& G, float tx, float ty, float tz, unsigned& off,
+                                            unsigned& cnt) {
+  const int cx = min((int)tx, G.nx - 1), cy = min((int)ty, G.ny - 1), cz = min((int)tz, G.nz - 1);
+  const unsigned long long d = G.dir[((long)cx * G.ny + cy) * G.nz + cz];
+  if (d == kCgNoMatch) return 0;
+  if (d == kCgFallback) return 2;
+  const int lvl = (int)(d >> 62);
+  unsigned long long e = d;
+  if (lvl != 0) {
+    const int m = 1 << lvl;
+    const int fx = min((int)((tx - (float)cx) * (float)m), m - 1);
+    const int fy = min((int)((ty - (float)cy) * (float)m), m - 1);
+    const int fz = min((int)((tz - (float)cz) * (float)m), m - 1);
+    e = reinterpret_cast<const unsigned long long*>(G.fine)[(unsigned)d + (unsigned)((fx * m + fy) * m + fz)];
+  }
+  if ((unsigned)(e >> 32) == kCgFineFallback) return 2;
+  off = (unsigned)e;
+  cnt = (unsigned)(e >> 32) & 0x3fffffffu;
+  return 1;
+}
 
 // Per-align device state (one per ctx, lives in device memory).
 struct AlignState {

@@ -1032,23 +1032,7 @@ __global__ __launch_bounds__(256) void k_cell_lookup(const AlignJob* __restrict_
       if (!(tx >= 0.f && tx < (float)G.nx && ty >= 0.f && ty < (float)G.ny && tz >= 0.f && tz < (float)G.nz)) {
         walk = !G.outside_nomatch;   // beyond every target point's reach (or outside the built box)
       } else {
-        const int cx = min((int)tx, G.nx - 1), cy = min((int)ty, G.ny - 1), cz = min((int)tz, G.nz - 1);
-        const unsigned d = gp(G.dir)[((long)cx * G.ny + cy) * G.nz + cz];
-        if (d == kCgFallback) {
-          walk = true;
-        } else if (d != kCgNoMatch) {
-          const int lvl = (int)(d >> 30), m = 1 << lvl;
-          const int fx = min((int)((tx - (float)cx) * (float)m), m - 1);
-          const int fy = min((int)((ty - (float)cy) * (float)m), m - 1);
-          const int fz = min((int)((tz - (float)cz) * (float)m), m - 1);
-          const unsigned long long e =
-              gp(reinterpret_cast<const unsigned long long*>(G.fine))[(d & 0x3fffffffu) + (unsigned)((fx * m + fy) * m + fz)];
-          if ((unsigned)(e >> 32) == kCgFineFallback) walk = true;
-          else {
-            off = (unsigned)e;
-            cnt = (unsigned)(e >> 32);
-          }
-        }
+        walk = cg_cell_list(G, tx, ty, tz, off, cnt) == 2;
       }
     }
     // this slice's part of the list: the (distance, position) minimum and the
@@ -2070,18 +2054,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       if (owned) {
         const float tx = (lqx - G.ox) * G.inv_s, ty = (lqy - G.oy) * G.inv_s, tz = (lqz - G.oz) * G.inv_s;
         if (tx >= 0.f && tx < (float)G.nx && ty >= 0.f && ty < (float)G.ny && tz >= 0.f && tz < (float)G.nz) {
-          const int cx = min((int)tx, G.nx - 1), cy = min((int)ty, G.ny - 1), cz = min((int)tz, G.nz - 1);
-          const unsigned d = gp(G.dir)[((long)cx * G.ny + cy) * G.nz + cz];
-          if (d != kCgNoMatch) {   // (no fallback cell in LOOKUP mode)
-            const int lvl = (int)(d >> 30), m = 1 << lvl;
-            const int fx = min((int)((tx - (float)cx) * (float)m), m - 1);
-            const int fy = min((int)((ty - (float)cy) * (float)m), m - 1);
-            const int fz = min((int)((tz - (float)cz) * (float)m), m - 1);
-            const unsigned long long e = gp(reinterpret_cast<const unsigned long long*>(
-                G.fine))[(d & 0x3fffffffu) + (unsigned)((fx * m + fy) * m + fz)];
-            off = (unsigned)e;
-            cnt = (unsigned)(e >> 32);
-          }
+          cg_cell_list(G, tx, ty, tz, off, cnt);   // (no fallback cell in LOOKUP mode)
         }
       }
       unsigned long long bk = ~0ull;

@@ -20,6 +20,7 @@ from dynamic_direct_lidar_odometry_amd import SOURCE, TARGET, scene  # noqa: E40
 def cfg2(n):
     src, tgt, _ = scene.s2s_pair(64, 2048, 2)
     c = P.Context(0)
+    c.set_target_grid(P.GRID_OFF)   # as bench.py's cfg2 leg (an S2S target is aligned against once)
     c.set_params(P.default_params(k_correspondences=10, max_correspondence_distance=1.0, optimizer=P.GAUSS_NEWTON,
                                   fixed_iterations=20, max_iterations=20))
     c.set_target(tgt)
@@ -46,6 +47,7 @@ def cfg4(n):
     params = P.default_params(k_correspondences=20, max_correspondence_distance=2.0, max_iterations=32,
                               transformation_epsilon=0.01)
     sh = ShardedGicp(0, 0, 1, P.comm_unique_id(), params)
+    sh.ctx.set_target_grid(P.GRID_ON)   # as bench.py's sharded leg: the cells built at the first align
     sh.set_target(sub, tcov)
     sh.set_source(prob["source"], scov)
     g = prob["guess"].astype(np.float32)
