@@ -1,6 +1,7 @@
 """One bench leg's GPU workload alone, for rocprofv3 runs (kernel trace / PMC
 passes) that must not mix legs.  Same problems and parameters as bench.py.
 
+    python tools/legs.py cfg3 [aligns]     # the headline: S2M 131k -> 500k, candidate cells (built first)
     python tools/legs.py cfg2 [aligns]     # S2S 131k <-> 131k, 20 fixed GN iterations
     python tools/legs.py cfg4 [aligns]     # S2M 262k -> 2M, one-rank RCCL (groups mode)
     python tools/legs.py cfg5 [frames]     # per scan: index, k=10 covariances (+ nanoflann tree), S2S align
@@ -29,6 +30,25 @@ def cfg2(n):
     c.compute_covariances(TARGET)
     for _ in range(n):
         c.align()
+    c.synchronize()
+
+
+def cfg3(n):
+    prob = bench.build_problem()
+    sub = np.ascontiguousarray(np.concatenate(prob["keyframes"])[prob["subset"]])
+    tcov = np.ascontiguousarray(bench.keyframe_covariances(lambda: P.Context(0), prob["keyframes"])[prob["subset"]])
+    c = P.Context(0)
+    c.set_params(P.default_params(k_correspondences=10))
+    c.set_source(prob["source"])
+    c.compute_covariances(SOURCE)
+    c.set_params(P.default_params(k_correspondences=20, max_correspondence_distance=2.0, max_iterations=32,
+                                  transformation_epsilon=0.01))
+    c.set_target_grid(P.GRID_ON)
+    c.set_target(sub)
+    c.set_covariances(TARGET, tcov)
+    g = prob["guess"].astype(np.float32)
+    for _ in range(n):
+        c.align(g)
     c.synchronize()
 
 
@@ -77,4 +97,4 @@ def cfg5(n):
 if __name__ == "__main__":
     leg = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    {"cfg2": cfg2, "cfg4": cfg4, "cfg5": cfg5}[leg](n)
+    {"cfg2": cfg2, "cfg3": cfg3, "cfg4": cfg4, "cfg5": cfg5}[leg](n)
