@@ -47,7 +47,7 @@ METRIC = "GICP iters/sec + ms/scan, 131k-pt source → 500k-pt submap; pose Δ v
 HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same workload
 # (tools/pmc_traffic.sh -> tools/pmc_traffic.py), committed per round
-TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r04_traffic.json"))
+TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r05_traffic.json"))
 
 
 def pmc_traffic():
@@ -151,7 +151,7 @@ def roofline_block(bytes_per_launch, launch_s, kernel, unit_bytes):
 
 def lin_kernel_label(ctx):
     g = ctx.grid_info()
-    if g["built"] and g["fallback_fine"] == 0 and g["overflow_cells"] == 0:
+    if g["built"] and not g["uses_walk"]:
         return "linearize = k_moments with the fused candidate-cell lookup (one kernel per outer iteration)"
     if g["built"]:
         return "linearize = k_cell_lookup + k_nn_seed (walk of the unlisted sub-groups) + k_moments (per outer iteration)"

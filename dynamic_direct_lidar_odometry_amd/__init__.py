@@ -93,6 +93,7 @@ class GicpGridInfo(C.Structure):
         ("fine_cells", C.c_int64),
         ("fallback_fine", C.c_int64),
         ("entries", C.c_int64),
+        ("uses_walk", C.c_int64),
     ]
 
     def as_dict(self):

@@ -470,6 +470,7 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   d.nz = b.nz;
   d.outside_nomatch = outside_nomatch ? 1 : 0;
   d.has_fallback = (g->info.fallback_fine > 0 || !outside_nomatch) ? 1 : 0;
+  g->info.uses_walk = d.has_fallback;
   g->ok = true;
   return GICP_OK;
 }

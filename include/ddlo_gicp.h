@@ -256,11 +256,16 @@ typedef struct gicp_grid_info {
   int64_t coarse_cells;      /* cells of the grid box                                 */
   int64_t band_cells;        /* coarse cells within reach of the target               */
   int64_t nomatch_cells;     /* ... of which no point is within the bound             */
-  int64_t overflow_cells;    /* ... whose candidates overflowed (the walk answers)   */
+  int64_t overflow_cells;    /* ... whose candidates overflowed kCgCandMax at level 0
+                                (their children's lists come from a direct walk)     */
   int64_t level_cells[4];    /* coarse cells finished at fine level 0..3              */
   int64_t fine_cells;        /* fine cells with a list                                */
   int64_t fallback_fine;     /* fine cells whose list exceeded the cap (the walk)     */
   int64_t entries;           /* list entries (16 B each)                              */
+  int64_t uses_walk;         /* 1: some queries still take the walk (a fine cell
+                                without a list, or the bound's reach beyond the grid);
+                                0: the linearize is one kernel (lookup fused into the
+                                moments)                                              */
 } gicp_grid_info;
 gicp_status gicp_get_target_grid_info(struct gicp_ctx* ctx, gicp_grid_info* out);
 /* Queries the last align's final linearize answered from the candidate cells
