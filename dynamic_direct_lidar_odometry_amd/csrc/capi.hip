@@ -694,6 +694,10 @@ gicp_status ensure_tie_tree(gicp_ctx* c) {
 }
 
 constexpr int kMaxFirstChunk = 8;  // largest predicted first chunk (iterations)
+// With fixed_iterations the count is known, so the whole align is one graph
+// (up to this many iterations): every later chunk is a separate graph launch
+// and a host round trip (cfg 2: 20 iterations were 1 + 12 chunks)
+constexpr int kMaxFixedChunk = 64;
 
 // One outer iteration: linearize (search + moments), then — on a sharded ctx —
 // this rank's reduced moments all-reduced across ranks (80 doubles over
@@ -787,7 +791,9 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
                                       g.scan_blocks, g.mom_blocks, g.lds_boxes,
                                       g.grid ? (g.grid_walk ? 2L : 1L) * g.lookup_blocks : 0}};
   const bool use_graph = !c->comm || c->comm_graphs;
-  const int first = std::max(1, std::min({c->predicted_iters, max_it, kMaxFirstChunk}));
+  const int first = c->params.fixed_iterations > 0
+                        ? std::max(1, std::min(max_it, kMaxFixedChunk))
+                        : std::max(1, std::min({c->predicted_iters, max_it, kMaxFirstChunk}));
   GraphSet* gs = nullptr;
   if (use_graph) {
     gicp_status s = graph_set(c, key, nblocks, &gs);
@@ -902,7 +908,7 @@ gicp_status graph_set(gicp_ctx* c, const std::array<long long, 8>& key, int nblo
     if (s) return s;
     drop_set(*slot);
   }
-  slot->first.resize(kMaxFirstChunk);
+  slot->first.resize(kMaxFixedChunk);
   gicp_status s = capture_chunk(c, false, 1, nblocks, 0, &slot->rest[0]);
   if (!s) s = capture_chunk(c, false, 1, nblocks, 1, &slot->rest[1]);
   if (s) return s;

@@ -160,25 +160,45 @@ __global__ __launch_bounds__(256) void k_key_dir(const unsigned long long* __res
   dir[p] = lo;
 }
 
-// Fine directory: one wavefront per coarse bucket; a bucket of more than
-// kFineMin keys (and fewer than 2^16) takes a slot, and lane f stores the
-// lower bound of refinement f (the next kFineBits Morton bits) relative to
-// the bucket start.  Slot order depends on scheduling, the contents do not.
-__global__ __launch_bounds__(256) void k_key_fine(const unsigned long long* __restrict__ keys, int* __restrict__ dir) {
-  const int c = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-  const int lane = lane_id();
+// Fine directory: a bucket of more than kFineMin keys (and fewer than 2^16)
+// takes a slot, and lane f of the wavefront refining it stores the lower
+// bound of refinement f (the next kFineBits Morton bits) relative to the
+// bucket start.  Two launches: k_key_big (a lane per bucket) assigns the
+// slots and leaves each slot's bucket in the slot's first int; k_key_fine (a
+// wavefront per possible slot) refines.  A wavefront per bucket spent ~30 us
+// per cloud launching 2^18 mostly idle wavefronts.  Slot order depends on
+// scheduling, the contents do not.
+__global__ __launch_bounds__(256) void k_key_big(int* __restrict__ dir) {
+  const int c = (int)blockIdx.x * blockDim.x + (int)threadIdx.x;
   if (c >= (1 << kDirBits)) return;
   int* const ctr = dir + (1 << kDirBits) + 1;
   int* const fslot = ctr + 1;
   unsigned short* const fine = reinterpret_cast<unsigned short*>(fslot + (1 << kDirBits));
-  const int lo = dir[c], hi = dir[c + 1];
-  if (hi - lo <= kFineMin || hi - lo > 65535) {
-    if (lane == 0) fslot[c] = -1;
-    return;
+  const int nk = dir[c + 1] - dir[c];
+  const bool big = nk > kFineMin && nk <= 65535;
+  const unsigned long long m = __ballot(big);
+  int base = 0;
+  if (m) {
+    if (lane_id() == __builtin_ctzll(m)) base = atomicAdd(ctr, __popcll(m));
+    base = __shfl(base, __builtin_ctzll(m));
   }
-  int slot = 0;
-  if (lane == 0) slot = atomicAdd(ctr, 1);
-  slot = __builtin_amdgcn_readfirstlane(slot);
+  int slot = -1;
+  if (big) {
+    slot = base + __popcll(m & ((1ull << lane_id()) - 1));
+    reinterpret_cast<int*>(fine + ((size_t)slot << kFineBits))[0] = c;
+  }
+  fslot[c] = slot;
+}
+
+__global__ __launch_bounds__(256) void k_key_fine(const unsigned long long* __restrict__ keys, int* __restrict__ dir) {
+  const int slot = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const int lane = lane_id();
+  int* const ctr = dir + (1 << kDirBits) + 1;
+  if (slot >= __builtin_amdgcn_readfirstlane(*ctr)) return;
+  int* const fslot = ctr + 1;
+  unsigned short* const fine = reinterpret_cast<unsigned short*>(fslot + (1 << kDirBits));
+  const int c = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(fine + ((size_t)slot << kFineBits))[0]);
+  const int lo = dir[c], hi = dir[c + 1];
   constexpr int sh = 63 - kDirBits - kFineBits;
   const unsigned long long want = ((unsigned long long)c << kFineBits) | (unsigned long long)lane;
   int a = lo, b = hi;
@@ -187,8 +207,8 @@ __global__ __launch_bounds__(256) void k_key_fine(const unsigned long long* __re
     if ((keys[mid] >> sh) < want) a = mid + 1;
     else b = mid;
   }
+  __builtin_amdgcn_wave_barrier();   // every lane has read the slot's bucket id before lanes 0-1 overwrite it
   fine[((size_t)slot << kFineBits) + lane] = (unsigned short)(a - lo);
-  if (lane == 0) fslot[c] = slot;
 }
 
 // Per-leaf SoA copy of the sorted points: leaf l = x[32], y[32], z[32], so
@@ -2977,7 +2997,9 @@ void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, int
 void launch_key_dir(hipStream_t s, const unsigned long long* keys, int n, int* dir) {
   k_key_dir<<<cdiv((1 << kDirBits) + 1, 256), 256, 0, s>>>(keys, n, dir);
   (void)hipMemsetAsync(dir + (1 << kDirBits) + 1, 0, sizeof(int), s);   // fine-slot counter
-  k_key_fine<<<(1 << kDirBits) / 4, 256, 0, s>>>(keys, dir);
+  k_key_big<<<(1 << kDirBits) / 256, 256, 0, s>>>(dir);
+  const long max_slots = (long)n / (kFineMin + 1) + 1;   // (fine_dir_ints)
+  k_key_fine<<<cdiv(max_slots, 4), 256, 0, s>>>(keys, dir);
 }
 void launch_leaf_soa(hipStream_t s, const float4* pts, int npad, float* soa) {
   k_leaf_soa<<<cdiv(npad, 256), 256, 0, s>>>(pts, npad, soa);
