@@ -16,6 +16,7 @@ from dynamic_direct_lidar_odometry_amd import SOURCE, TARGET, scene  # noqa: E40
 prob = scene.s2m_problem(64, 2048, 4, 500000, 3)
 sub = np.ascontiguousarray(np.concatenate(prob["keyframes"])[prob["subset"]])
 c = P.Context(0)
+c.set_target_grid(P.GRID_ON)   # the headline path (candidate cells, built at the first align)
 c.set_params(P.default_params(k_correspondences=10))
 c.set_target(sub)
 c.compute_covariances(TARGET)
