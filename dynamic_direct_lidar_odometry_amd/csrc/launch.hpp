@@ -117,7 +117,7 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
                int* count_host, float crop);
 size_t voxel_tmp_bytes(int n);
 constexpr size_t voxel_scratch_ints(int n) { return 7 * (size_t)n + 16 + 6 * 64; }
-void median_range_async(hipStream_t s, const float4* in, int n, float* d, float* d_sorted, void* tmp, size_t tmp_bytes,
+void median_range_async(hipStream_t s, const float4* in, int n, float* d, float* result, void* tmp, size_t tmp_bytes,
                         float* out);
 size_t median_tmp_bytes(int n);
 void launch_transform4(hipStream_t s, const float4* pts, const int* perm, int n, const float* T12, float4* out);

@@ -131,13 +131,16 @@ __global__ __launch_bounds__(256) void k_voxel_keys(const float4* __restrict__ i
   if (i >= n) return;
   const float4 p = in[i];
   unsigned k = 0xffffffffu;
-  if (voxel_input(p, crop)) {
+  const bool valid = voxel_input(p, crop);
+  if (valid) {
     const int i0 = (int)(floorf(p.x * inv_x) - (float)geo[0]);
     const int i1 = (int)(floorf(p.y * inv_y) - (float)geo[1]);
     const int i2 = (int)(floorf(p.z * inv_z) - (float)geo[2]);
     k = (unsigned)(i0 + i1 * geo[3] + i2 * geo[4]);
-    atomicAdd(nfinite, 1);
   }
+  // one add per wavefront (a per-point add on one word serialised the kernel: ~25 us per scan)
+  const unsigned long long m = __ballot(valid);
+  if (m && __lane_id() == (unsigned)__builtin_ctzll(__ballot(1))) atomicAdd(nfinite, __popcll(m));
   key[i] = k;
   idx[i] = i;
 }
@@ -286,22 +289,108 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   return 0;
 }
 
-// median range: d[n/2] of the sorted ranges, copied to `out` (pinned host
-// memory) in stream order; the caller reads it after waiting on the stream
-void median_range_async(hipStream_t s, const float4* in, int n, float* d, float* d_sorted, void* tmp, size_t tmp_bytes,
+// median range: the element n/2 of the sorted ranges (computeSpaciousness
+// sorts them, odom.cc:981-1001), found by a three-digit radix select on the
+// float bit patterns (non-negative floats order like their bits): 11 + 11 +
+// 10 bits, one histogram pass per digit over the ranges; each pass's blocks
+// first locate the digits chosen so far in the earlier histograms.  Copied
+// to `out` (pinned host memory) in stream order; the caller reads it after
+// waiting on the stream.  (A full radix sort of the ranges took ~30 us.)
+namespace {
+constexpr int kMedBins = 2048;
+constexpr int kMedThreads = 256;
+
+// block-wide: the bin of `hist` (nb bins) holding rank `rank` (0-based) and
+// the rank inside it; every thread returns both
+__device__ void med_find(const unsigned* __restrict__ hist, int nb, unsigned rank, unsigned* sh, unsigned& bin,
+                         unsigned& rin) {
+  const int t = threadIdx.x;
+  const int per = nb / kMedThreads;
+  unsigned local = 0;
+  for (int k = 0; k < per; ++k) local += hist[t * per + k];
+  sh[t] = local;
+  __syncthreads();
+  if (t == 0) {   // 256 partial sums: serial is enough
+    unsigned acc = 0;
+    int tt = 0;
+    while (tt < kMedThreads - 1 && acc + sh[tt] <= rank) acc += sh[tt++];
+    unsigned b = tt * per, a2 = acc;
+    while ((int)b < tt * per + per - 1 && a2 + hist[b] <= rank) a2 += hist[b++];
+    sh[kMedThreads] = b;
+    sh[kMedThreads + 1] = rank - a2;
+  }
+  __syncthreads();
+  bin = sh[kMedThreads];
+  rin = sh[kMedThreads + 1];
+  __syncthreads();
+}
+
+template <int PASS>
+__global__ __launch_bounds__(kMedThreads) void k_med_hist(const float4* __restrict__ in, int n, unsigned* __restrict__ d,
+                                                          unsigned* __restrict__ hist) {
+  __shared__ unsigned lh[kMedBins];
+  __shared__ unsigned sh[kMedThreads + 2];
+  for (int b = threadIdx.x; b < kMedBins; b += kMedThreads) lh[b] = 0;
+  unsigned prefix = 0;
+  if constexpr (PASS >= 1) {
+    unsigned b0, r0;
+    med_find(hist, kMedBins, (unsigned)(n / 2), sh, b0, r0);
+    prefix = b0;
+    if constexpr (PASS == 2) {
+      unsigned b1, r1;
+      med_find(hist + kMedBins, kMedBins, r0, sh, b1, r1);
+      prefix = (b0 << 11) | b1;
+    }
+  }
+  __syncthreads();
+  constexpr int shift = PASS == 0 ? 21 : (PASS == 1 ? 10 : 0);
+  constexpr unsigned dmask = PASS == 2 ? 1023u : 2047u;
+  for (int i = blockIdx.x * kMedThreads + threadIdx.x; i < n; i += gridDim.x * kMedThreads) {
+    unsigned v;
+    if constexpr (PASS == 0) {
+      const float4 p = in[i];
+      const double x = p.x, y = p.y, z = p.z;
+      v = __float_as_uint((float)sqrt((x * x + y * y) + z * z));   // k_ranges' operation order
+      d[i] = v;
+    } else {
+      v = d[i];
+    }
+    const bool take = PASS == 0 ? true : (PASS == 1 ? (v >> 21) == prefix : (v >> 10) == prefix);
+    if (take) atomicAdd(&lh[(v >> shift) & dmask], 1u);
+  }
+  __syncthreads();
+  unsigned* const out = hist + PASS * kMedBins;
+  for (int b = threadIdx.x; b < kMedBins; b += kMedThreads)
+    if (lh[b]) atomicAdd(out + b, lh[b]);
+}
+
+__global__ __launch_bounds__(kMedThreads) void k_med_final(const unsigned* __restrict__ hist, int n,
+                                                           float* __restrict__ result) {
+  __shared__ unsigned sh[kMedThreads + 2];
+  unsigned b0, r0, b1, r1, b2, r2;
+  med_find(hist, kMedBins, (unsigned)(n / 2), sh, b0, r0);
+  med_find(hist + kMedBins, kMedBins, r0, sh, b1, r1);
+  med_find(hist + 2 * kMedBins, 1024, r1, sh, b2, r2);
+  if (threadIdx.x == 0) result[0] = __uint_as_float((b0 << 21) | (b1 << 10) | b2);
+}
+}  // namespace
+
+void median_range_async(hipStream_t s, const float4* in, int n, float* d, float* result, void* tmp, size_t tmp_bytes,
                         float* out) {
-  k_ranges<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, d);
-  size_t t = tmp_bytes;
-  // non-negative floats sort like their bit patterns
-  (void)hipcub::DeviceRadixSort::SortKeys(tmp, t, reinterpret_cast<const unsigned*>(d),
-                                          reinterpret_cast<unsigned*>(d_sorted), n, 0, 32, s);
-  (void)hipMemcpyAsync(out, d_sorted + n / 2, sizeof(float), hipMemcpyDeviceToHost, s);
+  (void)tmp_bytes;   // >= median_tmp_bytes(n)
+  unsigned* const hist = static_cast<unsigned*>(tmp);
+  (void)hipMemsetAsync(hist, 0, sizeof(unsigned) * 3 * kMedBins, s);
+  const int blocks = std::max(1, std::min(cdiv_l(n, kMedThreads * 8), 256));
+  unsigned* const du = reinterpret_cast<unsigned*>(d);
+  k_med_hist<0><<<blocks, kMedThreads, 0, s>>>(in, n, du, hist);
+  k_med_hist<1><<<blocks, kMedThreads, 0, s>>>(in, n, du, hist);
+  k_med_hist<2><<<blocks, kMedThreads, 0, s>>>(in, n, du, hist);
+  k_med_final<<<1, kMedThreads, 0, s>>>(hist, n, result);
+  (void)hipMemcpyAsync(out, result, sizeof(float), hipMemcpyDeviceToHost, s);
 }
 size_t median_tmp_bytes(int n) {
-  size_t a = 0;
-  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, a, (const unsigned*)nullptr, (unsigned*)nullptr, n, 0, 32,
-                                          (hipStream_t)0);
-  return a;
+  (void)n;
+  return sizeof(unsigned) * 3 * kMedBins;
 }
 
 void launch_pack4(hipStream_t s, const unsigned char* raw, size_t stride, int n, float4* out) {
