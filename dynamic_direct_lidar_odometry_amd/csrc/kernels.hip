@@ -1938,6 +1938,7 @@ constexpr int kMomWaves = 8;    // waves per moment block (512 threads: 256 bloc
 // (A last-block-done fusion of k_lm_step into this kernel measured slower:
 // 27.3 us against 9 + 13.5 us — every block's agent-scope release writes
 // back its XCD's L2 before the completion counter.)
+template <bool PREMOM>
 __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, AlignState* __restrict__ st,
                                              const double* __restrict__ slab, int nblocks,
                                              const double* __restrict__ premom);
@@ -2258,7 +2259,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       atomicExch(arrive, 0u);   // re-armed for the next iteration (k_align_init zeroes it per align)
     }
     __syncthreads();
-    lm_step_body(job, job->state, job->slab, job->nblocks, nullptr);
+    lm_step_body<false>(job, job->state, job->slab, job->nblocks, nullptr);
   }
 }
 template __global__ void k_moments<false>(const AlignJob*);
@@ -2293,38 +2294,52 @@ __device__ void so3_exp_d(const double w[3], double R[9]) {  // gicp/so3.hpp:101
   R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
 
-// Eigen::LDLT<Matrix6d>(A).solve(rhs), pivoted (restated, see oracle).
-// Every array index is a compile-time constant (pivot swaps go through
-// select chains), so the 36 entries stay in registers (no scratch).
-__device__ void ldlt_solve6_d(const double* A_in, const double* rhs, double* x) {
+// Eigen::LDLT<Matrix6d>(H + lambda I).solve(rhs) (restated, see oracle).
+// Eigen's pivoted LDLT (ldlt_inplace) is left-looking: step k updates only
+// row / column k, so the diagonal entries k..5 its pivot search reads are
+// still A's own and the transpositions follow from diag(A) alone.  They are
+// found first; the factorization then runs unpivoted on the lower triangle of
+// P A P^T, gathered from LDS — the same operations on the same values as
+// swapping rows and columns in place (checked bit for bit against that form
+// on 2M random, tied and rank-deficient systems), without its select chains.
+// H, b: LDS (H's lower triangle is read, as Eigen's Lower LDLT); rhs = -b;
+// xs: this thread's 6-double LDS row for the un-permuting scatter.  Every
+// register-array index is a compile-time constant (no scratch).
+__device__ void ldlt_solve6_perm(const double* H, const double* b, double lambda, double* xs, double x[6]) {
   constexpr int n = 6;
-  double m[36];
+  double v[6];
+  int p[6];
 #pragma unroll
-  for (int i = 0; i < 36; ++i) m[i] = A_in[i];
-  int tr[6];
+  for (int i = 0; i < n; ++i) {
+    v[i] = fabs(H[7 * i] + lambda);
+    p[i] = i;
+  }
 #pragma unroll
-  for (int k = 0; k < n; ++k) {
-    int big = k;
-    double bigv = fabs(m[k * n + k]);
+  for (int k = 0; k < n - 1; ++k) {
+    // the first largest of v[k..5] (Eigen's maxCoeff keeps the first), swapped to k
+    double bv = v[k];
+    int bp = p[k], big = k;
 #pragma unroll
     for (int i = k + 1; i < n; ++i)
-      if (fabs(m[i * n + i]) > bigv) { bigv = fabs(m[i * n + i]); big = i; }
-    tr[k] = big;
+      if (v[i] > bv) { bv = v[i]; bp = p[i]; big = i; }
 #pragma unroll
-    for (int r = k + 1; r < n; ++r) {
-      if (big == r) {
-        // swap k <-> r on the lower triangle, as Eigen's ldlt_inplace
+    for (int i = k + 1; i < n; ++i)
+      if (big == i) { v[i] = v[k]; p[i] = p[k]; }
+    v[k] = bv;
+    p[k] = bp;
+  }
+  double m[36];
 #pragma unroll
-        for (int j = 0; j < k; ++j) { const double t = m[k * n + j]; m[k * n + j] = m[r * n + j]; m[r * n + j] = t; }
+  for (int i = 0; i < n; ++i)
 #pragma unroll
-        for (int i = r + 1; i < n; ++i) { const double t = m[i * n + k]; m[i * n + k] = m[i * n + r]; m[i * n + r] = t; }
-        { const double t = m[k * n + k]; m[k * n + k] = m[r * n + r]; m[r * n + r] = t; }
-#pragma unroll
-        for (int i = k + 1; i < r; ++i) { const double t = m[i * n + k]; m[i * n + k] = m[r * n + i]; m[r * n + i] = t; }
-      }
+    for (int j = 0; j <= i; ++j) {
+      const int hi = max(p[i], p[j]), lo = min(p[i], p[j]);
+      m[i * n + j] = i == j ? H[7 * p[i]] + lambda : H[hi * n + lo];
     }
-    double temp[6];
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
     if (k > 0) {
+      double temp[6];
 #pragma unroll
       for (int j = 0; j < k; ++j) temp[j] = m[j * n + j] * m[k * n + j];
       double s = 0;
@@ -2347,14 +2362,7 @@ __device__ void ldlt_solve6_d(const double* A_in, const double* rhs, double* x) 
   }
   double y[6];
 #pragma unroll
-  for (int i = 0; i < n; ++i) y[i] = rhs[i];
-  // y = P y (transpositions in order)
-#pragma unroll
-  for (int k = 0; k < n; ++k) {
-#pragma unroll
-    for (int r = k + 1; r < n; ++r)
-      if (tr[k] == r) { const double t = y[k]; y[k] = y[r]; y[r] = t; }
-  }
+  for (int i = 0; i < n; ++i) y[i] = -b[p[i]];   // P rhs
 #pragma unroll
   for (int i = 0; i < n; ++i)
 #pragma unroll
@@ -2366,143 +2374,118 @@ __device__ void ldlt_solve6_d(const double* A_in, const double* rhs, double* x) 
 #pragma unroll
     for (int j = i + 1; j < n; ++j) y[i] -= m[j * n + i] * y[j];
 #pragma unroll
-  for (int k = n - 1; k >= 0; --k) {
+  for (int i = 0; i < n; ++i) xs[p[i]] = y[i];   // P^T y
 #pragma unroll
-    for (int r = k + 1; r < n; ++r)
-      if (tr[k] == r) { const double t = y[k]; y[k] = y[r]; y[r] = t; }
-  }
-#pragma unroll
-  for (int i = 0; i < n; ++i) x[i] = y[i];
+  for (int i = 0; i < n; ++i) x[i] = xs[i];
 }
 
-// Moment accessors.  W(k,l) = sum M qt_k qt_l (qt = [q;1]), G(m,k) = sum (Me)_m qt_k.
-struct Moments {
-  const double* m;
-  __device__ double W(int k, int l, int a, int b) const {  // (a,b) entry of W(k,l)
-    const int ab = a <= b ? (a == 0 ? b : (a == 1 ? 2 + b : 5)) : (b == 0 ? a : (b == 1 ? 2 + a : 5));
-    if (k == 3 && l == 3) return m[ab];
-    if (k == 3) return m[6 + 6 * l + ab];
-    if (l == 3) return m[6 + 6 * k + ab];
-    const int kk = k <= l ? k : l, ll = k <= l ? l : k;
-    const int kl = kk == 0 ? ll : (kk == 1 ? 2 + ll : 5);
-    return m[24 + 6 * kl + ab];
-  }
-  __device__ double G(int mm, int k) const { return m[60 + 4 * mm + k]; }
-  __device__ double y0() const { return m[72]; }
-  __device__ double count() const { return m[73]; }
+// Moment slots.  W(k,l) = sum M qt_k qt_l (qt = [q;1]), G(m,k) = sum (Me)_m qt_k.
+constexpr int mom_ab(int a, int b) {   // symmetric 3 x 3 (a, b) -> 0..5
+  return a <= b ? (a == 0 ? b : (a == 1 ? 2 + b : 5)) : (b == 0 ? a : (b == 1 ? 2 + a : 5));
+}
+constexpr int mom_w(int k, int l, int a, int b) {   // (a, b) entry of W(k, l)
+  return (k == 3 && l == 3) ? mom_ab(a, b)
+         : k == 3           ? 6 + 6 * l + mom_ab(a, b)
+         : l == 3           ? 6 + 6 * k + mom_ab(a, b)
+                            : 24 + 6 * mom_ab(k, l) + mom_ab(a, b);
+}
+constexpr int mom_g(int mm, int k) { return 60 + 4 * mm + k; }
+constexpr int kMomY0 = 72, kMomCount = 73;
+
+// The LM step's inputs from the moments, one entry per thread through a
+// compile-time table of signed moment slots summed in order:
+//   [0, 36)  H = sum J^T M J, [36, 42) b = sum J^T M e, J = [skew(q) | -I]
+//            (nano_gicp_impl.hpp:317-324);
+//   [42, 186) W12[3k + a][3l + b] = W(k,l)[a][b], [186, 198) g12[3k + r] = G(r, k):
+//            the trials' cost decrease y0 - y(delta) = 2 <g12, d> - d^T W12 d over
+//            d = vec([Rd - I | td]) (e' = e - D qt for the frozen correspondences).
+// Column i of the skew generators S_c has two non-zeros S_c[r][i] = +-1,
+// ordered by c, so H_rr(i,j) = sum_{c,d,r,q} S_c[r][i] W(c,d)[r][q] S_d[q][j]
+// is a 4-term signed sum (the same products in the same order as the full one).
+constexpr int kNeqEntries = 198;
+struct NeqTerm {       // packed into three registers: byte t of idx / sgn is term t
+  unsigned idx;        // moment slots
+  unsigned sgn;        // signs: 1 = +1, 0xff = -1
+  unsigned ctl;        // bits 0-7: term count, bit 8: negate the sum
 };
-
-// skew generator: skew(q) = sum_c q_c S_c, S_c[r][s]
-__device__ __forceinline__ double Sgen(int c, int r, int s) {
-  // S_0 = [[0,0,0],[0,0,-1],[0,1,0]], S_1 = [[0,0,1],[0,0,0],[-1,0,0]], S_2 = [[0,-1,0],[1,0,0],[0,0,0]]
-  if (c == 0) return (r == 1 && s == 2) ? -1.0 : ((r == 2 && s == 1) ? 1.0 : 0.0);
-  if (c == 1) return (r == 0 && s == 2) ? 1.0 : ((r == 2 && s == 0) ? -1.0 : 0.0);
-  return (r == 0 && s == 1) ? -1.0 : ((r == 1 && s == 0) ? 1.0 : 0.0);
-}
-
-// H = sum J^T M J, b = sum J^T M e with J = [skew(q) | -I] (nano_gicp_impl.hpp:317-324),
-// one entry per thread: e in [0,36) -> H(e/6, e%6), e in [36,42) -> b(e-36).
-// Column i of the generators S_c has exactly two non-zeros S_c[r][i] = +-1:
-// (c, r, sign) = kSk[i][0..1], ordered by c, so the 4-term sums below add
-// the same products in the same order as the full sum over (c, d, r, q).
-__device__ __forceinline__ void skew_nz(int i, int p, int& c, int& r, double& sg) {
+struct NeqTable {
+  NeqTerm e[kNeqEntries];
+};
+constexpr void skew_nz_c(int i, int p, int& c, int& r, int& sg) {
   // i=0: S_1[2][0]=-1, S_2[1][0]=+1; i=1: S_0[2][1]=+1, S_2[0][1]=-1; i=2: S_0[1][2]=-1, S_1[0][2]=+1
-  const int cc[3][2] = {{1, 2}, {0, 2}, {0, 1}};
-  const int rr[3][2] = {{2, 1}, {2, 0}, {1, 0}};
-  const double ss[3][2] = {{-1.0, 1.0}, {1.0, -1.0}, {-1.0, 1.0}};
-  c = i == 0 ? cc[0][p] : i == 1 ? cc[1][p] : cc[2][p];
-  r = i == 0 ? rr[0][p] : i == 1 ? rr[1][p] : rr[2][p];
-  sg = i == 0 ? ss[0][p] : i == 1 ? ss[1][p] : ss[2][p];
+  constexpr int cc[3][2] = {{1, 2}, {0, 2}, {0, 1}};
+  constexpr int rr[3][2] = {{2, 1}, {2, 0}, {1, 0}};
+  constexpr int ss[3][2] = {{-1, 1}, {1, -1}, {-1, 1}};
+  c = cc[i][p];
+  r = rr[i][p];
+  sg = ss[i][p];
 }
-__device__ double normal_eq_entry(const Moments& mo, int e) {
-  if (e >= 36) {
-    const int i = e - 36;
-    if (i >= 3) return -mo.G(i - 3, 3);  // b_t = -G(:,3)
-    double s = 0.0;                      // b_r(i) = sum_c sum_r S_c[r][i] G(r,c)
-    for (int p = 0; p < 2; ++p) {
-      int c, r;
-      double sg;
-      skew_nz(i, p, c, r, sg);
-      s += sg * mo.G(r, c);
-    }
-    return s;
-  }
-  const int i = e / 6, j = e % 6;
-  if (i < 3 && j < 3) {  // H_rr(i,j) = sum_{c,d} sum_{r,q} S_c[r][i] W(c,d)[r][q] S_d[q][j]
-    double s = 0.0;
-    for (int p = 0; p < 2; ++p) {
-      int c, r;
-      double sr;
-      skew_nz(i, p, c, r, sr);
-      for (int u = 0; u < 2; ++u) {
-        int d, q;
-        double sq;
-        skew_nz(j, u, d, q, sq);
-        s += sr * mo.W(c, d, r, q) * sq;
+constexpr NeqTable make_neq_table() {
+  NeqTable T{};
+  auto add = [&](int e, int idx, int sg) {
+    const unsigned t = T.e[e].ctl & 0xffu;
+    T.e[e].idx |= (unsigned)idx << (8 * t);
+    T.e[e].sgn |= (sg < 0 ? 0xffu : 1u) << (8 * t);
+    T.e[e].ctl += 1u;
+  };
+  for (int e = 0; e < 42; ++e) {
+    if (e >= 36) {
+      const int i = e - 36;
+      if (i >= 3) {
+        add(e, mom_g(i - 3, 3), -1);   // b_t = -G(:,3)
+      } else {                         // b_r(i) = sum_c sum_r S_c[r][i] G(r,c)
+        for (int p = 0; p < 2; ++p) {
+          int c = 0, r = 0, sg = 0;
+          skew_nz_c(i, p, c, r, sg);
+          add(e, mom_g(r, c), sg);
+        }
       }
+      continue;
     }
-    return s;
-  }
-  if (i >= 3 && j >= 3) return mo.W(3, 3, i - 3, j - 3);  // H_tt = sum M
-  // H_rt(a, t) = -sum_c sum_r S_c[r][a] W(c,3)[r][t]
-  const int a = i < 3 ? i : j, t = i < 3 ? j - 3 : i - 3;
-  double s = 0.0;
-  for (int p = 0; p < 2; ++p) {
-    int c, r;
-    double sr;
-    skew_nz(a, p, c, r, sr);
-    s += sr * mo.W(c, 3, r, t);
-  }
-  return -s;
-}
-
-// The quadratic form of cost_decrease as a 12 x 12 matrix over d = vec(D)
-// (d[3k + a] = D[a][k]): W12[3k + a][3l + b] = W(k,l)[a][b], g12[3k + r] =
-// G(r, k); built once per LM step by 156 threads, so that the trials' cost
-// decreases are 12-term row products spread over 12 threads per trial (the
-// same products as cost_decrease, summed row by row).
-__device__ __forceinline__ double w12_entry(const Moments& mo, int e) {
-  const int r = e / 12, c = e % 12;
-  return mo.W(r / 3, c / 3, r % 3, c % 3);
-}
-// y0 - y(delta) for the frozen correspondences/M of the last linearize:
-// e' = e - D qt, D = [Rd - I | td]  =>  y0 - y = 2 <D, G> - sum_kl D_k^T W(k,l) D_l
-__device__ double cost_decrease(const Moments& mo, const double Rd[9], const double td[3]) {
-  double D[3][4];
-  for (int r = 0; r < 3; ++r) {
-    for (int c = 0; c < 3; ++c) D[r][c] = Rd[3 * r + c] - (r == c ? 1.0 : 0.0);
-    D[r][3] = td[r];
-  }
-  double lin = 0.0;
-  for (int r = 0; r < 3; ++r)
-    for (int k = 0; k < 4; ++k) lin += D[r][k] * mo.G(r, k);
-  double quad = 0.0;
-  for (int k = 0; k < 4; ++k)
-    for (int l = 0; l < 4; ++l)
-      for (int a = 0; a < 3; ++a) {
-        double s = 0.0;
-        for (int b2 = 0; b2 < 3; ++b2) s += mo.W(k, l, a, b2) * D[b2][l];
-        quad += D[a][k] * s;
+    const int i = e / 6, j = e % 6;
+    if (i < 3 && j < 3) {
+      for (int p = 0; p < 2; ++p) {
+        int c = 0, r = 0, sr = 0;
+        skew_nz_c(i, p, c, r, sr);
+        for (int u = 0; u < 2; ++u) {
+          int d = 0, q = 0, sq = 0;
+          skew_nz_c(j, u, d, q, sq);
+          add(e, mom_w(c, d, r, q), sr * sq);
+        }
       }
-  return 2.0 * lin - quad;
-}
-
-__device__ bool is_converged_d(const AlignJob* job, const double Rd[9], const double td[3]) {
-  if (job->fixed_iterations > 0) return false;
-  double m = 0.0;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) m = fmax(m, fabs(Rd[3 * i + j] - (i == j ? 1.0 : 0.0)) / job->rotation_epsilon);
-  for (int i = 0; i < 3; ++i) m = fmax(m, fabs(td[i]) / job->transformation_epsilon);
-  return m < 1;
-}
-
-__device__ void compose(const double Rd[9], const double td[3], const double R[9], const double t[3], double Ro[9],
-                        double to[3]) {
-  for (int i = 0; i < 3; ++i) {
-    for (int j = 0; j < 3; ++j)
-      Ro[3 * i + j] = Rd[3 * i + 0] * R[0 + j] + Rd[3 * i + 1] * R[3 + j] + Rd[3 * i + 2] * R[6 + j];
-    to[i] = (Rd[3 * i + 0] * t[0] + Rd[3 * i + 1] * t[1] + Rd[3 * i + 2] * t[2]) + td[i];
+    } else if (i >= 3 && j >= 3) {
+      add(e, mom_w(3, 3, i - 3, j - 3), 1);   // H_tt = sum M
+    } else {   // H_rt(a, t) = -sum_c sum_r S_c[r][a] W(c,3)[r][t]
+      const int a = i < 3 ? i : j, t = i < 3 ? j - 3 : i - 3;
+      for (int p = 0; p < 2; ++p) {
+        int c = 0, r = 0, sr = 0;
+        skew_nz_c(a, p, c, r, sr);
+        add(e, mom_w(c, 3, r, t), sr);
+      }
+      T.e[e].ctl |= 0x100u;
+    }
   }
+  for (int e = 0; e < 144; ++e) add(42 + e, mom_w(e / 12 / 3, e % 12 / 3, e / 12 % 3, e % 12 % 3), 1);
+  for (int e = 0; e < 12; ++e) add(186 + e, mom_g(e % 3, e / 3), 1);
+  return T;
+}
+__constant__ NeqTable kNeq = make_neq_table();
+// One table entry: a single slot is taken as is (times +-1, exact); a sum
+// starts from 0.0 and adds its terms in order (as the loops it restates).
+__device__ __forceinline__ double neq_term(const NeqTerm& E, const double* mom, int t) {
+  const double v = mom[(E.idx >> (8 * t)) & 0xffu];
+  return ((E.sgn >> (8 * t)) & 0xffu) == 1u ? v : -v;
+}
+__device__ __forceinline__ double neq_value(const NeqTerm& E, const double* mom) {
+  const unsigned n = E.ctl & 0xffu;
+  double s = neq_term(E, mom, 0);
+  if (n > 1) {
+    s = 0.0 + s;
+#pragma unroll
+    for (int t = 1; t < 4; ++t)
+      if (t < (int)n) s += neq_term(E, mom, t);
+  }
+  return (E.ctl & 0x100u) ? -s : s;
 }
 
 constexpr int kLmThreads = 512;
@@ -2515,22 +2498,25 @@ constexpr int kLmRowsPerPart = (kMomBlocksMax + kLmParts - 1) / kLmParts;  // sl
 // mom[kSlabStride] by one workgroup: thread (p, v2) sums column pair v2 of
 // rows p, p + 12, ... with 16-byte loads (kLmParts x 40 threads), then 80
 // threads add the 12 partials in order (fixed order => deterministic).
+// mom is complete after the caller's next barrier.
 __device__ __forceinline__ void reduce_slab(const double* slab_in, int nb, double (*part)[kSlabStride], double* mom) {
   const int tid = threadIdx.x;
   const auto slab = (const __attribute__((address_space(1))) d2v*)gp(slab_in);
   constexpr int kPairs = kSlabStride / 2;
   if (tid < kLmParts * kPairs) {
-    // unconditional (clamped) loads, summed in row order; fully unrolled, so
-    // the loads are all issued before the in-order adds consume them (no
-    // private array: it would go to scratch)
+    // unconditional (clamped) loads into registers, all issued before the
+    // in-order adds consume them (one memory latency, not one per batch the
+    // scheduler would otherwise interleave with the adds)
     const int v2 = tid % kPairs, p = tid / kPairs;
+    d2v x[kLmRowsPerPart];
+#pragma unroll
+    for (int r = 0; r < kLmRowsPerPart; ++r) x[r] = slab[(size_t)min(p + kLmParts * r, nb - 1) * kPairs + v2];
     double s0 = 0.0, s1 = 0.0;
 #pragma unroll
     for (int r = 0; r < kLmRowsPerPart; ++r) {
-      const int b = p + kLmParts * r;
-      const d2v x = slab[(size_t)min(b, nb - 1) * kPairs + v2];
-      s0 += b < nb ? x.x : 0.0;
-      s1 += b < nb ? x.y : 0.0;
+      const bool in = p + kLmParts * r < nb;
+      s0 += in ? x[r].x : 0.0;
+      s1 += in ? x[r].y : 0.0;
     }
     part[p][2 * v2] = s0;
     part[p][2 * v2 + 1] = s1;
@@ -2542,7 +2528,6 @@ __device__ __forceinline__ void reduce_slab(const double* slab_in, int nb, doubl
     for (int p = 0; p < kLmParts; ++p) s += part[p][tid];
     mom[tid] = s;
   }
-  __syncthreads();
 }
 
 // K5a (sharded align only): this rank's reduced moments -> job->mom, which
@@ -2553,25 +2538,28 @@ __global__ __launch_bounds__(kLmThreads) void k_mom_reduce(const AlignJob* __res
   __shared__ double part[kLmParts][kSlabStride];
   __shared__ double mom[kSlabStride];
   reduce_slab(job->slab, job->nblocks, part, mom);
+  __syncthreads();
   if (threadIdx.x < kSlabStride) gpw(job->mom)[threadIdx.x] = mom[threadIdx.x];
 }
 
 // One workgroup: (1) fixed-order reduction of the linearize partials,
-// (2) H and b one entry per thread, (3) every LM trial in its own thread —
-// the reference's trial sequence is fully determined up front (lambda_i =
-// nu_{i-1} lambda_{i-1}, nu doubling: lsq_registration_impl.hpp:187-223), so
-// trial i is evaluated with exactly the lambda the sequential loop would use,
-// (4) thread 0 replays the sequential accept/reject decisions, (5) the new
-// state is stored by many threads.  Every state word is loaded at the start
-// (its latency hides behind the slab loads).
+// (2) H, b and the cost-decrease form one entry per thread, (3) every LM
+// trial in its own thread — the reference's trial sequence is fully
+// determined up front (lambda_i = nu_{i-1} lambda_{i-1}, nu doubling:
+// lsq_registration_impl.hpp:187-223), so trial i is evaluated with exactly
+// the lambda the sequential loop would use, (4) wavefront 0 takes the
+// sequential accept/reject decisions as one ballot and stores the new state
+// while the other wavefronts store the per-linearize record.  Every state
+// and job word is loaded at the start (its latency hides behind the slab).
 #ifdef DDLO_LM_PROF   // developer build (make lmprof): per-phase cycle counts of one LM step, printed by thread 0
 #define LM_PROF(i) if (threadIdx.x == 0) lm_t[i] = __builtin_amdgcn_s_memtime()
 #else
 #define LM_PROF(i)
 #endif
 // st, slab, nblocks: job->state, job->slab, job->nblocks, passed as kernel
-// arguments so the slab loads need no job load first; premom: the moments
-// already reduced (and summed across shards: job->mom), else nullptr.
+// arguments so the slab loads need no job load first; premom (PREMOM): the
+// moments already reduced (and summed across shards: job->mom).
+template <bool PREMOM>
 __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, AlignState* __restrict__ st,
                                              const double* __restrict__ slab, int nblocks,
                                              const double* __restrict__ premom) {
@@ -2581,15 +2569,16 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
   LM_PROF(0);
   __shared__ double part[kLmParts][kSlabStride];
   __shared__ double mom[kSlabStride];
-  __shared__ double Hs[36], bs[6];
-  __shared__ double W12[144], g12[12];
-  __shared__ double tr_rho[kMaxTrials], tr_lambda[kMaxTrials], tr_cm[kMaxTrials], tr_fro[kMaxTrials];
+  __shared__ double nq[kNeqEntries];   // H (36), b (6), W12 (144), g12 (12)
+  double* const Hs = nq;
+  double* const bs = nq + 36;
+  double* const W12 = nq + 42;
+  double* const g12 = nq + 186;
+  __shared__ double tr_lambda[kMaxTrials], tr_cm[kMaxTrials], tr_fro[kMaxTrials];
   __shared__ double tr_R[kMaxTrials][9], tr_t[kMaxTrials][3];
-  __shared__ double tr_d[kMaxTrials][12], tr_row[kMaxTrials][12], tr_den[kMaxTrials];
+  __shared__ double tr_d[kMaxTrials][12], tr_row[kMaxTrials][12], tr_den[kMaxTrials], tr_x[kMaxTrials][6];
   __shared__ double Rt_s[12];
   __shared__ int tr_conv[kMaxTrials];
-  __shared__ int dec_s[2];   // chosen trial, accept
-  __shared__ double lambda0_s;
   const int tid = threadIdx.x;
   // state words, loaded before the slab (their latency overlaps it)
   const int it_pre = st->iter;
@@ -2597,47 +2586,31 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
   const int rec_pre = st->rec;
   const float src_radius = st->src_radius;
   const double lambda_pre = st->lambda;
-  if (tid < 12) Rt_s[tid] = tid < 9 ? st->R[tid] : st->t[tid - 9];
-  // job words too (scalar-cache misses at their first use would each stall a phase)
+  // the pose, held in a register until the slab loads are issued (an LDS
+  // store here would wait for it first)
+  double rt_v = 0.0;
+  if (tid < 12) rt_v = tid < 9 ? st->R[tid] : st->t[tid - 9];
+  // job words and this thread's table entry too (misses at their first use would each stall a phase)
   const int optimizer = job->optimizer, lm_max_iterations = job->lm_max_iterations;
   const int fixed_iterations = job->fixed_iterations, max_iterations = job->max_iterations;
   const double lm_init_lambda_factor = job->lm_init_lambda_factor;
   const double rotation_epsilon = job->rotation_epsilon, transformation_epsilon = job->transformation_epsilon;
   const int reuse = job->reuse;
   const float reuse_rec_eps = job->reuse_rec_eps, reuse_rec_conv = job->reuse_rec_conv;
-  if (premom) {  // moments already reduced (and summed across shards)
+  NeqTerm E{};
+  if (tid < kNeqEntries) E = kNeq.e[tid];
+  if constexpr (PREMOM) {  // moments already reduced (and summed across shards)
     if (tid < kSlabStride) mom[tid] = gp(premom)[tid];
-    __syncthreads();
   } else {
-    reduce_slab(slab, nblocks, part, mom);   // ends with a barrier: Rt_s is visible too
+    reduce_slab(slab, nblocks, part, mom);
   }
-  LM_PROF(1);
-  const Moments mo{mom};
-  if (tid < 42) {
-    const double v = normal_eq_entry(mo, tid);
-    if (tid < 36)
-      Hs[tid] = v;
-    else
-      bs[tid - 36] = v;
-  } else if (tid >= 64 && tid < 64 + 144) {
-    W12[tid - 64] = w12_entry(mo, tid - 64);
-  } else if (tid >= 256 && tid < 256 + 12) {
-    const int e = tid - 256;
-    g12[e] = mo.G(e % 3, e / 3);
-  }
+  if (tid < 12) Rt_s[tid] = rt_v;
   __syncthreads();
-  const bool lm = optimizer != 0;
-  if (lm && tid == 0) {
-    double lambda = lambda_pre;
-    if (lambda < 0.0) {
-      double mx = 0.0;
-      for (int e = 0; e < 6; ++e) mx = fmax(mx, fabs(Hs[7 * e]));
-      lambda = lm_init_lambda_factor * mx;
-    }
-    lambda0_s = lambda;
-  }
+  LM_PROF(1);
+  if (tid < kNeqEntries) nq[tid] = neq_value(E, mom);
   __syncthreads();
   LM_PROF(2);
+  const bool lm = optimizer != 0;
   const int ntr = lm ? min(lm_max_iterations, kMaxTrials) : 1;
   // one trial per thread (one wavefront issues them all: a trial per
   // wavefront with wave-uniform pivots measured 2x slower, the waves then
@@ -2646,19 +2619,20 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
     const int trial = tid;
     double lambda = 0.0;
     if (lm) {
-      lambda = lambda0_s;
+      lambda = lambda_pre;
+      if (lambda < 0.0) {   // the first LM step: lm_init_lambda_factor * max |diag H| (:180-183)
+        double mx = 0.0;
+        for (int e = 0; e < 6; ++e) mx = fmax(mx, fabs(Hs[7 * e]));
+        lambda = lm_init_lambda_factor * mx;
+      }
       double nu = 2.0;
       for (int k = 0; k < trial; ++k) {
         lambda = nu * lambda;
         nu = 2 * nu;
       }
     }
-    double A[36], nb6[6], d[6];
-    for (int e = 0; e < 36; ++e) A[e] = Hs[e];
-    if (lm)
-      for (int e = 0; e < 6; ++e) A[7 * e] += lambda;
-    for (int e = 0; e < 6; ++e) nb6[e] = -bs[e];
-    ldlt_solve6_d(A, nb6, d);
+    double d[6];
+    ldlt_solve6_perm(Hs, bs, lambda, tr_x[trial], d);   // GN: lambda 0 (H + 0 = H)
     double Rd[9], td[3];
     so3_exp_d(d, Rd);
     td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
@@ -2666,11 +2640,14 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
     for (int e = 0; e < 6; ++e) den += d[e] * (lambda * d[e] - bs[e]);
     tr_den[trial] = den;
     tr_lambda[trial] = lambda;
-    // is_converged's measure max(|Rd - I| / rot_eps, |td| / trans_eps) (lsq_registration_impl.hpp:128-139)
-    double cm = 0.0;
+    // is_converged's measure max((1 / rot_eps) |Rd - I|, (1 / trans_eps) |td|)
+    // (lsq_registration_impl.hpp:128-139); the product rounds monotonically,
+    // so scaling each largest |x| gives the same maximum
+    double mr = 0.0, mt = 0.0;
     for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) cm = fmax(cm, fabs(Rd[3 * i + j] - (i == j ? 1.0 : 0.0)) / rotation_epsilon);
-    for (int i = 0; i < 3; ++i) cm = fmax(cm, fabs(td[i]) / transformation_epsilon);
+      for (int j = 0; j < 3; ++j) mr = fmax(mr, fabs(Rd[3 * i + j] - (i == j ? 1.0 : 0.0)));
+    for (int i = 0; i < 3; ++i) mt = fmax(mt, fabs(td[i]));
+    const double cm = fmax(1.0 / rotation_epsilon * mr, 1.0 / transformation_epsilon * mt);
     tr_cm[trial] = cm;
     tr_conv[trial] = fixed_iterations <= 0 && cm < 1;
     double fro = 0.0;
@@ -2681,7 +2658,7 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
     tr_fro[trial] = fro;
     for (int e = 0; e < 9; ++e) tr_R[trial][e] = Rd[e];
     for (int e = 0; e < 3; ++e) tr_t[trial][e] = td[e];
-    // d = vec([Rd - I | td]), d[3k + a] = D[a][k] (cost_decrease)
+    // d = vec([Rd - I | td]), d[3k + a] = D[a][k]
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -2689,8 +2666,7 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
   }
   __syncthreads();
   LM_PROF(3);
-  // trial cost decrease y0 - y(delta) = 2 <g, d> - d^T W d (cost_decrease),
-  // one row of the quadratic form per thread: (trial, row) = (x / 12, x % 12)
+  // trial cost decrease, one row of the quadratic form per thread: (trial, row) = (x / 12, x % 12)
   for (int x = tid; lm && x < 12 * ntr; x += (int)blockDim.x) {
     const int tr = x / 12, i = x % 12;
     double srow = 0.0;
@@ -2699,58 +2675,43 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
     tr_row[tr][i] = tr_d[tr][i] * srow;
   }
   __syncthreads();
-  if (tid < ntr) {
-    double rho = 1.0;
-    if (lm) {
-      double lin = 0.0, quad = 0.0;
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) lin += tr_d[tid][3 * k + r] * g12[3 * k + r];
-#pragma unroll
-      for (int i = 0; i < 12; ++i) quad += tr_row[tid][i];
-      rho = (2.0 * lin - quad) / tr_den[tid];
-    }
-    tr_rho[tid] = rho;
-  }
-  __syncthreads();
-  // the per-linearize record, stored by many threads at once
-  if (tid < kSlabStride) st->last_mom[tid] = mom[tid];
-  else if (tid < kSlabStride + 9) st->last_lin_R[tid - kSlabStride] = Rt_s[tid - kSlabStride];
-  else if (tid < kSlabStride + 12) st->last_lin_t[tid - kSlabStride - 9] = Rt_s[tid - kSlabStride];
-  else if (tid < kSlabStride + 18) st->last_b[tid - kSlabStride - 12] = bs[tid - kSlabStride - 12];
   LM_PROF(4);
-  // the sequential decisions (thread 0)
-  if (tid == 0) {
-    const int it = it_pre;
-    st->nr_iterations = it;
-    st->final_cost = mo.y0();
-    st->num_corr = (int)mo.count();
-    bool ok = false;
-    int chosen = -1;
-    bool accept = false;
-    if (!lm) {  // step_gn: always take the step (lsq_registration_impl.hpp:155-173)
-      ok = true;
-      chosen = 0;
-      accept = true;
-    } else {    // step_lm decisions (:188-231)
-      for (int i = 0; i < ntr; ++i) {
-        if (tr_rho[i] < 0) {
-          if (tr_conv[i]) {
-            ok = true;
-            chosen = i;
-            break;
-          }
-          continue;
-        }
-        ok = true;
-        accept = true;
-        chosen = i;
-        break;
-      }
+  if (tid >= 64) {
+    // the per-linearize record, stored by the other wavefronts while wavefront 0 decides
+    const int u = tid - 64;
+    if (u < kSlabStride) st->last_mom[u] = mom[u];
+    else if (u < kSlabStride + 9) st->last_lin_R[u - kSlabStride] = Rt_s[u - kSlabStride];
+    else if (u < kSlabStride + 12) st->last_lin_t[u - kSlabStride - 9] = Rt_s[u - kSlabStride];
+    else if (u < kSlabStride + 18) st->last_b[u - kSlabStride - 12] = bs[u - kSlabStride - 12];
+    return;
+  }
+  // wavefront 0: the trials' gain ratios, then step_lm's sequential decisions
+  // (:188-231) as one ballot — the first trial that is accepted (rho >= 0, or
+  // NaN) or, rejected, has converged; step_gn always takes its step (:155-173)
+  const int lane = tid;
+  double rho = 1.0;
+  if (lm && lane < ntr) {
+    double lin = 0.0, quad = 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lin += tr_d[lane][3 * k + r] * g12[3 * k + r];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) quad += tr_row[lane][i];
+    rho = (2.0 * lin - quad) / tr_den[lane];
+  }
+  bool ok = true, accept = true;
+  int chosen = 0;
+  if (lm) {
+    const unsigned long long ball = __ballot(lane < ntr && (!(rho < 0) || tr_conv[lane]));
+    ok = ball != 0ull;
+    chosen = ok ? (int)__builtin_ctzll(ball) : ntr - 1;
+    const double rho_c = __shfl(rho, chosen);
+    accept = ok && !(rho_c < 0);
+    if (lane == 0) {
       st->lm_trials = trials_pre + (ok ? chosen + 1 : ntr);
       if (accept) {
-        const double c = 2 * tr_rho[chosen] - 1;
+        const double c = 2 * rho_c - 1;
         st->lambda = tr_lambda[chosen] * fmax(1.0 / 3.0, 1 - c * c * c);
       } else if (ok) {
         st->lambda = tr_lambda[chosen];
@@ -2758,8 +2719,13 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
         st->lambda = tr_lambda[ntr - 1] * 2.0;  // not observable: the align ends
       }
     }
+  }
+  if (lane == 0) {
+    st->nr_iterations = it_pre;
+    st->final_cost = mom[kMomY0];
+    st->num_corr = (int)mom[kMomCount];
     if (rec_pre) st->any_rec = 1;   // this iteration's search recorded references
-    st->iter = it + 1;
+    st->iter = it_pre + 1;
     st->have_prev = 1;
     int done = 0;
     if (!ok) {
@@ -2769,50 +2735,41 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
       st->converged = 1;
       done = 1;
     }
-    if (it + 1 >= max_iterations) done = 1;
+    if (it_pre + 1 >= max_iterations) done = 1;
     if (done) st->done = 1;
-    dec_s[0] = chosen;
-    dec_s[1] = accept ? 1 : 0;
   }
-  __syncthreads();
-  const int chosen = dec_s[0];
-  if (dec_s[1]) {   // accepted: x0 = delta * x0 (compose, lsq_registration_impl.hpp:193-197,225-228)
-    if (tid < 12) {   // one entry of (Rn | tn) per thread, compose()'s arithmetic
-      const double* Rd = tr_R[chosen];
-      const int i = tid < 9 ? tid / 3 : tid - 9;
-      double v;
-      if (tid < 9) {
-        const int j = tid % 3;
-        v = Rd[3 * i + 0] * Rt_s[0 + j] + Rd[3 * i + 1] * Rt_s[3 + j] + Rd[3 * i + 2] * Rt_s[6 + j];
-        st->R[tid] = v;
-      } else {
-        v = (Rd[3 * i + 0] * Rt_s[9] + Rd[3 * i + 1] * Rt_s[10] + Rd[3 * i + 2] * Rt_s[11]) + tr_t[chosen][i];
-        st->t[i] = v;
-        part[0][i] = v;   // tn for the reuse-recording test below
-      }
-    } else if (tid >= 64 && tid < 64 + 36) {
-      st->final_hessian[tid - 64] = Hs[tid - 64];
+  // accepted: x0 = delta * x0 (compose, lsq_registration_impl.hpp:193-197,225-228),
+  // one entry of (Rn | tn) per lane
+  double v = 0.0;
+  if (accept) {
+    const double* Rd = tr_R[chosen];
+    if (lane < 9) {
+      const int i = lane / 3, j = lane % 3;
+      v = Rd[3 * i + 0] * Rt_s[0 + j] + Rd[3 * i + 1] * Rt_s[3 + j] + Rd[3 * i + 2] * Rt_s[6 + j];
+      st->R[lane] = v;
+    } else if (lane < 12) {
+      const int i = lane - 9;
+      v = (Rd[3 * i + 0] * Rt_s[9] + Rd[3 * i + 1] * Rt_s[10] + Rd[3 * i + 2] * Rt_s[11]) + tr_t[chosen][i];
+      st->t[i] = v;
+    } else if (lane >= 16 && lane < 16 + 36) {
+      st->final_hessian[lane - 16] = Hs[lane - 16];
     }
   }
-  __syncthreads();
-  if (tid == 0) {
-    int rec = reuse;
-    if (dec_s[1]) {
-      // how far the step moved a source point: |dR q + dt - q| <= |dR - I|_F |q| + |dt|,
-      // |q| <= src_radius + |t|; the next search records references only
-      // after a small step (the one after it is expected to be smaller) ...
-      const double* tn = part[0];
-      const double* dt = tr_t[chosen];
-      const double mv = sqrt(tr_fro[chosen]) * ((double)src_radius + sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2])) +
-                        sqrt(dt[0] * dt[0] + dt[1] * dt[1] + dt[2] * dt[2]);
-      // ... and, with the reference's convergence test on, only while the step
-      // is still far from converging (is_converged's measure > reuse_rec_conv):
-      // references pay off only if two more iterations follow
-      rec = rec && mv < (double)reuse_rec_eps &&
-            (fixed_iterations > 0 || tr_cm[chosen] > (double)reuse_rec_conv);
-    }
-    st->rec = rec;
+  int rec = reuse;
+  if (accept) {
+    // how far the step moved a source point: |dR q + dt - q| <= |dR - I|_F |q| + |dt|,
+    // |q| <= src_radius + |t|; the next search records references only
+    // after a small step (the one after it is expected to be smaller) ...
+    const double tn0 = __shfl(v, 9), tn1 = __shfl(v, 10), tn2 = __shfl(v, 11);
+    const double* dt = tr_t[chosen];
+    const double mv = sqrt(tr_fro[chosen]) * ((double)src_radius + sqrt(tn0 * tn0 + tn1 * tn1 + tn2 * tn2)) +
+                      sqrt(dt[0] * dt[0] + dt[1] * dt[1] + dt[2] * dt[2]);
+    // ... and, with the reference's convergence test on, only while the step
+    // is still far from converging (is_converged's measure > reuse_rec_conv):
+    // references pay off only if two more iterations follow
+    rec = rec && mv < (double)reuse_rec_eps && (fixed_iterations > 0 || tr_cm[chosen] > (double)reuse_rec_conv);
   }
+  if (lane == 0) st->rec = rec;
   LM_PROF(5);
 #ifdef DDLO_LM_PROF
   if (tid == 0)
@@ -2828,7 +2785,10 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
                                                         const double* __restrict__ slab, int nblocks,
                                                         const double* __restrict__ premom,
                                                         AlignState* __restrict__ publish) {
-  if (!__builtin_amdgcn_readfirstlane(st->done)) lm_step_body(job, st, slab, nblocks, premom);
+  if (!__builtin_amdgcn_readfirstlane(st->done)) {
+    if (premom) lm_step_body<true>(job, st, slab, nblocks, premom);
+    else lm_step_body<false>(job, st, slab, nblocks, nullptr);
+  }
   if (publish) {
     static_assert(sizeof(AlignState) % 16 == 0, "AlignState is copied in 16-byte words");
     __threadfence();   // this block's state stores, then an L1 invalidate before they are read back

@@ -755,11 +755,13 @@ struct Gicp {
 
   bool is_converged(const Iso& delta) const {  // lsq_registration_impl.hpp:128-139
     if (p.fixed_iterations > 0) return false;
-    double m = 0.0;
+    // (1 / eps) * |x| per entry, then the max (:135-138); the product rounds
+    // monotonically, so scaling the largest |x| gives the same maximum
+    double mr = 0.0, mt = 0.0;
     for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) m = std::max(m, std::fabs(delta.R[3 * i + j] - (i == j ? 1.0 : 0.0)) / p.rotation_epsilon);
-    for (int i = 0; i < 3; ++i) m = std::max(m, std::fabs(delta.t[i]) / p.transformation_epsilon);
-    return m < 1;
+      for (int j = 0; j < 3; ++j) mr = std::max(mr, std::fabs(delta.R[3 * i + j] - (i == j ? 1.0 : 0.0)));
+    for (int i = 0; i < 3; ++i) mt = std::max(mt, std::fabs(delta.t[i]));
+    return std::max(1.0 / p.rotation_epsilon * mr, 1.0 / p.transformation_epsilon * mt) < 1;
   }
 
   static Iso make_delta(const double* d) {
