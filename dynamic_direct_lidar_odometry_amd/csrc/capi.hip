@@ -622,6 +622,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
 int linearize_blocks(int nsrc) { return linearize_geometry(nsrc, 0).mom_blocks; }   // slab rows
 LinGeom geometry(const gicp_ctx* c) {
   LinGeom g = linearize_geometry(c->src.cloud->n, c->tgt.cloud->upper_count());
+  g.state = c->state_dev.as<AlignState>();
   g.fuse_lm = !c->comm && lm_fusion_enabled();   // a sharded align all-reduces between the moments and the LM step
   g.grid = grid_active(c);
   g.grid_walk = !g.grid || c->tgt.cloud->grid->dev.has_fallback != 0;

@@ -2004,10 +2004,44 @@ __device__ __forceinline__ void resolve_tied_corr(const AlignJob* __restrict__ j
 // lookup of k_cell_lookup is done here, one query per lane, and the match's
 // coordinates come from its list entry -- no lookup kernel, no key / sec
 // round trip.  Same keys, ties and moments as k_cell_lookup + k_moments.
+// Fused lookup: list entries loaded per round (clamped loads, no branch).
+// 16 measured 2-4 % faster on cfg 3 than 8 (the waves are 2 per SIMD, so the
+// registers are free); 12, 32, exec-masked loads, two rounds in flight (8 or
+// 12 per round) and a flat wavefront-wide scan of all 64 lists (LDS atomic
+// min per owner) all slower: the lookup is bound by the memory system's
+// throughput of scattered lines, not by the rounds' latency
+// (tools/mom_timeline.py; -DDDLO_LOOKUP_U for A/B builds).
+#ifndef DDLO_LOOKUP_U
+#define DDLO_LOOKUP_U 16
+#endif
+constexpr int kLookupU = DDLO_LOOKUP_U;
+
+// developer build (-DDDLO_MOM_PROF): a wave timeline of the fused-lookup
+// moment kernel, s_memrealtime stamps (100 MHz, one clock for the device)
+// printed by every 16th wavefront
+#ifdef DDLO_MOM_PROF
+#define MOM_PROF(i) if (LOOKUP) mp_t[i] = __builtin_amdgcn_s_memrealtime()
+constexpr int kMomProfIters = 8, kMomProfWaves = 2048;
+__device__ unsigned long long g_mom_prof[kMomProfIters * kMomProfWaves * 6];   // [iteration][wave][stamp]
+#else
+#define MOM_PROF(i)
+#endif
 template <bool FUSE_LM, bool LOOKUP = false>
-__global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __restrict__ job) {
-  AlignState* st = job->state;
-  if (__builtin_amdgcn_readfirstlane(st->done)) return;
+__global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __restrict__ job,
+                                                            AlignState* __restrict__ st) {
+#ifdef DDLO_MOM_PROF
+  unsigned long long mp_t[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  MOM_PROF(0);
+  // st (= job->state) is a kernel argument and the pose is loaded with the
+  // done flag, before the test: the state words are one load from the
+  // arguments, not three dependent ones (job -> state -> done -> pose)
+  const auto sg = gp(st);
+  double R[9], t[3];
+  for (int e = 0; e < 9; ++e) R[e] = sg->R[e];
+  for (int e = 0; e < 3; ++e) t[e] = sg->t[e];
+  const int st_rec = sg->rec, st_any_rec = sg->any_rec;
+  if (__builtin_amdgcn_readfirstlane(sg->done)) return;
   const CloudDev src = job->src;
   const CloudDev tgt = job->tgt;
   const auto src_cov = gp(job->src_cov);
@@ -2017,17 +2051,18 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
   const auto sqd = gpw(job->sqd);
   const auto slab = gpw(job->slab);
   const double max_corr2 = job->max_corr2;
-  const int rec = st->rec;   // this iteration records reuse references
-  const int first_rec_done = st->any_rec;   // an earlier iteration of this align recorded
+  const int rec = st_rec;   // this iteration records reuse references
+  const int first_rec_done = st_any_rec;   // an earlier iteration of this align recorded
   const int tie_detect = job->tie_detect;
   const bool slice_check = tie_detect && job->tie_scan >= 2 && !(job->tie_ab & 4);
   const bool tie3m = tie_detect && job->tie_scan == 3 && !rec;   // the mirrored key of a non-recording search
   __shared__ NfWaveStack tie_stk[kMomWaves];   // nanoflann search frames of a tied query (per wave)
-  double R[9], t[3];
-  for (int e = 0; e < 9; ++e) R[e] = st->R[e];
-  for (int e = 0; e < 3; ++e) t[e] = st->t[e];
   const int lane = lane_id();
   const int wib = threadIdx.x >> 6;
+#ifdef DDLO_MOM_PROF
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
+  MOM_PROF(1);
   const int wave = blockIdx.x * kMomWaves + wib;
   const int nwaves_total = gridDim.x * kMomWaves;
   const int ngroups = (src.n + 63) >> 6;
@@ -2081,11 +2116,8 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       unsigned long long bk = ~0ull;
       float d2 = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
       const bool track2 = tie_detect;   // the second distance only feeds the tie test
-      constexpr int kU = 8;   // loads in flight
-      for (unsigned k = 0; k < cnt; k += kU) {
-        float4 pp[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) pp[u] = ldg4(G.ent, off + min(k + u, cnt - 1));
+      constexpr int kU = kLookupU;   // loads in flight
+      auto consume = [&](const float4 (&pp)[kU], unsigned k) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
           if (k + u < cnt) {
@@ -2102,11 +2134,22 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
             }
           }
         }
+      };
+      auto fetch = [&](float4 (&pp)[kU], unsigned k) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) pp[u] = ldg4(G.ent, off + min(k + u, cnt - 1));
+      };
+      for (unsigned k = 0; k < cnt; k += kU) {
+        float4 pp[kU];
+        fetch(pp, k);
+        consume(pp, k);
       }
       lkey = owned ? umin64(bk, dkey(job->cap2, -1)) : dkey(INFINITY, -1);
       const float lkd = __uint_as_float((unsigned)(lkey >> 32));
       lsec = (owned && (unsigned)lkey != 0xffffffffu && d2 == lkd) ? (unsigned)(lkey >> 32) : 0xffffffffu;
       b = make_float4(bx, by, bz, 0.f);
+
+      MOM_PROF(2);
     }
     if (active) {
       const unsigned long long k = LOOKUP ? lkey : key[i];
@@ -2121,6 +2164,7 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
           a = ldg4(src.pts, i);
           b = ldg4(tgt.pts, j);
         }
+
         load_sym6(src_cov + 6 * (size_t)i, ca);
         load_sym6(tgt_cov + 6 * (size_t)j, cb);
       }
@@ -2222,10 +2266,12 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     }
     C.qq[0] = C.q[0] * C.q[0]; C.qq[1] = C.q[0] * C.q[1]; C.qq[2] = C.q[0] * C.q[2];
     C.qq[3] = C.q[1] * C.q[1]; C.qq[4] = C.q[1] * C.q[2]; C.qq[5] = C.q[2] * C.q[2];
+    MOM_PROF(3);
     acc0 += final_pair(treduce<5, 0>(C));
     acc1 += final_pair(treduce<5, 1>(C));
     acc2 += final_pair(treduce<5, 2>(C));
   }
+  MOM_PROF(4);
   __shared__ double red[kMomWaves][kMomentSlots];
   if ((lane & 1) == 0) {
     const int base = moment_base(lane);
@@ -2245,6 +2291,13 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     else
       slab[(size_t)blockIdx.x * kSlabStride + threadIdx.x] = sum;
   }
+#ifdef DDLO_MOM_PROF
+  MOM_PROF(5);
+  if (LOOKUP && lane == 0 && wave < kMomProfWaves) {
+    unsigned long long* o = g_mom_prof + ((size_t)min(st->iter, kMomProfIters - 1) * kMomProfWaves + wave) * 6;
+    for (int e = 0; e < 6; ++e) o[e] = mp_t[e];
+  }
+#endif
   if constexpr (FUSE_LM) {
     __shared__ int last_s;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its sc1 slab stores are done
@@ -2259,13 +2312,13 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
       atomicExch(arrive, 0u);   // re-armed for the next iteration (k_align_init zeroes it per align)
     }
     __syncthreads();
-    lm_step_body<false>(job, job->state, job->slab, job->nblocks, nullptr);
+    lm_step_body<false>(job, st, job->slab, job->nblocks, nullptr);
   }
 }
-template __global__ void k_moments<false>(const AlignJob*);
-template __global__ void k_moments<true>(const AlignJob*);
-template __global__ void k_moments<false, true>(const AlignJob*);
-template __global__ void k_moments<true, true>(const AlignJob*);
+template __global__ void k_moments<false>(const AlignJob*, AlignState*);
+template __global__ void k_moments<true>(const AlignJob*, AlignState*);
+template __global__ void k_moments<false, true>(const AlignJob*, AlignState*);
+template __global__ void k_moments<true, true>(const AlignJob*, AlignState*);
 
 // ---------------------------------------------------------------------------
 // K5: slab reduction + LM/GN step on one workgroup.
@@ -2553,8 +2606,10 @@ __global__ __launch_bounds__(kLmThreads) void k_mom_reduce(const AlignJob* __res
 // and job word is loaded at the start (its latency hides behind the slab).
 #ifdef DDLO_LM_PROF   // developer build (make lmprof): per-phase cycle counts of one LM step, printed by thread 0
 #define LM_PROF(i) if (threadIdx.x == 0) lm_t[i] = __builtin_amdgcn_s_memtime()
+#define LM_PROF_TRIAL(i) if (threadIdx.x == 0) lm_tt[i] = __builtin_amdgcn_s_memtime()
 #else
 #define LM_PROF(i)
+#define LM_PROF_TRIAL(i)
 #endif
 // st, slab, nblocks: job->state, job->slab, job->nblocks, passed as kernel
 // arguments so the slab loads need no job load first; premom (PREMOM): the
@@ -2564,7 +2619,7 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
                                              const double* __restrict__ slab, int nblocks,
                                              const double* __restrict__ premom) {
 #ifdef DDLO_LM_PROF
-  unsigned long long lm_t[6];
+  unsigned long long lm_t[6], lm_tt[4] = {0, 0, 0, 0};
 #endif
   LM_PROF(0);
   __shared__ double part[kLmParts][kSlabStride];
@@ -2631,10 +2686,13 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
         nu = 2 * nu;
       }
     }
+    LM_PROF_TRIAL(0);
     double d[6];
     ldlt_solve6_perm(Hs, bs, lambda, tr_x[trial], d);   // GN: lambda 0 (H + 0 = H)
+    LM_PROF_TRIAL(1);
     double Rd[9], td[3];
     so3_exp_d(d, Rd);
+    LM_PROF_TRIAL(2);
     td[0] = d[3]; td[1] = d[4]; td[2] = d[5];
     double den = 0.0;
     for (int e = 0; e < 6; ++e) den += d[e] * (lambda * d[e] - bs[e]);
@@ -2663,6 +2721,7 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int a = 0; a < 3; ++a) tr_d[trial][3 * k + a] = k < 3 ? Rd[3 * a + k] - (a == k ? 1.0 : 0.0) : td[a];
+    LM_PROF_TRIAL(3);
   }
   __syncthreads();
   LM_PROF(3);
@@ -2773,8 +2832,9 @@ __device__ __forceinline__ void lm_step_body(const AlignJob* __restrict__ job, A
   LM_PROF(5);
 #ifdef DDLO_LM_PROF
   if (tid == 0)
-    printf("lm_prof %d %llu %llu %llu %llu %llu\n", it_pre, lm_t[1] - lm_t[0], lm_t[2] - lm_t[1], lm_t[3] - lm_t[2],
-           lm_t[4] - lm_t[3], lm_t[5] - lm_t[4]);
+    printf("lm_prof %d %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", it_pre, lm_t[1] - lm_t[0], lm_t[2] - lm_t[1],
+           lm_t[3] - lm_t[2], lm_t[4] - lm_t[3], lm_t[5] - lm_t[4], lm_tt[0] - lm_t[2], lm_tt[1] - lm_tt[0],
+           lm_tt[2] - lm_tt[1], lm_tt[3] - lm_tt[2]);
 #endif
 }
 
@@ -3057,8 +3117,8 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
   static const int fused_lookup = env_knob("DDLO_GRID_FUSED", 1);   // 0: separate lookup kernel (A/B)
   if (g.grid && !g.grid_walk && fused_lookup) {
     // every query is answered by its cell: the lookup runs inside the moment kernel
-    if (g.fuse_lm) k_moments<true, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
-    else k_moments<false, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
+    if (g.fuse_lm) k_moments<true, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state);
+    else k_moments<false, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state);
     return;
   }
   if (g.grid) k_cell_lookup<<<g.lookup_blocks, 256, 0, s>>>(job);
@@ -3091,8 +3151,8 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
     else if (occ_scan == 5) k_nn_scan<5, 6><<<scan_blocks, 64 * kScanWaves, 0, s>>>(job);   // 6-task batches: 7.5 KB LDS per wave
     else k_nn_scan<4><<<scan_blocks, 64 * kScanWaves, 0, s>>>(job);
   }
-  if (g.fuse_lm) k_moments<true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
-  else k_moments<false><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job);
+  if (g.fuse_lm) k_moments<true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state);
+  else k_moments<false><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state);
 }
 int search_queries_per_wave() { return kSearchQ; }
 int task_cap_per_region(int nsrc) {
@@ -3126,3 +3186,10 @@ void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr,
 }
 
 }  // namespace ddlo
+
+#ifdef DDLO_MOM_PROF
+// developer build: the fused moment kernel's wave stamps of the last align, [iteration][wave][6]
+extern "C" int ddlo_dev_mom_prof(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ddlo::g_mom_prof), sizeof(ddlo::g_mom_prof));
+}
+#endif

@@ -54,6 +54,7 @@ void launch_align_init(hipStream_t s, AlignJob* job, const AlignJob* job_src);
 struct LinGeom {
   int seed_blocks, collect_blocks, scan_blocks, mom_blocks, lds_boxes, lookup_blocks;
   bool fuse_lm = false;   // the LM step runs in the moment kernel's last block (no k_lm_step launch)
+  AlignState* state = nullptr;   // the job's state (job->state), a kernel argument of the moment kernel
   bool grid = false;      // the target's candidate cells answer the search first (k_cell_lookup)
   bool grid_walk = true;  // ... and some of its cells have no list: the walk kernel follows the lookup
 };

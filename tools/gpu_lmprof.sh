@@ -8,5 +8,6 @@ import numpy as np
 rows=[list(map(int,l.split()[1:])) for l in open('gpurun_out/lmprof.log') if l.startswith('lm_prof')]
 a=np.array(rows)
 print(len(a), 'steps; median cycles per phase (reduce, H/b/W12 table, trials, cost rows, wave-0 decisions + state):')
-print(np.median(a[:,1:],axis=0), 'total', np.median(a[:,1:].sum(1)))
+print(np.median(a[:,1:6],axis=0), 'total', np.median(a[:,1:6].sum(1)))
+print('trial 0 (lambda, LDLT solve, so3 exp, measures + stores):', np.median(a[:,6:10],axis=0))
 PY
