@@ -2545,6 +2545,7 @@ constexpr int kLmThreads = 512;
 constexpr int kMaxTrials = 64;
 constexpr int kMomBlocksMax = 256;                      // moment-kernel blocks (slab rows)
 constexpr int kLmParts = 12;                                          // slab row partitions
+// (1024 threads, 25 partitions of 11 rows: reduction 5.5k -> 5.8k cycles, no gain)
 constexpr int kLmRowsPerPart = (kMomBlocksMax + kLmParts - 1) / kLmParts;  // slab rows per reducer thread
 
 // Fixed-order reduction of the linearize slab (nblocks x kSlabStride) into
