@@ -48,13 +48,12 @@ __global__ __launch_bounds__(256) void k_pack_bbox(const unsigned char* __restri
     x = p[0];
     y = p[1];
     z = p[2];
-    ok = true;
-    if (!(isfinite(x) && isfinite(y) && isfinite(z))) {
-      atomicOr(nonfinite, 1);
-      ok = false;
-    }
+    ok = isfinite(x) && isfinite(y) && isfinite(z);
     out[i] = make_float4(x, y, z, __int_as_float(i));
   }
+  // one flag write per wavefront holding a non-finite point (one word takes ~88 atomics per us)
+  const unsigned long long bad = __ballot(i < n && !ok);
+  if (bad && __lane_id() == (unsigned)__builtin_ctzll(bad)) atomicOr(nonfinite, 1);
   __shared__ float red[6][4];
   float v[6] = {ok ? x : INFINITY, ok ? y : INFINITY, ok ? z : INFINITY,
                 ok ? x : -INFINITY, ok ? y : -INFINITY, ok ? z : -INFINITY};

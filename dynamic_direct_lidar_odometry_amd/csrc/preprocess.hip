@@ -125,8 +125,7 @@ __global__ void k_voxel_geometry(const float* __restrict__ part, int nparts, flo
 // sort last, they are dropped by the caller's count).
 __global__ __launch_bounds__(256) void k_voxel_keys(const float4* __restrict__ in, int n, float inv_x, float inv_y,
                                                     float inv_z, float crop, const int* __restrict__ geo,
-                                                    unsigned* __restrict__ key, int* __restrict__ idx,
-                                                    int* __restrict__ nfinite) {
+                                                    unsigned* __restrict__ key, int* __restrict__ idx) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 p = in[i];
@@ -138,11 +137,19 @@ __global__ __launch_bounds__(256) void k_voxel_keys(const float4* __restrict__ i
     const int i2 = (int)(floorf(p.z * inv_z) - (float)geo[2]);
     k = (unsigned)(i0 + i1 * geo[3] + i2 * geo[4]);
   }
-  // one add per wavefront (a per-point add on one word serialised the kernel: ~25 us per scan)
-  const unsigned long long m = __ballot(valid);
-  if (m && __lane_id() == (unsigned)__builtin_ctzll(__ballot(1))) atomicAdd(nfinite, __popcll(m));
   key[i] = k;
   idx[i] = i;
+}
+
+// Whether any point left the voxel pass (non-finite or cropped): their keys
+// (UINT_MAX) sort last and form the last run.  small[9] = n - 1 if so, else
+// n.  (Counting the valid points with atomics on one word serialised the key
+// kernel: ~25 us per scan per point, still ~23 us with one add per wavefront.)
+__global__ void k_voxel_tail(const unsigned* __restrict__ uniq, int n, int* __restrict__ small) {
+  if (threadIdx.x == 0) {
+    const int nr = small[8];
+    small[9] = (nr > 0 && uniq[nr - 1] == 0xffffffffu) ? n - 1 : n;
+  }
 }
 
 // Centroid of each run of equal voxel index: float sums in input order
@@ -255,7 +262,7 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   unsigned* uniq = reinterpret_cast<unsigned*>(order + n);
   int* counts = reinterpret_cast<int*>(uniq + n);
   int* offsets = counts + n;
-  int* small = offsets + n;   // [0..6] geometry, [8] nruns, [9] nfinite
+  int* small = offsets + n;   // [0..6] geometry, [8] nruns, [9] < n: some point left the pass
   float* part = reinterpret_cast<float*>(small + 16);
   // inverse_leaf_size_ = 1 / leaf_size_ (float)
   const float inv = 1.0f / leaf;
@@ -263,13 +270,14 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   (void)hipMemsetAsync(small, 0, 16 * sizeof(int), s);
   k_minmax_partial<<<nparts, 256, 0, s>>>(in, n, crop, part);
   k_voxel_geometry<<<1, 64, 0, s>>>(part, nparts, inv, inv, inv, small);
-  k_voxel_keys<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, inv, inv, inv, crop, small, keys, idx, small + 9);
+  k_voxel_keys<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, inv, inv, inv, crop, small, keys, idx);
   size_t need = voxel_tmp_bytes(n);
   if (need > tmp_bytes) return -2;
   size_t t = tmp_bytes;
   (void)hipcub::DeviceRadixSort::SortPairs(tmp, t, keys, keys_sorted, idx, order, n, 0, 32, s);
   t = tmp_bytes;
   (void)hipcub::DeviceRunLengthEncode::Encode(tmp, t, keys_sorted, uniq, counts, small + 8, n, s);
+  k_voxel_tail<<<1, 64, 0, s>>>(uniq, n, small);
   t = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, t, counts, offsets, n, s);
   int h[16];
@@ -301,23 +309,45 @@ constexpr int kMedBins = 2048;
 constexpr int kMedThreads = 256;
 
 // block-wide: the bin of `hist` (nb bins) holding rank `rank` (0-based) and
-// the rank inside it; every thread returns both
+// the rank inside it; every thread returns both.  Each thread sums `per`
+// consecutive bins, a block scan of those sums (wavefront shuffles + the four
+// wavefront totals) finds the one thread whose range holds the rank, and that
+// thread walks its own bins (a serial walk of the 256 sums by one thread cost
+// ~7 us per call in the odometry chain's trace).
 __device__ void med_find(const unsigned* __restrict__ hist, int nb, unsigned rank, unsigned* sh, unsigned& bin,
                          unsigned& rin) {
   const int t = threadIdx.x;
-  const int per = nb / kMedThreads;
+  const int per = nb / kMedThreads;   // 8 or 4
+  unsigned h[8];
   unsigned local = 0;
-  for (int k = 0; k < per; ++k) local += hist[t * per + k];
-  sh[t] = local;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    h[k] = k < per ? hist[t * per + k] : 0u;
+    local += h[k];
+  }
+  const int lane = t & 63, w = t >> 6;
+  unsigned incl = local;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned v = __shfl_up(incl, d);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) sh[w] = incl;
   __syncthreads();
-  if (t == 0) {   // 256 partial sums: serial is enough
-    unsigned acc = 0;
-    int tt = 0;
-    while (tt < kMedThreads - 1 && acc + sh[tt] <= rank) acc += sh[tt++];
-    unsigned b = tt * per, a2 = acc;
-    while ((int)b < tt * per + per - 1 && a2 + hist[b] <= rank) a2 += hist[b++];
-    sh[kMedThreads] = b;
-    sh[kMedThreads + 1] = rank - a2;
+  for (int k = 0; k < w; ++k) incl += sh[k];
+  const unsigned excl = incl - local;
+  if (excl <= rank && rank < incl) {   // exactly one thread (rank < the total)
+    unsigned a = excl;
+    int b = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (b == k && k < per - 1 && a + h[k] <= rank) {
+        a += h[k];
+        b = k + 1;
+      }
+    }
+    sh[kMedThreads] = (unsigned)(t * per + b);
+    sh[kMedThreads + 1] = rank - a;
   }
   __syncthreads();
   bin = sh[kMedThreads];
