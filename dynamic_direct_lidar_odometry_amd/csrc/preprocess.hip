@@ -95,11 +95,12 @@ __global__ __launch_bounds__(256) void k_minmax_partial(const float4* __restrict
 // (1, div_b.x, div_b.x * div_b.y); geo[0..2] = min_b, geo[3..4] = divb_mul
 // y/z, geo[5] = 1 if the grid overflows an int index (the reference then
 // returns the input unchanged), geo[6] = 1 if there is no finite point.
-__global__ void k_voxel_geometry(const float* __restrict__ part, int nparts, float inv_x, float inv_y, float inv_z,
-                                 int* __restrict__ geo) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// From the 64 partial boxes (min / max are exact in any order); every block
+// of the key kernel derives it itself (no single-thread geometry launch).
+constexpr int kVoxParts = 64;
+__device__ void voxel_geometry(const float* __restrict__ part, float inv_x, float inv_y, float inv_z, int* geo) {
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (int b = 0; b < nparts; ++b)
+  for (int b = 0; b < kVoxParts; ++b)
     for (int a = 0; a < 3; ++a) {
       mn[a] = fminf(mn[a], part[b * 6 + a]);
       mx[a] = fmaxf(mx[a], part[b * 6 + 3 + a]);
@@ -124,14 +125,27 @@ __global__ void k_voxel_geometry(const float* __restrict__ part, int nparts, flo
 // Voxel index of every point (non-finite or cropped points get UINT_MAX and
 // sort last, they are dropped by the caller's count).
 __global__ __launch_bounds__(256) void k_voxel_keys(const float4* __restrict__ in, int n, float inv_x, float inv_y,
-                                                    float inv_z, float crop, const int* __restrict__ geo,
-                                                    unsigned* __restrict__ key, int* __restrict__ idx) {
+                                                    float inv_z, float crop, const float* __restrict__ part,
+                                                    int* __restrict__ small, unsigned* __restrict__ key,
+                                                    int* __restrict__ idx) {
+  __shared__ float sp[kVoxParts * 6];
+  __shared__ int geo[7];
+  for (int e = threadIdx.x; e < kVoxParts * 6; e += blockDim.x) sp[e] = part[e];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    geo[5] = 0;
+    voxel_geometry(sp, inv_x, inv_y, inv_z, geo);
+    if (blockIdx.x == 0) {   // the flags the host reads
+      small[6] = geo[6];
+      small[5] = geo[6] ? 0 : geo[5];
+    }
+  }
+  __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 p = in[i];
   unsigned k = 0xffffffffu;
-  const bool valid = voxel_input(p, crop);
-  if (valid) {
+  if (voxel_input(p, crop)) {   // (no such point when geo[6]: the geometry is not read)
     const int i0 = (int)(floorf(p.x * inv_x) - (float)geo[0]);
     const int i1 = (int)(floorf(p.y * inv_y) - (float)geo[1]);
     const int i2 = (int)(floorf(p.z * inv_z) - (float)geo[2]);
@@ -266,11 +280,9 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   float* part = reinterpret_cast<float*>(small + 16);
   // inverse_leaf_size_ = 1 / leaf_size_ (float)
   const float inv = 1.0f / leaf;
-  const int nparts = 64;
   (void)hipMemsetAsync(small, 0, 16 * sizeof(int), s);
-  k_minmax_partial<<<nparts, 256, 0, s>>>(in, n, crop, part);
-  k_voxel_geometry<<<1, 64, 0, s>>>(part, nparts, inv, inv, inv, small);
-  k_voxel_keys<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, inv, inv, inv, crop, small, keys, idx);
+  k_minmax_partial<<<kVoxParts, 256, 0, s>>>(in, n, crop, part);
+  k_voxel_keys<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, inv, inv, inv, crop, part, small, keys, idx);
   size_t need = voxel_tmp_bytes(n);
   if (need > tmp_bytes) return -2;
   size_t t = tmp_bytes;
