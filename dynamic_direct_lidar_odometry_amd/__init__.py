@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes as C
 import math
 import os
+import sys
 
 import numpy as np
 
@@ -94,6 +95,8 @@ class GicpGridInfo(C.Structure):
         ("fallback_fine", C.c_int64),
         ("entries", C.c_int64),
         ("uses_walk", C.c_int64),
+        ("build_status", C.c_int64),
+        ("scratch_bytes", C.c_int64),
     ]
 
     def as_dict(self):
@@ -123,11 +126,16 @@ def load():
     # process.  Loading this library (ROCm's) first and torch afterwards (e.g.
     # torch.distributed for the shard ranks' unique id) leaves torch's other
     # bundled libraries on ROCm's runtime, and the process aborts in its exit
-    # teardown.  So torch, when installed, loads first.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # teardown.  So torch, when installed, loads first (then the library runs
+    # on torch's bundled HIP runtime).  A process that never imports torch can
+    # set DDLO_TORCH_FIRST=0 to skip that import: the library then binds to
+    # the ROCm runtime it was linked against (its RUNPATH, /opt/rocm), as a C++
+    # host does (tests/test_gpu_process.py).
+    if "torch" not in sys.modules and os.environ.get("DDLO_TORCH_FIRST", "1") != "0":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = C.CDLL(path)
     P, S, I, D = C.c_void_p, C.c_size_t, C.c_int, C.c_double
     sig = {

@@ -283,6 +283,12 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   // scratch
   const long nbx = (dims[0] + 3) / 4, nby = (dims[1] + 3) / 4, nbz = (dims[2] + 3) / 4;
   const long nblocked = nbx * nby * nbz * 64;
+  {   // the per-cell scratch and directory (~21 B per coarse cell) must fit in free device memory with room
+      // for the lists; otherwise the build is not attempted (the walk answers: maybe_build_grid)
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && (size_t)ncells * 21 + ((size_t)256 << 20) > fr)
+      return fail(GICP_ENOMEM, "candidate cells: not enough free device memory for the build");
+  }
   DevBuf rep, rep_tmp, flags, ctr, band, dnum, cub_tmp, cnn, db_buf;
   HIP_TRY(rep.ensure(sizeof(int) * (size_t)ncells));
   HIP_TRY(rep_tmp.ensure(sizeof(int) * (size_t)ncells));
@@ -456,6 +462,14 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   g->info.fine_cells = (int64_t)fine_base[4] - g->info.fallback_fine;
   g->info.entries = ent_base[4];
   g->info.bytes = (int64_t)(g->dir.bytes + g->fine.bytes + g->ent.bytes);
+  {   // the build's transient scratch at its peak (released on return)
+    size_t sb = rep.bytes + rep_tmp.bytes + flags.bytes + ctr.bytes + band.bytes + dnum.bytes + cub_tmp.bytes +
+                cnn.bytes + db_buf.bytes + fl_final.bytes + fl_next.bytes;
+    for (int l = 0; l <= kCgMaxLevel; ++l)
+      sb += hdr[l].bytes + pool[l].bytes + cmax[l].bytes + sband[l].bytes + sparent[l].bytes + fin_sel[l].bytes +
+            ent_n[l].bytes + fine_n[l].bytes;
+    g->info.scratch_bytes = (int64_t)sb;
+  }
   g->info.built = 1;
   CellGridDev& d = g->dev;
   d.dir = g->dir.as<unsigned long long>();
@@ -476,7 +490,8 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
 }
 
 // gicp_set_target_grid policy: build the target's candidate cells for this
-// ctx's bound (auto: at the second align against the same target and bound)
+// ctx's bound (auto: at the kGridAutoAligns-th (32nd) align against the same
+// target and bound)
 gicp_status maybe_build_grid(gicp_ctx* c) {
   if (!c->grid_mode || !c->tgt.cloud) return GICP_OK;
   CloudData& t = *c->tgt.cloud;
@@ -493,7 +508,21 @@ gicp_status maybe_build_grid(gicp_ctx* c) {
   if (c->grid_mode == GICP_GRID_AUTO && t.grid_aligns < kGridAutoAligns) return GICP_OK;
   std::shared_ptr<CellGridData> g;
   const gicp_status s = cellgrid_build(c, t, cap2, &g);
-  if (s) return s;
+  if (s) {
+    // The cells are an optional speed-up: a build that fails (pool or table
+    // limits, the byte budget, device memory) leaves this target on the walk
+    // for this bound and is not retried.  Only a device fault (the stream no
+    // longer synchronizes) is the align's error.
+    g.reset();   // its partial buffers are released (nothing queued reads them)
+    (void)hipGetLastError();
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return s;
+    auto none = std::make_shared<CellGridData>();
+    none->cap2 = cap2;
+    none->info.build_status = s;
+    t.grid = none;
+    g_last_error.clear();
+    return GICP_OK;
+  }
   t.grid = g;
   return GICP_OK;
 }
@@ -501,6 +530,21 @@ gicp_status maybe_build_grid(gicp_ctx* c) {
 // Just before k_align_init reads the pinned job: whole (job_full = 1) unless
 // only the guess changed since the job it last copied whole, whose device copy
 // is still in place (k_align_init alone writes the device job).
+// finalize_job records the job as the device's copy before anything is
+// launched; an error return before the launch has happened must forget it,
+// or the next align would send only its guess to a device job that never
+// received this one (JobCommit: armed after finalize_job, done() once the
+// launch succeeded).
+struct JobCommit {
+  gicp_ctx* c;
+  bool ok = false;
+  explicit JobCommit(gicp_ctx* ctx) : c(ctx) {}
+  void done() { ok = true; }
+  ~JobCommit() {
+    if (!ok) c->job_last_valid = false;
+  }
+};
+
 void finalize_job(gicp_ctx* c) {
   AlignJob& j = *c->job_host;
   j.job_full = 0;
@@ -1234,6 +1278,7 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
     s = fill_job(c, guess16, nblocks);
     if (s) return s;
     finalize_job(c);
+    JobCommit commit(c);
     const int max_it = c->job_host->max_iterations;
     end_ev = c->ev1;
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
@@ -1241,6 +1286,8 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
       s = max_it > 0 ? run_align_eager_profiled(c, max_it, nblocks) : GICP_OK;
       if (s) return s;
       if (max_it <= 0) launch_align_init(c->stream, c->job_dev.as<AlignJob>(), c->job_host_dev);
+      HIP_TRY(hipGetLastError());
+      commit.done();
       HIP_TRY(hipEventRecord(c->ev1, c->stream));
       HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1250,6 +1297,7 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
       int fc = 0;
       s = run_align_graph(c, max_it, nblocks, &fc);
       if (s) return s;
+      commit.done();
       // chunk fc's end-of-chunk copy already put the final state in its
       // slot; the (at most one) speculative no-op chunk still queued writes
       // the other slot and does not delay the return
@@ -1434,11 +1482,13 @@ gicp_status gicp_linearize(gicp_ctx* c, const double* pose16, double* H36, doubl
     c->job_host->max_iterations = 1;
     c->job_host->fixed_iterations = 1;
     finalize_job(c);
+    JobCommit commit(c);
     AlignJob* jd = c->job_dev.as<AlignJob>();
     launch_align_init(c->stream, jd, c->job_host_dev);
     s = enqueue_iteration(c, jd, nblocks, nullptr);
     if (s) return s;
     HIP_TRY(hipGetLastError());
+    commit.done();
     HIP_TRY(hipMemcpyAsync(c->state_host, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->state_slot = 0;
@@ -1965,8 +2015,13 @@ gicp_status gicp_set_tie_trees_from_root(gicp_ctx* c, int root, const void* cons
   if (!c->comm) return fail(GICP_ESTATE, "no communicator (gicp_set_comm)");
   if (root < 0 || root >= c->nranks) return fail(GICP_EINVAL, "root out of range");
   const int R = c->nranks, me = c->rank;
-  if (me == root && (!blobs || !sizes)) return fail(GICP_EINVAL, "the root passes every rank's blob");
-  if (R == 1) return gicp_set_tie_tree(c, blobs[0], sizes[0]);   // nothing to send
+  // A root without blobs (its builder failed) still enters the collective and
+  // broadcasts a failure word, so no rank waits forever on the broadcast.
+  const bool root_failed = me == root && (!blobs || !sizes);
+  if (R == 1) {
+    if (root_failed) return fail(GICP_EINVAL, "the root passes every rank's blob");
+    return gicp_set_tie_tree(c, blobs[0], sizes[0]);   // nothing to send
+  }
   const Rccl& r = rccl();
   if (!r.ok || !r.broadcast || !r.send || !r.recv || !r.group_start || !r.group_end)
     return fail(GICP_ECOMM, "RCCL point-to-point entry points missing");
@@ -1974,16 +2029,22 @@ gicp_status gicp_set_tie_trees_from_root(gicp_ctx* c, int root, const void* cons
   if (s) return s;
   s = drain_tail(c);
   if (s) return s;
-  // every rank's blob size (one broadcast), then root -> rank point-to-point
+  // every rank's blob size and the root's status word (one broadcast), then
+  // root -> rank point-to-point
   DevBuf dsz;
-  HIP_TRY(dsz.ensure(sizeof(unsigned long long) * (size_t)R));
-  std::vector<unsigned long long> sz((size_t)R, 0);
-  if (me == root)
-    for (int k = 0; k < R; ++k) sz[(size_t)k] = sizes[k];
-  HIP_TRY(hipMemcpyAsync(dsz.p, sz.data(), sizeof(unsigned long long) * R, hipMemcpyHostToDevice, c->stream));
-  NCCL_TRY(r.broadcast(dsz.p, dsz.p, (size_t)R, ncclUint64, root, c->comm, c->stream));
-  HIP_TRY(hipMemcpyAsync(sz.data(), dsz.p, sizeof(unsigned long long) * R, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(dsz.ensure(sizeof(unsigned long long) * ((size_t)R + 1)));
+  std::vector<unsigned long long> sz((size_t)R + 1, 0);
+  if (me == root) {
+    if (root_failed) sz[(size_t)R] = 1;
+    else
+      for (int k = 0; k < R; ++k) sz[(size_t)k] = sizes[k];
+  }
+  HIP_TRY(hipMemcpyAsync(dsz.p, sz.data(), sizeof(unsigned long long) * (R + 1), hipMemcpyHostToDevice, c->stream));
+  NCCL_TRY(r.broadcast(dsz.p, dsz.p, (size_t)R + 1, ncclUint64, root, c->comm, c->stream));
+  HIP_TRY(hipMemcpyAsync(sz.data(), dsz.p, sizeof(unsigned long long) * (R + 1), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (root_failed) return fail(GICP_EINVAL, "the root passes every rank's blob");
+  if (sz[(size_t)R]) return fail(GICP_ECOMM, "the root's tie-tree builder failed (no blobs sent)");
   DevBuf sendb, recvb;
   std::vector<size_t> off((size_t)R + 1, 0);
   for (int k = 0; k < R; ++k) off[(size_t)k + 1] = off[(size_t)k] + (k == root ? 0 : (size_t)sz[(size_t)k]);

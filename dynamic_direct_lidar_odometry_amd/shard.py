@@ -139,7 +139,7 @@ class ShardedGicp:
         per-keyframe covariances of odom.cc:1147-1149,1302-1310 are).  Slab
         mode balances the owned source at `guess` when source and guess are
         given (else the target count)."""
-        from . import TARGET
+        from . import TARGET, GicpError
         if self.mode == "groups":
             self.slab = None
             self.local_index = np.arange(len(points), dtype=np.int64)
@@ -167,9 +167,17 @@ class ShardedGicp:
             else:
                 blobs = None
                 if self.rank == 0:
-                    self.ctx.tie_builder_set(whole)
                     try:
+                        self.ctx.tie_builder_set(whole)
                         blobs = [self.ctx.tie_builder_export(self._slab_index(whole, s)) for s in slabs]
+                    except Exception:
+                        # the other ranks are already waiting in the collective: enter it with no blobs
+                        # (a failure word goes out, every rank raises) before re-raising here
+                        try:
+                            self.ctx.set_tie_trees_from_root(0, None)
+                        except GicpError:
+                            pass
+                        raise
                     finally:
                         self.ctx.tie_builder_set(None)
                 self.ctx.set_tie_trees_from_root(0, blobs)

@@ -266,6 +266,12 @@ typedef struct gicp_grid_info {
                                 without a list, or the bound's reach beyond the grid);
                                 0: the linearize is one kernel (lookup fused into the
                                 moments)                                              */
+  int64_t build_status;      /* 0, or the gicp_status of a build that failed (pool or
+                                table limits, GICP_OPT_GRID_BUDGET_MB, device memory):
+                                the target then stays on the walk for this bound and
+                                the align itself succeeds                             */
+  int64_t scratch_bytes;     /* the build's transient device scratch at its peak (not
+                                held afterwards; not in gicp_get_device_bytes)       */
 } gicp_grid_info;
 gicp_status gicp_get_target_grid_info(struct gicp_ctx* ctx, gicp_grid_info* out);
 /* Queries the last align's final linearize answered from the candidate cells

@@ -190,6 +190,10 @@ class OdomRef:
         self.initialized = False    # ddlo_initialized_
         self.thresh = float(params.keyframe_thresh_dist)
         self.submap = None
+        # on_align(kind, inputs, T, result): called after each of the two aligns of a frame with the exact
+        # inputs the oracle aligned ("s2s": source, target, target_cov, guess; "s2m": source, source_cov,
+        # target, target_cov, guess), so a test can run the GPU on identical inputs
+        self.on_align = None
 
     def _preprocess(self, pts):
         a = pts.astype(F)
@@ -247,6 +251,9 @@ class OdomRef:
         g.set_covariances(1, self.target_cov)
         T_S2S, r1 = g.align()
         src_cov = g.get_covariances(0)
+        if self.on_align is not None:
+            self.on_align("s2s", dict(source=scan, target=self.target, target_cov=self.target_cov, guess=None),
+                          T_S2S, r1)
         self.T_s2s = mat4_mul(self.T_s2s_prev, T_S2S)
         self.T_s2s_prev = self.T_s2s.copy()
         self.target, self.target_cov = scan, src_cov        # swapSourceAndTarget
@@ -255,6 +262,9 @@ class OdomRef:
         g2.set_covariances(0, src_cov)
         g2.set_covariances(1, self.submap[1])
         self.T, r2 = g2.align(self.T_s2s)
+        if self.on_align is not None:
+            self.on_align("s2m", dict(source=scan, source_cov=src_cov, target=self.submap[0],
+                                      target_cov=self.submap[1], guess=self.T_s2s.copy()), self.T, r2)
         self.T = self.T.astype(F)
         self.T_s2s_prev = self.T.copy()
         self.pose = self.T[:3, 3].copy()
