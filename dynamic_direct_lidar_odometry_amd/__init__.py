@@ -222,7 +222,7 @@ def _xyz(points):
     return a, 12
 
 
-OPT_TIE_ORDER, OPT_TIE_LAZY, OPT_TIE_PARTIAL_LEVELS, OPT_COV_TASKS = 1, 2, 3, 4
+OPT_TIE_ORDER, OPT_TIE_LAZY, OPT_TIE_PARTIAL_LEVELS, OPT_COV_TASKS, OPT_GRID_MAX_MB = 1, 2, 3, 4, 5
 
 
 def set_default_option(option: int, value: int):

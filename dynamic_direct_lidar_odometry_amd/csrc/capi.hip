@@ -111,7 +111,7 @@ int env_int(const char* name, int dflt) {
 
 // Options (gicp_set_option): the values new contexts take.  A -DDDLO_DEV
 // build still reads the old A/B environment variables as the initial values.
-static std::atomic<int> g_opt_default[GICP_OPT_COUNT] = {{0}, {1}, {1}, {3}, {0}};
+static std::atomic<int> g_opt_default[GICP_OPT_COUNT] = {{0}, {1}, {1}, {3}, {0}, {0}};
 static const bool g_opt_env_read = [] {
   auto rd = [](const char* name, int opt, bool flag) {
     const char* v = dev_getenv(name);
@@ -126,8 +126,10 @@ static const bool g_opt_env_read = [] {
 
 static gicp_status check_option(int option, int value) {
   if (option <= 0 || option >= GICP_OPT_COUNT) return fail(GICP_EINVAL, "unknown option");
-  if (option == GICP_OPT_TIE_PARTIAL_LEVELS ? (value < 0 || value > 24) : (value != 0 && value != 1))
-    return fail(GICP_EINVAL, "option value out of range");
+  const bool ok = option == GICP_OPT_TIE_PARTIAL_LEVELS ? (value >= 0 && value <= 24)
+                  : option == GICP_OPT_GRID_MAX_MB        ? value >= 0
+                                                          : (value == 0 || value == 1);
+  if (!ok) return fail(GICP_EINVAL, "option value out of range");
   return GICP_OK;
 }
 
@@ -248,6 +250,9 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
   }
   const long ncells = dims[0] * dims[1] * dims[2];
   if (ncells > kGridMaxCells || !std::isfinite(ext[0] + ext[1] + ext[2])) return GICP_OK;   // not built: the walk
+  const size_t cap_bytes = c->grid_max_mb > 0 ? ((size_t)c->grid_max_mb << 20) : ~(size_t)0;
+  if ((size_t)ncells * sizeof(unsigned long long) > cap_bytes)
+    return fail(GICP_ENOMEM, "candidate cells: the directory exceeds GICP_OPT_GRID_MAX_MB");
   hipEvent_t e0, e1;
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
@@ -440,6 +445,9 @@ gicp_status cellgrid_build(gicp_ctx* c, CloudData& cd, float cap2, std::shared_p
     fine_base[l + 1] += tot[1];
   }
   if ((size_t)fine_base[4] >= 0x3ffffffeu) return fail(GICP_ENOMEM, "candidate cells: fine table too large");
+  if ((size_t)ncells * sizeof(unsigned long long) + sizeof(uint2) * (size_t)fine_base[4] +
+          sizeof(float4) * (size_t)ent_base[4] > cap_bytes)
+    return fail(GICP_ENOMEM, "candidate cells: the lists exceed GICP_OPT_GRID_MAX_MB");
   HIP_TRY(g->fine.ensure(sizeof(uint2) * std::max<size_t>(fine_base[4], 1)));
   HIP_TRY(g->ent.ensure(sizeof(float4) * std::max<size_t>(ent_base[4], 1)));
   b.fine = g->fine.as<uint2>();
@@ -552,6 +560,7 @@ void finalize_job(gicp_ctx* c) {
   std::memcpy(probe.guess_R, c->job_last.guess_R, sizeof(probe.guess_R));
   std::memcpy(probe.guess_t, c->job_last.guess_t, sizeof(probe.guess_t));
   probe.job_full = c->job_last.job_full;
+  probe.ticket = c->job_last.ticket;
   if (!c->job_last_valid || std::memcmp(&probe, &c->job_last, sizeof(AlignJob)) != 0) {
     j.job_full = 1;
     c->job_last = j;
@@ -571,6 +580,7 @@ gicp_status fill_job(gicp_ctx* c, const float* guess16, int nblocks) {
   j.sqd = c->sqd.as<float>();
   j.slab = c->slab.as<double>();
   j.state = c->state_dev.as<AlignState>();
+  j.ticket = (++c->ticket) & ((1ull << 47) - 1);
   j.stats = c->stats_on ? c->stats.as<unsigned int>() : nullptr;
   for (int r = 0; r < 3; ++r) {
     for (int cc = 0; cc < 3; ++cc) j.guess_R[3 * r + cc] = guess16 ? (double)guess16[4 * r + cc] : (r == cc ? 1.0 : 0.0);
@@ -894,8 +904,41 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
     const char* v = dev_getenv("DDLO_SPIN_WAIT");
     return !(v && *v == '0');
   }();
+  const unsigned long long ticket = c->job_host->ticket;
   for (;;) {
-    if (spin) {
+    if (spin && !g.fuse_lm) {
+      // chunk k's last LM step writes its publication word (ticket, done,
+      // iter) after the state (AlignState::pub): the host polls that word in
+      // pinned memory, which lands as the kernel stores it, instead of the
+      // chunk's event, which completes only after the command processor has
+      // retired the kernel.  The event is still queried every 64 polls (an
+      // error, or a word that never comes, ends the wait).
+      static std::atomic<int> waiters{0};
+      waiters.fetch_add(1, std::memory_order_relaxed);
+      const volatile unsigned long long* pw = &(c->state_host + (k & 1))->pub;
+      const int expect = first + k;   // iterations after chunk k unless done earlier
+      hipError_t q = hipErrorNotReady;
+      for (unsigned n = 1;; ++n) {
+        const unsigned long long w = *pw;
+        if ((w >> 17) == ticket && (((w >> 16) & 1ull) || (int)(w & 0xffffu) >= expect)) {
+          q = hipSuccess;
+          break;
+        }
+        if ((n & 63) == 0) {
+          q = hipEventQuery(c->chunk_ev[k]);
+          if (q != hipErrorNotReady) {
+            const unsigned long long w2 = *pw;   // the event completed: the word has landed
+            if (q == hipSuccess && !((w2 >> 17) == ticket && (((w2 >> 16) & 1ull) || (int)(w2 & 0xffffu) >= expect)))
+              q = hipErrorUnknown;
+            break;
+          }
+        }
+        if (waiters.load(std::memory_order_relaxed) > 1) std::this_thread::yield();
+      }
+      waiters.fetch_sub(1, std::memory_order_relaxed);
+      if (q == hipErrorUnknown) return fail(GICP_EHIP, "align chunk completed without its state publication");
+      HIP_TRY(q);
+    } else if (spin) {
       // several host threads waiting at once (gicp_s2s_batch's workers):
       // they yield the core between polls, so the pollers do not starve the
       // HIP runtime's own threads
@@ -923,7 +966,8 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   *final_chunk = k;
   c->state_slot = k & 1;
   c->tail_ev = c->chunk_ev[launched - 1];
-  c->tail_pending = launched - 1 > k;
+  // (a published chunk may still be retiring its last kernel: the tail covers it too)
+  c->tail_pending = launched - 1 > k || (spin && !g.fuse_lm);
   // Speculate next time only if this align outran its predicted first chunk:
   // when the prediction held, the queued no-op chunk only delays the next
   // align (A/B at cfg 3: 0.466 -> 0.459 ms/scan without it).
@@ -1054,6 +1098,7 @@ gicp_status gicp_ctx_create(int device, gicp_ctx** out) {
   c->tie_lazy = g_opt_default[GICP_OPT_TIE_LAZY].load() != 0;
   c->partial_levels = g_opt_default[GICP_OPT_TIE_PARTIAL_LEVELS].load();
   c->cov_tasks = g_opt_default[GICP_OPT_COV_TASKS].load() != 0;
+  c->grid_max_mb = g_opt_default[GICP_OPT_GRID_MAX_MB].load();
   {
     // DDLO_NF_OWN_STREAM=1 (development): every ctx builds its trees on its
     // own stream, the partial tree gated on the tie count (the S2S batch's
@@ -1335,10 +1380,13 @@ gicp_status gicp_align(gicp_ctx* c, const float* guess16, float* out16, gicp_res
     res->lm_lambda = st.lambda;
     res->ties_resolved = st.ties_resolved;
     res->tie_reruns = reruns;
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, end_ev));
-    res->device_ms = ms;
     if (c->profiling) {
+      // (profiled aligns only: a graph align returns as soon as its state is
+      // published, before its end event has completed)
+      float ms = 0.f;
+      HIP_TRY(hipEventSynchronize(end_ev));
+      HIP_TRY(hipEventElapsedTime(&ms, c->ev0, end_ev));
+      res->device_ms = ms;
       double tot = 0.0;
       for (int i = 0; i < st.iter; ++i) {
         float m = 0.f;
@@ -1567,6 +1615,7 @@ gicp_status gicp_set_option(gicp_ctx* c, int option, int value) {
     case GICP_OPT_TIE_LAZY: c->tie_lazy = value != 0; break;
     case GICP_OPT_TIE_PARTIAL_LEVELS: c->partial_levels = value; break;
     case GICP_OPT_COV_TASKS: c->cov_tasks = value != 0; break;
+    case GICP_OPT_GRID_MAX_MB: c->grid_max_mb = value; break;
   }
   return GICP_OK;
 }
@@ -1580,6 +1629,7 @@ gicp_status gicp_get_option(const gicp_ctx* c, int option, int* value) {
     case GICP_OPT_TIE_LAZY: *value = c->tie_lazy ? 1 : 0; break;
     case GICP_OPT_TIE_PARTIAL_LEVELS: *value = c->partial_levels; break;
     case GICP_OPT_COV_TASKS: *value = c->cov_tasks ? 1 : 0; break;
+    case GICP_OPT_GRID_MAX_MB: *value = c->grid_max_mb; break;
   }
   return GICP_OK;
 }

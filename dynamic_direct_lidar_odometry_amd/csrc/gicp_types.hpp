@@ -167,7 +167,11 @@ struct AlignState {
                          // (the host builds it and runs the align again)
   int ties_resolved;     // tied queries re-run through the target's nanoflann tree (this align)
   int tie_err;           // a re-run failed (bits as k_nf_resolve_*: 1 depth, 2 tree build, 16 distance mismatch)
-  int pad[2];            // 16-byte multiple (copied in 16-byte words)
+  // publication word (pinned copies only; 0 in the device state): k_lm_step
+  // writes (ticket << 17 | done << 16 | iter) after the rest of the copy and a
+  // system-scope fence, so the host that sees its align's ticket and the
+  // chunk's iteration reads a complete state without waiting on a HIP event
+  unsigned long long pub;
 };
 
 // Everything a kernel needs for one align, written by the host before launch.
@@ -184,7 +188,8 @@ struct AlignJob {
   double guess_R[9];
   double guess_t[3];
   long long job_full;      // k_align_init copies the whole job (1) or, when nothing else changed since the
-                           // previous align of the ctx, only guess_R / guess_t and this word (0)
+                           // previous align of the ctx, only guess_R / guess_t, this word and the ticket (0)
+  unsigned long long ticket;   // the align's sequence number on its ctx (AlignState::pub)
   double max_corr2;        // max_correspondence_distance^2 (double compare)
   float cap2;              // nextafter(float(max_corr2), +inf), the search bound
   // fp64 copies of the seed kernel's float knobs (scalar loads where they are

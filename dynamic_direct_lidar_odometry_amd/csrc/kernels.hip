@@ -636,6 +636,15 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
   }
 };
 
+// developer build (-DDDLO_COV_PROF): per 32-query group of k_covariances2,
+// (start, end) s_memrealtime stamps (100 MHz), leaves scanned / exact-tested,
+// splits, the hardware wave slot and the group's largest k-th distance
+// (tools/cov_timeline.py reads them through ddlo_dev_cov_prof)
+#ifdef DDLO_COV_PROF
+constexpr int kCovProfGroups = 8192;
+__device__ unsigned long long g_cov_prof[kCovProfGroups * 4];
+#endif
+
 // covariances with two lanes per query: wave w handles sorted points
 // [32w, 32w+32) (leaf w); seeds leaves w-1 .. w+1
 template <int KCAP, bool EXACT, int MINW>
@@ -647,6 +656,9 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
   const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
   const int ngroups = (c.n + 31) >> 5;
   for (int g = wave; g < ngroups; g += nwaves_total) {
+#ifdef DDLO_COV_PROF
+    const unsigned long long cp_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int i = g * 32 + (lane_id() & 31);
     KnnVisitor2<KCAP, EXACT> vis;
     vis.init(k);
@@ -669,6 +681,20 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
       split_search<KnnVisitor2<KCAP, EXACT>, 32>(c, vis, gp(c.keys)[min(i, c.n - 1)], L);
     }
     vis.merge_halves();
+#ifdef DDLO_COV_PROF
+    {
+      const float kd = wave_max(vis.active && lane_id() < 32 ? vis.kth_dist() : 0.f);
+      const unsigned long long cp_t1 = __builtin_amdgcn_s_memrealtime();
+      if (lane_id() == 0 && g < kCovProfGroups) {
+        unsigned long long* o = g_cov_prof + (size_t)g * 4;
+        o[0] = cp_t0;
+        o[1] = cp_t1;
+        o[2] = (unsigned long long)vis.st_scan | ((unsigned long long)vis.st_exact << 32);
+        o[3] = (unsigned long long)__float_as_uint(kd) | ((unsigned long long)vis.st_splits << 32) |
+               ((unsigned long long)(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) & 0xffff) << 40);
+      }
+    }
+#endif
     if (!vis.active || lane_id() >= 32) continue;
     const bool kth_tie = vis.td == vis.kth_dist(), inner = vis.inner_tie();
     cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
@@ -927,27 +953,40 @@ __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_d
                                                     const AlignJob* __restrict__ job_src) {
   static_assert(sizeof(AlignJob) % 8 == 0, "AlignJob is copied in 8-byte words");
   static_assert(offsetof(AlignJob, guess_R) % 8 == 0 && offsetof(AlignJob, guess_t) == offsetof(AlignJob, guess_R) + 72 &&
-                    offsetof(AlignJob, job_full) == offsetof(AlignJob, guess_R) + 96,
-                "guess_R, guess_t, job_full: 13 consecutive 8-byte words");
-  constexpr int kHdr0 = (int)(offsetof(AlignJob, guess_R) / 8), kHdrN = 13;
+                    offsetof(AlignJob, job_full) == offsetof(AlignJob, guess_R) + 96 &&
+                    offsetof(AlignJob, ticket) == offsetof(AlignJob, guess_R) + 104,
+                "guess_R, guess_t, job_full, ticket: 14 consecutive 8-byte words");
+  constexpr int kHdr0 = (int)(offsetof(AlignJob, guess_R) / 8), kHdrN = 14, kHdrFull = 12;
   __shared__ unsigned long long job_lds[sizeof(AlignJob) / 8];
   __shared__ int full_s;
   const AlignJob* job = job_dev;
   double gR[9], gt[3];
+  // The device job's words this kernel needs, loaded before the host job's
+  // header arrives (values only: they are used, and dereferenced, only when
+  // the header says the device job is still the one of the last align, i.e.
+  // job_full = 0; the device job buffer itself lives as long as the ctx).
+  AlignState* const st_dev = job_dev->state;
+  unsigned* const ctr_dev = job_dev->task_ctr;
+  unsigned* const fb_dev = job_dev->fb_count;
+  const int grid_dev = job_dev->grid_on;
+  const int maxit_dev = job_dev->max_iterations;
+  const int rec0_dev = job_dev->reuse && job_dev->reuse_rec0;
+  bool full = true;
   if (job_src) {
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(job_src);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(job_dev);
     // system scope: read past every GPU cache (the host rewrites this buffer per align).
-    // First the guess and the full-copy flag (one round trip); the rest of the
+    // First the guess, the full-copy flag and the ticket (one round trip); the rest of the
     // job only when the host changed more than the guess since the last align.
     if ((int)threadIdx.x < kHdrN) {
       const unsigned long long v = __hip_atomic_load(src + kHdr0 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       job_lds[kHdr0 + threadIdx.x] = v;
       dst[kHdr0 + threadIdx.x] = v;
-      if (threadIdx.x == kHdrN - 1) full_s = v != 0ull;
+      if (threadIdx.x == kHdrFull) full_s = v != 0ull;
     }
     __syncthreads();
-    if (full_s) {
+    full = full_s != 0;
+    if (full) {
       for (int w = threadIdx.x; w < (int)(sizeof(AlignJob) / 8); w += blockDim.x) {
         if (w >= kHdr0 && w < kHdr0 + kHdrN) continue;
         const unsigned long long v = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -964,10 +1003,17 @@ __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_d
     for (int i = 0; i < 9; ++i) gR[i] = job->guess_R[i];
     for (int i = 0; i < 3; ++i) gt[i] = job->guess_t[i];
   }
-  AlignState* st = job->state;
-  if (threadIdx.x <= kTaskCounters) job->task_ctr[threadIdx.x * kCtrStride] = 0u;   // + the moment kernel's arrival counter
-  if (job->grid_on && threadIdx.x <= kFbSegs) job->fb_count[threadIdx.x * 32] = 0u;   // the lookup's walk list (+ total)
-  if (threadIdx.x < 64) {   // source radius from the top-level boxes (<= 64 of them)
+  AlignState* st = full ? job->state : st_dev;
+  unsigned* const task_ctr = full ? job->task_ctr : ctr_dev;
+  const int grid_on = full ? job->grid_on : grid_dev;
+  unsigned* const fb_count = full ? job->fb_count : fb_dev;
+  const int max_iterations = full ? job->max_iterations : maxit_dev;
+  const int rec0 = full ? (job->reuse && job->reuse_rec0) : rec0_dev;
+  if (threadIdx.x <= kTaskCounters) task_ctr[threadIdx.x * kCtrStride] = 0u;   // + the moment kernel's arrival counter
+  if (grid_on && threadIdx.x <= kFbSegs) fb_count[threadIdx.x * 32] = 0u;   // the lookup's walk list (+ total)
+  // source radius from the top-level boxes (<= 64 of them); an unchanged job
+  // (same source cloud) keeps the last align's st->src_radius
+  if (full && threadIdx.x < 64) {
     const CloudDev& c = job->src;
     const int top = c.nlevels - 1;
     const int off = lvl_off(c, top), cnt = lvl_cnt(c, top);
@@ -979,18 +1025,16 @@ __global__ __launch_bounds__(256) void k_align_init(AlignJob* __restrict__ job_d
       r = sqrtf(mx * mx + my * my + mz * mz) * 1.0001f;
     }
     for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m));
-    if (threadIdx.x == 0) {
-      st->src_radius = r;
-      st->rec = job->reuse && job->reuse_rec0;
-      st->any_rec = 0;
-    }
+    if (threadIdx.x == 0) st->src_radius = r;
   }
   if (threadIdx.x == 0) {
+    st->rec = rec0;
+    st->any_rec = 0;
     for (int i = 0; i < 9; ++i) st->R[i] = gR[i];
     for (int i = 0; i < 3; ++i) st->t[i] = gt[i];
     st->lambda = -1.0;
     st->iter = 0;
-    st->done = job->max_iterations <= 0 ? 1 : 0;
+    st->done = max_iterations <= 0 ? 1 : 0;
     st->converged = 0;
     st->nr_iterations = 0;
     st->lm_failed = 0;
@@ -2851,11 +2895,20 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
   }
   if (publish) {
     static_assert(sizeof(AlignState) % 16 == 0, "AlignState is copied in 16-byte words");
+    static_assert(offsetof(AlignState, pub) == sizeof(AlignState) - 8, "the publication word is the last 8 bytes");
     __threadfence();   // this block's state stores, then an L1 invalidate before they are read back
     __syncthreads();
     const int4* src = reinterpret_cast<const int4*>(st);
     int4* dst = reinterpret_cast<int4*>(publish);
     for (int w = threadIdx.x; w < (int)(sizeof(AlignState) / 16); w += blockDim.x) dst[w] = src[w];
+    // then the publication word, after every thread's copy is visible to the host
+    const unsigned long long tk = job->ticket;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long w = (tk << 17) | ((unsigned long long)(st->done != 0) << 16) | ((unsigned)st->iter & 0xffffu);
+      __hip_atomic_store(&publish->pub, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -3187,6 +3240,12 @@ void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr,
 
 }  // namespace ddlo
 
+#ifdef DDLO_COV_PROF
+// developer build: k_covariances2's per-group records of the last launch, [group][4]
+extern "C" int ddlo_dev_cov_prof(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ddlo::g_cov_prof), sizeof(ddlo::g_cov_prof));
+}
+#endif
 #ifdef DDLO_MOM_PROF
 // developer build: the fused moment kernel's wave stamps of the last align, [iteration][wave][6]
 extern "C" int ddlo_dev_mom_prof(unsigned long long* out) {

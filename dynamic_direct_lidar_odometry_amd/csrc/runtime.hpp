@@ -340,6 +340,8 @@ struct gicp_ctx {
   int state_slot = 0;              // slot holding the state of the last align / linearize
   hipEvent_t tail_ev = nullptr;    // last chunk launched by the last align (may still be queued)
   bool tail_pending = false;
+  int grid_max_mb = 0;             // GICP_OPT_GRID_MAX_MB (0: no cap)
+  unsigned long long ticket = 0;   // aligns launched (AlignJob::ticket)
   int* flag_host = nullptr;       // pinned
   bool have_align = false;        // a linearize ran against the current src/tgt
   int last_nsrc = 0;
@@ -977,7 +979,14 @@ inline gicp_status compute_cov(gicp_ctx* c, Side& side, int k_use = 0) {
   return GICP_OK;
 }
 
-inline void invalidate_align(gicp_ctx* c) { c->have_align = false; }
+// A cloud, covariance or tie-tree change: no linearization to report, and the
+// next align sends its whole job (k_align_init keeps per-source values such as
+// st->src_radius only across aligns whose job is unchanged; a new cloud may
+// reuse the old one's pool blocks, so equal pointers do not prove the same cloud)
+inline void invalidate_align(gicp_ctx* c) {
+  c->have_align = false;
+  c->job_last_valid = false;
+}
 
 }  // namespace rt
 }  // namespace ddlo

@@ -98,7 +98,8 @@ typedef struct gicp_result {
   double final_cost;          /* sum e^T M e at the last linearize               */
   double final_hessian[36];   /* getFinalHessian(), row-major                    */
   double lm_lambda;           /* lambda after the last step                      */
-  double device_ms;           /* device time of the align (HIP events)           */
+  double device_ms;           /* device time of the align (HIP events; only when
+                                 profiling is enabled, else 0)                   */
   double linearize_ms;        /* summed device time of the linearize kernels
                                  (only when profiling is enabled, else 0)       */
   int32_t ties_resolved;      /* correspondences whose nearest distance was an
@@ -224,7 +225,10 @@ enum gicp_option {
                                        lazily; 0: on the whole tree */
   GICP_OPT_TIE_PARTIAL_LEVELS = 3,  /* big levels of that partial tree (0..24, default 3) */
   GICP_OPT_COV_TASKS = 4,           /* 1: the task-based k-NN for covariances (default 0: a lane per query) */
-  GICP_OPT_COUNT = 5
+  GICP_OPT_GRID_MAX_MB = 5,         /* device MiB a target's candidate cells may hold (0, the default: no
+                                       cap); a build that would exceed it is abandoned and the target stays
+                                       on the walk (gicp_grid_info.build_status = GICP_ENOMEM) */
+  GICP_OPT_COUNT = 6
 };
 gicp_status gicp_set_option(struct gicp_ctx* ctx, int option, int value);
 gicp_status gicp_get_option(const struct gicp_ctx* ctx, int option, int* value);

@@ -105,10 +105,14 @@ def test_default_options():
     assert P.get_default_option(P.OPT_TIE_LAZY) == 1
     assert P.get_default_option(P.OPT_TIE_PARTIAL_LEVELS) == 3
     assert P.get_default_option(P.OPT_COV_TASKS) == 0
+    assert P.get_default_option(P.OPT_GRID_MAX_MB) == 0
+    with P.default_option(P.OPT_GRID_MAX_MB, 150):
+        assert P.get_default_option(P.OPT_GRID_MAX_MB) == 150
     with P.default_option(P.OPT_TIE_ORDER, 0):
         assert P.get_default_option(P.OPT_TIE_ORDER) == 0
     assert P.get_default_option(P.OPT_TIE_ORDER) == 1
-    for opt, val in ((0, 1), (5, 1), (P.OPT_TIE_ORDER, 2), (P.OPT_TIE_PARTIAL_LEVELS, -1), (P.OPT_TIE_PARTIAL_LEVELS, 25)):
+    for opt, val in ((0, 1), (6, 1), (P.OPT_TIE_ORDER, 2), (P.OPT_TIE_PARTIAL_LEVELS, -1), (P.OPT_TIE_PARTIAL_LEVELS, 25),
+                     (P.OPT_GRID_MAX_MB, -1)):
         with pytest.raises(P.GicpError):
             P.set_default_option(opt, val)
 

@@ -146,6 +146,47 @@ def test_grid_auto_builds_for_a_long_lived_target(pair):
     c.close()
 
 
+@pytest.mark.parametrize("stage", ["directory", "lists"])
+def test_grid_build_over_budget_falls_back_to_the_walk(pair, stage):
+    """a candidate-cell build that fails is not the align's error.  With GICP_OPT_GRID_MAX_MB below
+    what the target's cells need (below the directory alone, or between the directory and directory + lists)
+    the build is abandoned, the target stays on the walk for that bound (build_status GICP_ENOMEM, not built,
+    not retried), and every align equals the cells-off one bit for bit; a larger cap builds as usual."""
+    tgt, src, T, tcov, scov = pair
+    kw = dict(k_correspondences=10, max_correspondence_distance=2.0, max_iterations=32, transformation_epsilon=0.01)
+    cw = make(tgt, src, tcov, scov, P.GRID_OFF, **kw)
+    full = make(tgt, src, tcov, scov, P.GRID_ON, **kw)
+    full.align(perturbed(T, 0.1, 0.01).astype(np.float32))
+    need, dir_bytes = full.grid_info()["bytes"], 8 * full.grid_info()["coarse_cells"]
+    full.close()
+    cap_mb = max(1, (dir_bytes >> 20) // 2) if stage == "directory" else (dir_bytes + need) // 2 >> 20
+    assert (cap_mb << 20) < need and (stage == "directory") == ((cap_mb << 20) < dir_bytes), (cap_mb, dir_bytes, need)
+    c = P.Context(0)
+    c.set_option(P.OPT_GRID_MAX_MB, cap_mb)
+    c.set_params(P.default_params(**kw))
+    c.set_target_grid(P.GRID_ON)
+    c.set_target(tgt)
+    c.set_covariances(TARGET, tcov)
+    c.set_source(src)
+    c.set_covariances(SOURCE, scov)
+    for dt, yaw in [(0.3, 0.02), (0.1, -0.01)]:
+        G = perturbed(T, dt, yaw).astype(np.float32)
+        pg, rg = c.align(G)
+        pw, rw = cw.align(G)
+        np.testing.assert_array_equal(pg, pw)
+        assert (rg.iterations_run, rg.lm_trials) == (rw.iterations_run, rw.lm_trials)
+        info = c.grid_info()
+        assert info["built"] == 0 and info["build_status"] == 6, info   # GICP_ENOMEM
+    c.set_option(P.OPT_GRID_MAX_MB, (need >> 20) + 64)
+    c.set_target(tgt)   # a new target cloud: a new build, within the cap
+    c.set_covariances(TARGET, tcov)
+    pg, _ = c.align(perturbed(T, 0.3, 0.02).astype(np.float32))
+    assert c.grid_info()["built"] == 1 and c.grid_info()["build_status"] == 0
+    np.testing.assert_array_equal(pg, cw.align(perturbed(T, 0.3, 0.02).astype(np.float32))[0])
+    c.close()
+    cw.close()
+
+
 def test_grid_follows_the_target_cloud(pair):
     """The cells belong to the cloud: after a swap the (former target) source
     has them and the new target has none; the results equal the walk's."""

@@ -143,16 +143,34 @@ def test_cfg5_chain_through_loop_revisit():
                       f"{seen['revisit'][2]}", flush=True)
         return "revisit" in seen and i >= seen["revisit"][0] + 30
 
-    # absolute poses: 1e-4 through the closure frame.  The chain integrates ~730 frames of fp32 pose
-    # updates, and once the submaps hold first-lap keyframes the S2M aligns pull against their drift: the
-    # two sides' accumulated rounding then grows ~1e-5 m per frame (1.00e-4 at frame 731, 2.1e-4 at 739,
-    # decisions still exact), so the 30 frames after it are held to 1e-3
+    # absolute poses: 1e-4 through the closure frame, 1e-3 for the 30 frames after it.  Why the two chains
+    # part at all: every align is bit-identical on identical inputs (test_cfg5_identical_input_aligns_...,
+    # 160 aligns over frames 680-759, max |dT| 0, same iterations and LM trials; S2M Hessians well
+    # conditioned, smallest eigenvalue 2.2e6-4.0e6 against 2.7e9-2.9e9), and so are the k = 10 covariances;
+    # the one input that differs is the voxel filter's float centroids: PCL sums a voxel's points in
+    # std::sort's (introsort, unstable) order, which the oracle reproduces, the device in input order, so
+    # ~5 % of the centroids differ by one ulp (tools/chain_inputs.py, profiles/r06_chain_inputs.txt).  Those
+    # ulps move frame 2's S2S pose by 1.6e-9; each keyframe cloud is then built from its own side's pose and
+    # each S2M aligns against it, so the difference feeds back (1e-6 by frame 10, tools/chain_diff.py).
+    # With the voxel filters off the chains are identical (test_cfg5_chain_without_voxel_filter_exact).
+    # Once first-lap keyframes re-enter the submaps the two sides' maps pull against their own first-lap
+    # poses and the gap grows ~1e-5 m per frame (1.00e-4 at frame 731, 2.1e-4 at 739; decisions exact).
     stats, nk = run_chain(frames, OD.default_odom_params(), progress=True, stop=stop,
                           pose_tol=lambda i: 1e-4 if i <= LAP_FRAMES else 1e-3)
     print(f"chain: {stats['frames']} frames, {nk} keyframes, {stats['changes']} submap changes, "
           f"max |dT| {stats['max_dpose']:.3g}, max |d step| {stats['max_dstep']:.3g}", flush=True)
     assert "revisit" in seen, stats
     assert stats["max_dstep"] < 1e-4, stats   # every frame's own motion within the north star's 1e-4
+
+
+def test_cfg5_chain_without_voxel_filter_exact(frames210):
+    """The chain's only non-identical input is the voxel filter's centroid summation order (see above): with
+    both voxel filters off (scans and keyframes at full resolution, the crop box kept) the GPU driver and the
+    oracle chain agree BIT FOR BIT over 90 frames of the loop: every decision, iteration count and pose."""
+    p = OD.default_odom_params(vf_scan_use=0, vf_submap_use=0)
+    stats, nk = run_chain(frames210[:90], p, pose_tol=lambda i: 0.0)
+    assert stats["tracked"] >= 85 and nk >= 2, (stats, nk)
+    assert stats["max_dpose"] == 0.0, stats
 
 
 def identical_input_aligns(frames, params, first=0, report=None):
