@@ -636,81 +636,6 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
   }
 };
 
-// Four lanes per query (lanes l, l + 16, l + 32, l + 48 of a 16-query wave):
-// each quarter keeps the exact top-k of its quarter of every leaf (positions
-// 8q .. 8q + 7).  The bound is the smallest of the four quarters' k-th keys
-// (any quarter's k points lie in the union), exchanged after every leaf by two
-// butterfly steps; at the end the lists merge pairwise (lanes l ^ 32, then
-// l ^ 16) into the union's exact top-k.  Half the serial scan per lane of
-// KnnVisitor2 and half the queries per wavefront: a wave whose queries reach
-// many leaves (the far, sparse end of a scan) finishes sooner, which is what
-// bounds k_covariances2 (tools/cov_timeline.py).
-template <int KCAP, bool EXACT>
-struct KnnVisitor4 : KnnVisitor<KCAP, EXACT> {
-  unsigned long long wk_all = ~0ull;   // the smallest k-th key over the four quarters
-  __device__ __forceinline__ float bound() const {
-    return fminf(__uint_as_float((unsigned)(wk_all >> 32)), this->tight);
-  }
-  __device__ __forceinline__ bool need(float4 lo, float4 hi) const {
-    return box_dist2(this->qx, this->qy, this->qz, lo, hi) <= bound();
-  }
-  static __device__ __forceinline__ unsigned long long xor32(unsigned long long v) {
-    const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
-    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    return ((unsigned long long)swap_partner(rh, hi) << 32) | swap_partner(rl, lo);
-  }
-  static __device__ __forceinline__ unsigned long long xor16(unsigned long long v) {
-    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, 16), hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), 16);
-    return ((unsigned long long)hi << 32) | lo;
-  }
-  __device__ __forceinline__ void exchange() {   // whole wave
-    const unsigned long long m = umin64(this->wk, xor32(this->wk));
-    wk_all = umin64(m, xor16(m));
-  }
-  __device__ __forceinline__ void process(const WaveLds* L, int start) {
-    const int h0 = (lane_id() >> 4) * (kLeafSize / 4);
-    for (int j = 0; j < kLeafSize / 4; ++j) {
-      const float d = dist2(this->qx, this->qy, this->qz, L->px[h0 + j], L->py[h0 + j], L->pz[h0 + j]);
-      const unsigned long long key = dkey(d, start + h0 + j);
-      if (this->active && key < wk_all && d <= this->tight) this->insert(key);
-      else this->td = fminf(this->td, this->active ? d : INFINITY);   // active lanes only (see KnnVisitor::process)
-    }
-    exchange();
-  }
-  __device__ __forceinline__ void scan_leaf(const CloudDev& c, int leaf, WaveLds* L) {
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane_id() < kLeafSize) p = ldg4(c.pts, leaf * kLeafSize + lane_id());
-    stage_points<KnnVisitor4>(L, p);
-    process(L, leaf * kLeafSize);
-  }
-  __device__ __forceinline__ bool scan_leaves(const CloudDev& c, int base, unsigned long long ex, WaveLds* L) {
-    return scan_leaves_lds(c, base, ex, *this, L);
-  }
-  // merge the list of lane l ^ X into lane l's, for the lanes with bit X clear
-  // (the others keep theirs unchanged while the swaps read them)
-  template <int X>
-  __device__ __forceinline__ void merge_from() {
-    const bool low = (lane_id() & X) == 0;
-#pragma unroll
-    for (int s = 0; s < KCAP; ++s) {
-      const unsigned long long other = X == 32 ? xor32(this->K[s]) : xor16(this->K[s]);
-      if (low) {
-        if (other < this->wk) this->insert(other);
-        else this->td = fminf(this->td, key_dist(other));
-      }
-    }
-    const unsigned tb = __float_as_uint(this->td);
-    const unsigned to = X == 32 ? swap_partner(__builtin_amdgcn_permlane32_swap(tb, tb, false, false), tb)
-                                : (unsigned)__shfl_xor((int)tb, 16);
-    this->td = fminf(this->td, __uint_as_float(to));
-  }
-  __device__ __forceinline__ void merge_quarters() {
-    merge_from<32>();
-    merge_from<16>();
-  }
-};
-
 // developer build (-DDDLO_COV_PROF): per 32-query group of k_covariances2,
 // (start, end) s_memrealtime stamps (100 MHz), leaves scanned / exact-tested,
 // splits, the hardware wave slot and the group's largest k-th distance
@@ -783,71 +708,6 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
     }
   }
 }
-// covariances with four lanes per query: wave w handles sorted points
-// [16w, 16w+16) (half of leaf w / 2); seeds leaves w/2 - 1 .. w/2 + 1
-template <int KCAP, bool EXACT, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_covariances4(CloudDev c, int k, int method, double* __restrict__ cov6,
-                                                            TieList ties) {
-  __shared__ WaveLds lds[4];
-  WaveLds* L = &lds[threadIdx.x >> 6];
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
-  const int ngroups = (c.n + 15) >> 4;
-  for (int g = wave; g < ngroups; g += nwaves_total) {
-#ifdef DDLO_COV_PROF
-    const unsigned long long cp_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    const int i = g * 16 + (lane_id() & 15);
-    KnnVisitor4<KCAP, EXACT> vis;
-    vis.init(k);
-    vis.wk_all = ~0ull;
-    vis.nfull = k <= kLeafSize ? c.n / kLeafSize : 0;
-    vis.active = i < c.n;
-    const float4 q = ldg4(c.pts, min(i, c.n - 1));
-    vis.qx = q.x;
-    vis.qy = q.y;
-    vis.qz = q.z;
-    {
-      const int lf = g >> 1;
-      const int s0 = max(lf - 1, 0), s1 = min(lf + 1, c.cnt0 - 1);
-      for (int l = s0; l <= s1; ++l) {
-        vis.scan_leaf(c, l, L);
-        const float4 lo = ldg4(c.box_lo, l), hi = ldg4(c.box_hi, l);
-        vis.note_leaf(f4v{lo.x, lo.y, lo.z, 0.f}, f4v{hi.x, hi.y, hi.z, 0.f}, l);
-      }
-      vis.skip_lo = s0;
-      vis.skip_hi = s1;
-      split_search<KnnVisitor4<KCAP, EXACT>, 16>(c, vis, gp(c.keys)[min(i, c.n - 1)], L);
-    }
-    vis.merge_quarters();
-#ifdef DDLO_COV_PROF
-    {
-      const float kd = wave_max(vis.active && lane_id() < 16 ? vis.kth_dist() : 0.f);
-      const unsigned long long cp_t1 = __builtin_amdgcn_s_memrealtime();
-      if (lane_id() == 0 && g < kCovProfGroups) {
-        unsigned long long* o = g_cov_prof + (size_t)g * 4;
-        o[0] = cp_t0;
-        o[1] = cp_t1;
-        o[2] = (unsigned long long)vis.st_scan | ((unsigned long long)vis.st_exact << 32);
-        o[3] = (unsigned long long)__float_as_uint(kd) | ((unsigned long long)vis.st_splits << 32);
-      }
-    }
-#endif
-    if (!vis.active || lane_id() >= 16) continue;
-    const bool kth_tie = vis.td == vis.kth_dist(), inner = vis.inner_tie();
-    cov_from_keys<KCAP>(c, vis.K, k, method, cov6 + 6 * (size_t)i);
-    if (ties.list && (kth_tie || inner)) {   // rare: a tie whose order matters is re-run (nftree.hip)
-      bool push = true;
-      if constexpr (KCAP <= 16) {
-        const int j = kth_tie ? -1 : vis.single_pair();
-        if (j >= 0) push = !cov_order_free<KCAP>(c, vis.K, k, method, j, cov6 + 6 * (size_t)i);
-      }
-      if (push) ties.push(i);
-    }
-  }
-}
-template __global__ void k_covariances4<10, true, 4>(CloudDev, int, int, double*, TieList);
-template __global__ void k_covariances4<20, true, 2>(CloudDev, int, int, double*, TieList);
 template __global__ void k_covariances2<10, true, 3>(CloudDev, int, int, double*, TieList);
 template __global__ void k_covariances2<10, true, 4>(CloudDev, int, int, double*, TieList);
 template __global__ void k_covariances2<20, true, 3>(CloudDev, int, int, double*, TieList);
@@ -3228,20 +3088,10 @@ static int env_knob(const char* name, int dflt) {   // development knobs (A/B of
   const char* v = dev_getenv(name);
   return v && *v ? std::atoi(v) : dflt;
 }
-#ifndef DDLO_COV_4LANE_DEFAULT
-#define DDLO_COV_4LANE_DEFAULT 1
-#endif
 bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo,
                         TieList ties) {
   const int nb = group_blocks(c.n);
   static const int two_lanes = env_knob("DDLO_COV_2LANE", 1);   // two lanes per query (A/B)
-  static const int four_lanes = env_knob("DDLO_COV_4LANE", DDLO_COV_4LANE_DEFAULT);   // four lanes per query (A/B)
-  if (four_lanes && !redo && (k == 10 || k == 20)) {
-    const int nb4 = std::max(1, std::min(cdiv(cdiv(c.n, 16), 4), 16384));
-    if (k == 10) k_covariances4<10, true, 4><<<nb4, 256, 0, s>>>(c, k, method, cov6, ties);
-    else k_covariances4<20, true, 2><<<nb4, 256, 0, s>>>(c, k, method, cov6, ties);
-    return true;
-  }
   if (two_lanes && !redo && (k == 10 || k == 20)) {
     const int nb2 = std::max(1, std::min(cdiv(cdiv(c.n, 32), 4), 8192));
     static const int occ = env_knob("DDLO_COV_OCC", 3);
