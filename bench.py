@@ -25,7 +25,7 @@ k_moments, launched back to back per outer iteration) timed with HIP events
 on the library's stream inside this process; algorithmic bytes per launch =
 76 * N_s (SURVEY.md §8(d) B_lin), peak HBM 8 TB/s (MI355X_MICROARCH.md);
 traffic = HBM-side bytes per launch from the committed rocprofv3 --pmc
-passes (profiles/r02_traffic.json).  cpu_baseline = the C++/OpenMP
+passes (profiles/r06_traffic.json).  cpu_baseline = the C++/OpenMP
 oracle (oracle/cpu_ref.cpp, a restatement of the reference algorithm, "port")
 timed on this host on the same problem.
 """
@@ -47,7 +47,7 @@ METRIC = "GICP iters/sec + ms/scan, 131k-pt source → 500k-pt submap; pose Δ v
 HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same workload
 # (tools/pmc_traffic.sh -> tools/pmc_traffic.py), committed per round
-TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r05_traffic.json"))
+TRAFFIC_JSON = os.environ.get("DDLO_TRAFFIC_JSON", os.path.join(HERE, "profiles", "r06_traffic.json"))
 
 
 def pmc_traffic():

@@ -387,7 +387,10 @@ class Context:
             ab = self._abuf = (gb, ob, rb, gb.ctypes.data, ob.ctypes.data, C.pointer(rb))
         gb, ob, rb, gp, op, rp = ab
         if guess is not None:
-            np.copyto(gb, np.reshape(guess, (4, 4)), casting="unsafe")
+            if type(guess) is np.ndarray and guess.shape == (4, 4):
+                gb[...] = guess   # (~1.6 us less than reshape + copyto per call)
+            else:
+                np.copyto(gb, np.reshape(guess, (4, 4)), casting="unsafe")
         self._check(self.L.gicp_align(self.h, None if guess is None else gp, op, rp))
         return ob.copy(), GicpResult.from_buffer_copy(rb)
 

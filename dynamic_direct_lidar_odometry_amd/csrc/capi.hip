@@ -677,9 +677,12 @@ int linearize_blocks(int nsrc) { return linearize_geometry(nsrc, 0).mom_blocks; 
 LinGeom geometry(const gicp_ctx* c) {
   LinGeom g = linearize_geometry(c->src.cloud->n, c->tgt.cloud->upper_count());
   g.state = c->state_dev.as<AlignState>();
-  g.fuse_lm = !c->comm && lm_fusion_enabled();   // a sharded align all-reduces between the moments and the LM step
   g.grid = grid_active(c);
   g.grid_walk = !g.grid || c->tgt.cloud->grid->dev.has_fallback != 0;
+  // the LM step in the moment kernel's last block: a sharded align all-reduces
+  // between the two, so never there; on by default for the one-kernel lookup
+  // linearize (DDLO_FUSE_LM: development A/B for every path)
+  g.fuse_lm = !c->comm && lm_fusion_enabled(g.grid && !g.grid_walk);
   return g;
 }
 
@@ -763,7 +766,7 @@ constexpr int kMaxFixedChunk = 64;
 gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks, AlignState* publish) {
   (void)nblocks;   // = geometry(c).mom_blocks (fill_job)
   const LinGeom g = geometry(c);
-  launch_linearize(c->stream, jd, g);
+  launch_linearize(c->stream, jd, g, publish);   // (fused LM step: the moment kernel's last block publishes)
   if (c->comm) {
     launch_mom_reduce(c->stream, jd);
     NCCL_TRY(rccl().all_reduce(c->mom.p, c->mom.p, kSlabStride, ncclFloat64, ncclSum, c->comm, c->stream));
@@ -771,7 +774,6 @@ gicp_status enqueue_iteration(gicp_ctx* c, const AlignJob* jd, int nblocks, Alig
   if (!g.fuse_lm)
     launch_lm_step(c->stream, jd, c->state_dev.as<AlignState>(), c->slab.as<double>(), g.mom_blocks,
                    c->comm ? c->mom.as<double>() : nullptr, publish);
-  else if (publish) HIP_TRY(hipMemcpyAsync(publish, c->state_dev.p, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
   return GICP_OK;
 }
 
@@ -906,7 +908,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   }();
   const unsigned long long ticket = c->job_host->ticket;
   for (;;) {
-    if (spin && !g.fuse_lm) {
+    if (spin) {
       // chunk k's last LM step writes its publication word (ticket, done,
       // iter) after the state (AlignState::pub): the host polls that word in
       // pinned memory, which lands as the kernel stores it, instead of the
@@ -938,18 +940,6 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
       waiters.fetch_sub(1, std::memory_order_relaxed);
       if (q == hipErrorUnknown) return fail(GICP_EHIP, "align chunk completed without its state publication");
       HIP_TRY(q);
-    } else if (spin) {
-      // several host threads waiting at once (gicp_s2s_batch's workers):
-      // they yield the core between polls, so the pollers do not starve the
-      // HIP runtime's own threads
-      static std::atomic<int> waiters{0};
-      waiters.fetch_add(1, std::memory_order_relaxed);
-      hipError_t q;
-      while ((q = hipEventQuery(c->chunk_ev[k])) == hipErrorNotReady) {
-        if (waiters.load(std::memory_order_relaxed) > 1) std::this_thread::yield();
-      }
-      waiters.fetch_sub(1, std::memory_order_relaxed);
-      HIP_TRY(q);
     } else {
       HIP_TRY(hipEventSynchronize(c->chunk_ev[k]));
     }
@@ -967,7 +957,7 @@ gicp_status run_align_graph(gicp_ctx* c, int max_it, int nblocks, int* final_chu
   c->state_slot = k & 1;
   c->tail_ev = c->chunk_ev[launched - 1];
   // (a published chunk may still be retiring its last kernel: the tail covers it too)
-  c->tail_pending = launched - 1 > k || (spin && !g.fuse_lm);
+  c->tail_pending = launched - 1 > k || spin;
   // Speculate next time only if this align outran its predicted first chunk:
   // when the prediction held, the queued no-op chunk only delays the next
   // align (A/B at cfg 3: 0.466 -> 0.459 ms/scan without it).
@@ -1036,12 +1026,12 @@ gicp_status run_align_eager_profiled(gicp_ctx* c, int max_it, int nblocks) {
 }  // namespace
 
 namespace ddlo {
-bool lm_fusion_enabled() {
-  static const bool on = [] {
+bool lm_fusion_enabled(bool lookup) {
+  static const int on = [] {   // -1: the default (fused on the lookup path only)
     const char* v = dev_getenv("DDLO_FUSE_LM");
-    return v && *v && std::atoi(v) != 0;
+    return v && *v ? std::atoi(v) : -1;
   }();
-  return on;
+  return on < 0 ? lookup : on != 0;
 }
 }  // namespace ddlo
 

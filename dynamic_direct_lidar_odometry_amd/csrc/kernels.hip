@@ -2069,9 +2069,30 @@ __device__ unsigned long long g_mom_prof[kMomProfIters * kMomProfWaves * 6];   /
 #else
 #define MOM_PROF(i)
 #endif
+// Copy the state to the host-mapped slot, then its publication word
+// (AlignState::pub: ticket, done, iter) after a system-scope fence, so the
+// host that sees the word reads a complete state.  Whole block.
+__device__ __forceinline__ void publish_state(const AlignJob* __restrict__ job, const AlignState* __restrict__ st,
+                                              AlignState* __restrict__ publish) {
+  static_assert(sizeof(AlignState) % 16 == 0, "AlignState is copied in 16-byte words");
+  static_assert(offsetof(AlignState, pub) == sizeof(AlignState) - 8, "the publication word is the last 8 bytes");
+  __threadfence();   // this block's state stores, then an L1 invalidate before they are read back
+  __syncthreads();
+  const int4* src = reinterpret_cast<const int4*>(st);
+  int4* dst = reinterpret_cast<int4*>(publish);
+  for (int w = threadIdx.x; w < (int)(sizeof(AlignState) / 16); w += blockDim.x) dst[w] = src[w];
+  const unsigned long long tk = job->ticket;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long w = (tk << 17) | ((unsigned long long)(st->done != 0) << 16) | ((unsigned)st->iter & 0xffffu);
+    __hip_atomic_store(&publish->pub, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <bool FUSE_LM, bool LOOKUP = false>
 __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __restrict__ job,
-                                                            AlignState* __restrict__ st) {
+                                                            AlignState* __restrict__ st, AlignState* __restrict__ publish) {
 #ifdef DDLO_MOM_PROF
   unsigned long long mp_t[6] = {0, 0, 0, 0, 0, 0};
 #endif
@@ -2084,7 +2105,12 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
   for (int e = 0; e < 9; ++e) R[e] = sg->R[e];
   for (int e = 0; e < 3; ++e) t[e] = sg->t[e];
   const int st_rec = sg->rec, st_any_rec = sg->any_rec;
-  if (__builtin_amdgcn_readfirstlane(sg->done)) return;
+  if (__builtin_amdgcn_readfirstlane(sg->done)) {
+    // a no-op iteration after convergence: the chunk's publication still
+    // happens (as k_lm_step's after an early exit), by block 0
+    if (FUSE_LM && publish && blockIdx.x == 0) publish_state(job, st, publish);
+    return;
+  }
   const CloudDev src = job->src;
   const CloudDev tgt = job->tgt;
   const auto src_cov = gp(job->src_cov);
@@ -2356,12 +2382,13 @@ __global__ __launch_bounds__(64 * kMomWaves) void k_moments(const AlignJob* __re
     }
     __syncthreads();
     lm_step_body<false>(job, st, job->slab, job->nblocks, nullptr);
+    if (publish) publish_state(job, st, publish);
   }
 }
-template __global__ void k_moments<false>(const AlignJob*, AlignState*);
-template __global__ void k_moments<true>(const AlignJob*, AlignState*);
-template __global__ void k_moments<false, true>(const AlignJob*, AlignState*);
-template __global__ void k_moments<true, true>(const AlignJob*, AlignState*);
+template __global__ void k_moments<false>(const AlignJob*, AlignState*, AlignState*);
+template __global__ void k_moments<true>(const AlignJob*, AlignState*, AlignState*);
+template __global__ void k_moments<false, true>(const AlignJob*, AlignState*, AlignState*);
+template __global__ void k_moments<true, true>(const AlignJob*, AlignState*, AlignState*);
 
 // ---------------------------------------------------------------------------
 // K5: slab reduction + LM/GN step on one workgroup.
@@ -2893,23 +2920,7 @@ __global__ __launch_bounds__(kLmThreads) void k_lm_step(const AlignJob* __restri
     if (premom) lm_step_body<true>(job, st, slab, nblocks, premom);
     else lm_step_body<false>(job, st, slab, nblocks, nullptr);
   }
-  if (publish) {
-    static_assert(sizeof(AlignState) % 16 == 0, "AlignState is copied in 16-byte words");
-    static_assert(offsetof(AlignState, pub) == sizeof(AlignState) - 8, "the publication word is the last 8 bytes");
-    __threadfence();   // this block's state stores, then an L1 invalidate before they are read back
-    __syncthreads();
-    const int4* src = reinterpret_cast<const int4*>(st);
-    int4* dst = reinterpret_cast<int4*>(publish);
-    for (int w = threadIdx.x; w < (int)(sizeof(AlignState) / 16); w += blockDim.x) dst[w] = src[w];
-    // then the publication word, after every thread's copy is visible to the host
-    const unsigned long long tk = job->ticket;
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned long long w = (tk << 17) | ((unsigned long long)(st->done != 0) << 16) | ((unsigned)st->iter & 0xffffu);
-      __hip_atomic_store(&publish->pub, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (publish) publish_state(job, st, publish);
 }
 
 // ---------------------------------------------------------------------------
@@ -3166,12 +3177,12 @@ LinGeom linearize_geometry(int nsrc, int tgt_upper) {
   return g;
 }
 
-void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
+void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g, AlignState* publish) {
   static const int fused_lookup = env_knob("DDLO_GRID_FUSED", 1);   // 0: separate lookup kernel (A/B)
   if (g.grid && !g.grid_walk && fused_lookup) {
     // every query is answered by its cell: the lookup runs inside the moment kernel
-    if (g.fuse_lm) k_moments<true, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state);
-    else k_moments<false, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state);
+    if (g.fuse_lm) k_moments<true, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state, publish);
+    else k_moments<false, true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state, nullptr);
     return;
   }
   if (g.grid) k_cell_lookup<<<g.lookup_blocks, 256, 0, s>>>(job);
@@ -3204,8 +3215,8 @@ void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g) {
     else if (occ_scan == 5) k_nn_scan<5, 6><<<scan_blocks, 64 * kScanWaves, 0, s>>>(job);   // 6-task batches: 7.5 KB LDS per wave
     else k_nn_scan<4><<<scan_blocks, 64 * kScanWaves, 0, s>>>(job);
   }
-  if (g.fuse_lm) k_moments<true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state);
-  else k_moments<false><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state);
+  if (g.fuse_lm) k_moments<true><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state, publish);
+  else k_moments<false><<<g.mom_blocks, 64 * kMomWaves, 0, s>>>(job, g.state, nullptr);
 }
 int search_queries_per_wave() { return kSearchQ; }
 int task_cap_per_region(int nsrc) {

@@ -58,9 +58,10 @@ struct LinGeom {
   bool grid = false;      // the target's candidate cells answer the search first (k_cell_lookup)
   bool grid_walk = true;  // ... and some of its cells have no list: the walk kernel follows the lookup
 };
-bool lm_fusion_enabled();   // DDLO_FUSE_LM (unsharded graph aligns)
+bool lm_fusion_enabled(bool lookup);   // unsharded aligns on the one-kernel lookup path (DDLO_FUSE_LM: dev A/B)
 LinGeom linearize_geometry(int nsrc, int tgt_upper);
-void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g);
+// publish: with g.fuse_lm, the host-mapped state slot the fused LM step publishes to (or nullptr)
+void launch_linearize(hipStream_t s, const AlignJob* job, const LinGeom& g, AlignState* publish = nullptr);
 int search_queries_per_wave();
 int task_cap_per_region(int nsrc);   // task-list slots per region for nsrc source points
 int moment_blocks(int nsrc);  // slab rows written by the moment kernel
