@@ -292,6 +292,30 @@ struct KeyList<KCAP, true> {
   __device__ __forceinline__ const unsigned long long& operator[](int s) const { return p[64 * s]; }
 };
 
+// Compare-exchange of two 64-bit keys: slot = min(key, slot), key = the
+// larger, from ONE compare.  Written out because the compiler turns the two
+// selects of one predicate into umin + umax and lowers each with its own
+// 64-bit compare (9 instructions and a twice as long dependent chain per slot
+// of the insertion network that bounds a kNN leaf scan).  The s_nop covers the
+// VALU-writes-VCC -> v_cndmask hazard, as the compiler's own code does.
+__device__ __forceinline__ void cmp_exchange_u64(unsigned long long& key, unsigned long long& slot) {
+  const unsigned long long a = key, b = slot;
+  unsigned lo0, lo1, hi0, hi1;
+  asm volatile(
+      "v_cmp_lt_u64_e32 vcc, %[a], %[b]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[lo0], %[b0], %[a0], vcc\n\t"
+      "v_cndmask_b32_e32 %[lo1], %[b1], %[a1], vcc\n\t"
+      "v_cndmask_b32_e32 %[hi0], %[a0], %[b0], vcc\n\t"
+      "v_cndmask_b32_e32 %[hi1], %[a1], %[b1], vcc"
+      : [lo0] "=&v"(lo0), [lo1] "=&v"(lo1), [hi0] "=&v"(hi0), [hi1] "=&v"(hi1)
+      : [a] "v"(a), [b] "v"(b), [a0] "v"((unsigned)a), [a1] "v"((unsigned)(a >> 32)), [b0] "v"((unsigned)b),
+        [b1] "v"((unsigned)(b >> 32))
+      : "vcc");
+  slot = ((unsigned long long)lo1 << 32) | lo0;
+  key = ((unsigned long long)hi1 << 32) | hi0;
+}
+
 template <int KCAP, bool EXACT, bool KLDS = false>
 struct KnnVisitor : VisitStats {
   WaveBox box;
@@ -390,11 +414,7 @@ struct KnnVisitor : VisitStats {
       td = fminf(td, key_dist(out));   // the key pushed out of the list
     } else {
 #pragma unroll
-      for (int s = 0; s < KCAP; ++s) {
-        const unsigned long long lo = umin64(key, K[s]);
-        key = key < K[s] ? K[s] : key;
-        K[s] = lo;
-      }
+      for (int s = 0; s < KCAP; ++s) cmp_exchange_u64(key, K[s]);
       td = fminf(td, key_dist(key));   // the key pushed out of the list
     }
     update_worst();
