@@ -41,9 +41,17 @@ def main():
               f"{float(r['Percentage']):.1f} |")
     trace = list(csv.DictReader(open(f"{d}/{pre}_kernel_trace.csv")))
     trace.sort(key=lambda x: int(x["Start_Timestamp"]))
-    seq = [(short(x["Kernel_Name"]).split("<")[0], (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3) for x in trace]
+    # k_moments<true, ...> is the LM step fused into the moment kernel (the one-kernel candidate-cell
+    # iteration of a graph align since round 6): it ends its iteration like k_lm_step does
+    seq = []
+    for x in trace:
+        full = short(x["Kernel_Name"])
+        n = full.split("<")[0]
+        if n == "k_moments" and full.replace(" ", "").startswith("k_moments<true"):
+            n = "k_moments_fused"
+        seq.append((n, (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3))
     SEARCH = ("k_cell_lookup", "k_nn_seed", "k_nn_collect", "k_nn_scan")
-    LOOP = SEARCH + ("k_moments", "k_lm_step", "k_mom_reduce")
+    LOOP = SEARCH + ("k_moments", "k_moments_fused", "k_lm_step", "k_mom_reduce")
     # a sharded align's all-reduce sits between k_mom_reduce and k_lm_step (RCCL's own kernel)
     SKIP = ("ncclDevKernel", "ncclKernel", "__amd_rocclr")
     aligns = []
@@ -60,6 +68,7 @@ def main():
             cur = None
     per_pos = defaultdict(lambda: defaultdict(list))
     active_lin, active_search, active_mom, active_lm = [], [], [], []
+    active_lin_eager, active_fused, fused_pos = [], [], defaultdict(list)
     noop, noop_eager = [], []
     eager_aligns = 0
     for a in aligns:
@@ -67,7 +76,7 @@ def main():
         iters, it_k = [], defaultdict(float)
         for n, us in a:
             it_k[n] += us
-            if n == "k_lm_step":
+            if n in ("k_lm_step", "k_moments_fused"):
                 iters.append(it_k)
                 it_k = defaultdict(float)
         # a graph align launches <= kMaxFirstChunk (8) + a few single-iteration
@@ -77,10 +86,21 @@ def main():
         it = 0
         for k in iters:
             s_us = sum(k[n] for n in SEARCH)
+            if k["k_moments_fused"] > 0:
+                f = k["k_moments_fused"]
+                if f < MOM_NOOP_US:
+                    (noop_eager if eager else noop).append(f)
+                    continue
+                fused_pos[it].append(f)
+                active_fused.append(f)
+                it += 1
+                continue
             m, l = k["k_moments"], k["k_lm_step"]
             if s_us < NOOP_US and m < MOM_NOOP_US:
                 (noop_eager if eager else noop).append(s_us + m + l)
                 continue
+            if eager:
+                active_lin_eager.append(s_us + m)
             per_pos[it]["search"].append(s_us)
             per_pos[it]["seed"].append(k["k_nn_seed"])
             per_pos[it]["collect"].append(k["k_nn_collect"])
@@ -108,6 +128,15 @@ def main():
           f"(search {avg(active_search):.1f} + moments {avg(active_mom):.1f})")
     print(f"- k_lm_step average over active iterations: {avg(active_lm):.1f} us")
     print(f"- no-op iteration (3 launches) average: {avg(noop + noop_eager):.1f} us")
+    if active_fused:
+        print(f"\n## Graph aligns: the LM step fused into the lookup moment kernel ({len(active_fused)} active "
+              f"iterations)\n")
+        print("| iteration | n | k_moments<true, true> us (lookup + moments + fan-in + LM step) |")
+        print("|---:|---:|---:|")
+        for it in sorted(fused_pos):
+            print(f"| {it} | {len(fused_pos[it])} | {avg(fused_pos[it]):.1f} |")
+        print(f"\n- fused iteration average: **{avg(active_fused):.1f} us**; the linearize alone is timed on the "
+              f"eager profiled aligns above (unfused, as bench.py's roofline): {avg(active_lin_eager):.1f} us")
 
 
 if __name__ == "__main__":
