@@ -472,6 +472,12 @@ struct ddlo_odom {
   Quatf rotq;
   std::vector<std::unique_ptr<Keyframe>> keyframes;
   std::vector<int> submap_prev, keyframe_convex, keyframe_concave;
+  // the hulls are functions of the keyframe positions (append-only, never
+  // moved) and, for the concave one, alpha: recomputed only when a keyframe
+  // was added or alpha changed (the reference reruns qhull every scan; the
+  // 3-D Delaunay of the concave hull costs ~0.1-0.6 ms of host time)
+  int convex_nk = -1, concave_nk = -1;
+  double concave_alpha = -1.0;
   bool have_median = false;
   float median_prev = 0.f;
   double thresh_dist = 1.0;
@@ -598,11 +604,18 @@ gicp_status submap_keyframes(ddlo_odom* o, bool* changed) {
   std::vector<float> kpos(3 * (size_t)nk);
   for (int i = 0; i < nk; ++i)
     for (int a = 0; a < 3; ++a) kpos[3 * i + a] = o->keyframes[i]->pose[a];
-  if (nk >= 4) o->keyframe_convex = convex_hull(kpos.data(), nk);  // computeConvexHull: >= 4 keyframes
+  if (nk >= 4 && nk != o->convex_nk) {   // computeConvexHull: >= 4 keyframes
+    o->keyframe_convex = convex_hull(kpos.data(), nk);
+    o->convex_nk = nk;
+  }
   std::vector<float> cds;
   for (int c : o->keyframe_convex) cds.push_back(ds[c]);
   push_submap_indices(cds, o->p.submap_kcv, o->keyframe_convex, cur);
-  if (nk >= 5) o->keyframe_concave = concave_hull(kpos.data(), nk, o->thresh_dist);  // >= 5 keyframes
+  if (nk >= 5 && (nk != o->concave_nk || o->thresh_dist != o->concave_alpha)) {   // >= 5 keyframes
+    o->keyframe_concave = concave_hull(kpos.data(), nk, o->thresh_dist);
+    o->concave_nk = nk;
+    o->concave_alpha = o->thresh_dist;
+  }
   std::vector<float> kds;
   for (int c : o->keyframe_concave) kds.push_back(ds[c]);
   push_submap_indices(kds, o->p.submap_kcc, o->keyframe_concave, cur);
