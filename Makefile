@@ -93,7 +93,7 @@ statsprof: $(OBJS)
 # developer variant: k_covariances2 stores per-group stamps (tools/cov_timeline.py; load with DDLO_GICP_LIB)
 covprof: $(OBJS)
 	@mkdir -p $(LIBDIR)/covprof
-	$(HIPCC) $(HIPFLAGS) -DDDLO_COV_PROF -c $(CSRC)/kernels.hip -o $(LIBDIR)/covprof/kernels.o
+	$(HIPCC) $(HIPFLAGS) -DDDLO_COV_PROF -DDDLO_DEV -c $(CSRC)/kernels.hip -o $(LIBDIR)/covprof/kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/covprof/libddlo_gicp.so $(LIBDIR)/covprof/kernels.o $(filter-out $(LIBDIR)/kernels.o,$(OBJS))
 
 .PHONY: covprof
