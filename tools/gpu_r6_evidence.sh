@@ -33,3 +33,5 @@ cat $O/bench.json | cut -c1-600
 timeout -k 10 600 python -u tools/slab_cells_table.py 2 4 8 > $O/slab_cells_table.log 2>&1 || { echo SLAB_FAIL; tail -20 $O/slab_cells_table.log; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 echo ALL_OK
+bash tools/gpu_odom_prof.sh > $O/odom_prof.txt 2>&1 || { echo ODOM_PROF_FAIL; tail $O/odom_prof.txt; exit 1; }
+echo ODOM_PROF_OK
