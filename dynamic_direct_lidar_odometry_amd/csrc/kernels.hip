@@ -667,60 +667,25 @@ __device__ unsigned long long g_cov_prof[kCovProfGroups * 4];
 
 // covariances with two lanes per query: wave w handles sorted points
 // [32w, 32w+32) (leaf w); seeds leaves w-1 .. w+1
-// presplit > 0: every group has two work items (wavefronts 2g, 2g + 1).  A
-// group whose 32 points span more than `presplit` metres (the bounding box of
-// the points themselves) is cut at its largest Morton jump and each half is
-// searched by its own wavefront, in parallel; otherwise item 2g takes the
-// whole group and item 2g + 1 exits.  The widest groups (far, sparse ranges,
-// whose Morton runs jump) were the kernel's tail: one wavefront walked their
-// sub-ranges one after another (tools/cov_timeline.py).  A query's neighbours
-// do not depend on which lanes search beside it, so results are unchanged.
 template <int KCAP, bool EXACT, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, int method, double* __restrict__ cov6,
-                                                            TieList ties, float presplit) {
+                                                            TieList ties) {
   __shared__ WaveLds lds[4];
   WaveLds* L = &lds[threadIdx.x >> 6];
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves_total = (gridDim.x * blockDim.x) >> 6;
   const int ngroups = (c.n + 31) >> 5;
-  const int nitems = presplit > 0.f ? 2 * ngroups : ngroups;
-  for (int item = wave; item < nitems; item += nwaves_total) {
+  for (int g = wave; g < ngroups; g += nwaves_total) {
 #ifdef DDLO_COV_PROF
     const unsigned long long cp_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int g = presplit > 0.f ? item >> 1 : item;
     const int i = g * 32 + (lane_id() & 31);
-    const bool inr = i < c.n;
-    const float4 q = ldg4(c.pts, min(i, c.n - 1));
-    const unsigned long long qkey = gp(c.keys)[min(i, c.n - 1)];
-    bool mine = inr;
-    if (presplit > 0.f) {
-      const float ext = fmaxf(fmaxf(wave_max(inr ? q.x : -INFINITY) - wave_min(inr ? q.x : INFINITY),
-                                    wave_max(inr ? q.y : -INFINITY) - wave_min(inr ? q.y : INFINITY)),
-                              wave_max(inr ? q.z : -INFINITY) - wave_min(inr ? q.z : INFINITY));
-      const int half = item & 1;
-      if (ext > presplit) {
-        const int sp = morton_jump_split<32>(qkey, 0, 32);
-        const int qi = lane_id() & 31;
-        mine = inr && (half ? qi >= sp : qi < sp);
-      } else if (half) {
-#ifdef DDLO_COV_PROF
-        if (lane_id() == 0 && item < kCovProfGroups) g_cov_prof[(size_t)item * 4] = g_cov_prof[(size_t)item * 4 + 1] = 0ull;
-#endif
-        continue;   // an unsplit group: the first item searches all of it
-      }
-      if (!__any(mine)) {
-#ifdef DDLO_COV_PROF
-        if (lane_id() == 0 && item < kCovProfGroups) g_cov_prof[(size_t)item * 4] = g_cov_prof[(size_t)item * 4 + 1] = 0ull;
-#endif
-        continue;
-      }
-    }
     KnnVisitor2<KCAP, EXACT> vis;
     vis.init(k);
     vis.wk_other = ~0ull;
     vis.nfull = k <= kLeafSize ? c.n / kLeafSize : 0;
-    vis.active = mine;
+    vis.active = i < c.n;
+    const float4 q = ldg4(c.pts, min(i, c.n - 1));
     vis.qx = q.x;
     vis.qy = q.y;
     vis.qz = q.z;
@@ -733,15 +698,15 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
       }
       vis.skip_lo = s0;
       vis.skip_hi = s1;
-      split_search<KnnVisitor2<KCAP, EXACT>, 32>(c, vis, qkey, L);
+      split_search<KnnVisitor2<KCAP, EXACT>, 32>(c, vis, gp(c.keys)[min(i, c.n - 1)], L);
     }
     vis.merge_halves();
 #ifdef DDLO_COV_PROF
     {
       const float kd = wave_max(vis.active && lane_id() < 32 ? vis.kth_dist() : 0.f);
       const unsigned long long cp_t1 = __builtin_amdgcn_s_memrealtime();
-      if (lane_id() == 0 && item < kCovProfGroups) {
-        unsigned long long* o = g_cov_prof + (size_t)item * 4;
+      if (lane_id() == 0 && g < kCovProfGroups) {
+        unsigned long long* o = g_cov_prof + (size_t)g * 4;
         o[0] = cp_t0;
         o[1] = cp_t1;
         o[2] = (unsigned long long)vis.st_scan | ((unsigned long long)vis.st_exact << 32);
@@ -763,10 +728,10 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
     }
   }
 }
-template __global__ void k_covariances2<10, true, 3>(CloudDev, int, int, double*, TieList, float);
-template __global__ void k_covariances2<10, true, 4>(CloudDev, int, int, double*, TieList, float);
-template __global__ void k_covariances2<20, true, 3>(CloudDev, int, int, double*, TieList, float);
-template __global__ void k_covariances2<20, true, 2>(CloudDev, int, int, double*, TieList, float);
+template __global__ void k_covariances2<10, true, 3>(CloudDev, int, int, double*, TieList);
+template __global__ void k_covariances2<10, true, 4>(CloudDev, int, int, double*, TieList);
+template __global__ void k_covariances2<20, true, 3>(CloudDev, int, int, double*, TieList);
+template __global__ void k_covariances2<20, true, 2>(CloudDev, int, int, double*, TieList);
 
 // kNN of external queries (any order) against a cloud; outputs original indices.
 template <int KCAP, bool EXACT>
@@ -3154,24 +3119,19 @@ static int env_knob(const char* name, int dflt) {   // development knobs (A/B of
   const char* v = dev_getenv(name);
   return v && *v ? std::atoi(v) : dflt;
 }
-constexpr int kCovPresplitDm = 20;   // 2 m (A/B: tools/gpu_r6_n.sh)
 bool launch_covariances(hipStream_t s, const CloudDev& c, int k, int method, double* cov6, const unsigned char* redo,
                         TieList ties) {
   const int nb = group_blocks(c.n);
   static const int two_lanes = env_knob("DDLO_COV_2LANE", 1);   // two lanes per query (A/B)
   if (two_lanes && !redo && (k == 10 || k == 20)) {
-    // groups of 32 points wider than this are searched as two halves in parallel (k_covariances2;
-    // DDLO_COV_PRESPLIT_DM: development A/B, decimetres, 0 = off)
-    static const float presplit = 0.1f * (float)env_knob("DDLO_COV_PRESPLIT_DM", kCovPresplitDm);
-    const int items = cdiv(c.n, 32) * (presplit > 0.f ? 2 : 1);
-    const int nb2 = std::max(1, std::min(cdiv(items, 4), 16384));
+    const int nb2 = std::max(1, std::min(cdiv(cdiv(c.n, 32), 4), 8192));
     static const int occ = env_knob("DDLO_COV_OCC", 3);
     // k = 20 at 2 waves / SIMD: 191 VGPRs, no spills (3 waves: 168 VGPRs + 16 spilled; DDLO_COV_OCC20=3)
     static const int occ20 = env_knob("DDLO_COV_OCC20", 2);
-    if (k == 10 && occ == 4) k_covariances2<10, true, 4><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties, presplit);
-    else if (k == 10) k_covariances2<10, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties, presplit);
-    else if (occ20 == 3) k_covariances2<20, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties, presplit);
-    else k_covariances2<20, true, 2><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties, presplit);
+    if (k == 10 && occ == 4) k_covariances2<10, true, 4><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties);
+    else if (k == 10) k_covariances2<10, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties);
+    else if (occ20 == 3) k_covariances2<20, true, 3><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties);
+    else k_covariances2<20, true, 2><<<nb2, 256, 0, s>>>(c, k, method, cov6, ties);
     return true;
   }
   if (k == 10) k_covariances<10, true><<<nb, 256, 0, s>>>(c, k, method, cov6, redo, ties);

@@ -16,7 +16,6 @@ from dynamic_direct_lidar_odometry_amd import odometry as OD  # noqa: E402
 
 nf = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 4
 voxel = "--voxel" in sys.argv
-gq = 16 if "--items" in sys.argv else 32   # --items: two work items per 32-point group (the presplit kernel)
 frames = scene.loop_sequence(64, 2048, 0, nf, device=0)[0]
 L = P.load()
 L.ddlo_dev_cov_prof.restype = C.c_int
@@ -31,10 +30,8 @@ for fi, f in enumerate(frames):
     c.compute_covariances(TARGET)
     c.synchronize()
     assert L.ddlo_dev_cov_prof(buf.ctypes.data_as(C.c_void_p)) == 0
-    ng = (len(f) + gq - 1) // gq
+    ng = (len(f) + 31) // 32
     b = buf[:ng]
-    b = b[b[:, 1] != 0]   # items that searched (a presplit kernel's empty second items record zeros)
-    ng = len(b)
     t0 = b[:, 0].astype(np.int64)
     t1 = b[:, 1].astype(np.int64)
     dur = (t1 - t0) / 100.0   # us
