@@ -614,13 +614,21 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
     const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
     wk_other = ((unsigned long long)swap_partner(rh, hi) << 32) | swap_partner(rl, lo);
   }
+  // The staged points are read four at a time (one 16-byte LDS read per
+  // axis): a per-point loop waited for one LDS round trip per point.
   __device__ __forceinline__ void process(const WaveLds* L, int start) {
     const int h0 = (lane_id() >> 5) * (kLeafSize / 2);
-    for (int j = 0; j < kLeafSize / 2; ++j) {
-      const float d = dist2(this->qx, this->qy, this->qz, L->px[h0 + j], L->py[h0 + j], L->pz[h0 + j]);
-      const unsigned long long key = dkey(d, start + h0 + j);
-      if (this->active && key < wk_both() && d <= this->tight) this->insert(key);
-      else this->td = fminf(this->td, this->active ? d : INFINITY);   // active lanes only (see KnnVisitor::process)
+    for (int j0 = 0; j0 < kLeafSize / 2; j0 += 4) {
+      const f4v X = *reinterpret_cast<const f4v*>(&L->px[h0 + j0]);
+      const f4v Y = *reinterpret_cast<const f4v*>(&L->py[h0 + j0]);
+      const f4v Z = *reinterpret_cast<const f4v*>(&L->pz[h0 + j0]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float d = dist2(this->qx, this->qy, this->qz, X[u], Y[u], Z[u]);
+        const unsigned long long key = dkey(d, start + h0 + j0 + u);
+        if (this->active && key < wk_both() && d <= this->tight) this->insert(key);
+        else this->td = fminf(this->td, this->active ? d : INFINITY);   // active lanes only (see KnnVisitor::process)
+      }
     }
     exchange();
   }
