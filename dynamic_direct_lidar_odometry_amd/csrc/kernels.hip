@@ -698,10 +698,15 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
     vis.qy = q.y;
     vis.qz = q.z;
     {
+      // the seed leaves with the next one's points in flight (as scan_leaves_lds)
       const int s0 = max(g - 1, 0), s1 = min(g + 1, c.cnt0 - 1);
+      float4 pn = lane_id() < kLeafSize ? ldg4(c.pts, s0 * kLeafSize + lane_id()) : make_float4(0.f, 0.f, 0.f, 0.f);
       for (int l = s0; l <= s1; ++l) {
-        vis.scan_leaf(c, l, L);
+        const float4 p = pn;
+        if (l < s1 && lane_id() < kLeafSize) pn = ldg4(c.pts, (l + 1) * kLeafSize + lane_id());
         const float4 lo = ldg4(c.box_lo, l), hi = ldg4(c.box_hi, l);
+        stage_points<KnnVisitor2<KCAP, EXACT>>(L, p);
+        vis.process(L, l * kLeafSize);
         vis.note_leaf(f4v{lo.x, lo.y, lo.z, 0.f}, f4v{hi.x, hi.y, hi.z, 0.f}, l);
       }
       vis.skip_lo = s0;
