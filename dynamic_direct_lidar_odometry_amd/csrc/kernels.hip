@@ -601,6 +601,17 @@ template <int KCAP, bool EXACT>
 struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
   using Base = KnnVisitor<KCAP, EXACT>;
   unsigned long long wk_other = ~0ull;   // the other half's k-th key
+#ifdef DDLO_COV_PROF
+  // s_memtime cycles: waiting for a leaf's points, scanning them, a leaf block's box tests
+  unsigned long long pt_last = 0, pt_wait = 0, pt_proc = 0, pt_box = 0;
+  __device__ __forceinline__ void prof_mark(int k) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (k == 1) pt_wait += t - pt_last;
+    else if (k == 2) pt_proc += t - pt_last;
+    else if (k == 4) pt_box += t - pt_last;
+    pt_last = t;
+  }
+#endif
   __device__ __forceinline__ unsigned long long wk_both() const { return umin64(this->wk, wk_other); }
   __device__ __forceinline__ float bound() const {
     return fminf(__uint_as_float((unsigned)(wk_both() >> 32)), this->tight);
@@ -615,9 +626,15 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
     wk_other = ((unsigned long long)swap_partner(rh, hi) << 32) | swap_partner(rl, lo);
   }
   // The staged points are read four at a time (one 16-byte LDS read per
-  // axis): a per-point loop waited for one LDS round trip per point.
+  // axis): a per-point loop waited for one LDS round trip per point.  For
+  // k = 20 the insertion test is also evaluated without short-circuit
+  // branches, with the halves' bound (wk_both) kept in registers and
+  // refreshed only after an insertion: k = 20 0.59 -> 0.53 ms per 131k-point
+  // scan, while k = 10 measured 3 % slower that way (tools/gpu_r6_x.sh).
   __device__ __forceinline__ void process(const WaveLds* L, int start) {
     const int h0 = (lane_id() >> 5) * (kLeafSize / 2);
+    const bool act = this->active;
+    unsigned long long wkb = wk_both();
     for (int j0 = 0; j0 < kLeafSize / 2; j0 += 4) {
       const f4v X = *reinterpret_cast<const f4v*>(&L->px[h0 + j0]);
       const f4v Y = *reinterpret_cast<const f4v*>(&L->py[h0 + j0]);
@@ -626,8 +643,17 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
       for (int u = 0; u < 4; ++u) {
         const float d = dist2(this->qx, this->qy, this->qz, X[u], Y[u], Z[u]);
         const unsigned long long key = dkey(d, start + h0 + j0 + u);
-        if (this->active && key < wk_both() && d <= this->tight) this->insert(key);
-        else this->td = fminf(this->td, this->active ? d : INFINITY);   // active lanes only (see KnnVisitor::process)
+        if constexpr (KCAP > 16) {
+          const bool ins = act & (key < wkb) & (d <= this->tight);
+          if (ins) {
+            this->insert(key);
+            wkb = wk_both();
+          }
+          this->td = fminf(this->td, (act & !ins) ? d : INFINITY);   // active lanes only (see KnnVisitor::process)
+        } else {
+          if (act && key < wk_both() && d <= this->tight) this->insert(key);
+          else this->td = fminf(this->td, act ? d : INFINITY);   // active lanes only (see KnnVisitor::process)
+        }
       }
     }
     exchange();
@@ -671,6 +697,7 @@ struct KnnVisitor2 : KnnVisitor<KCAP, EXACT> {
 #ifdef DDLO_COV_PROF
 constexpr int kCovProfGroups = 8192;
 __device__ unsigned long long g_cov_prof[kCovProfGroups * 4];
+__device__ unsigned long long g_cov_prof2[kCovProfGroups * 4];   // cycles: point wait, scan, box tests; blocks
 #endif
 
 // covariances with two lanes per query: wave w handles sorted points
@@ -719,6 +746,11 @@ __global__ __launch_bounds__(256, MINW) void k_covariances2(CloudDev c, int k, i
       const float kd = wave_max(vis.active && lane_id() < 32 ? vis.kth_dist() : 0.f);
       const unsigned long long cp_t1 = __builtin_amdgcn_s_memrealtime();
       if (lane_id() == 0 && g < kCovProfGroups) {
+        unsigned long long* o2 = g_cov_prof2 + (size_t)g * 4;
+        o2[0] = vis.pt_wait;
+        o2[1] = vis.pt_proc;
+        o2[2] = vis.pt_box;
+        o2[3] = vis.st_blocks;
         unsigned long long* o = g_cov_prof + (size_t)g * 4;
         o[0] = cp_t0;
         o[1] = cp_t1;
@@ -3286,6 +3318,9 @@ void launch_export_corr(hipStream_t s, const AlignJob* job, int nsrc, int* corr,
 
 #ifdef DDLO_COV_PROF
 // developer build: k_covariances2's per-group records of the last launch, [group][4]
+extern "C" int ddlo_dev_cov_prof2(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ddlo::g_cov_prof2), sizeof(ddlo::g_cov_prof2));
+}
 extern "C" int ddlo_dev_cov_prof(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ddlo::g_cov_prof), sizeof(ddlo::g_cov_prof));
 }

@@ -298,6 +298,7 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
     L->bhi[lane] = f4v{hi.x, hi.y, hi.z, 0.f};
     ov = box_overlap(vis.box, lo, hi) && !(base + lane >= vis.skip_lo && base + lane <= vis.skip_hi);
   }
+  vis.prof_mark(3);
   unsigned long long mask = __ballot(ov);
   vis.st_blocks += 1;
   vis.st_box += __popcll(mask);
@@ -313,6 +314,7 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
   }
   vis.st_exact += __popcll(ex);
   bool shrink = __any(vis.bound() < before);   // tightened by a box: later blocks see the smaller wave box
+  vis.prof_mark(4);
   if (ex) shrink |= vis.scan_leaves(c, base, ex, L);
   if (shrink) vis.box = make_wave_box(vis.active, vis.qx, vis.qy, vis.qz, vis.bound());
 }
@@ -342,8 +344,11 @@ __device__ __forceinline__ bool scan_leaves_lds(const CloudDev& c, int base, uns
     if (__any(vis.active && vis.need(make_float4(blo.x, blo.y, blo.z, 0.f), make_float4(bhi.x, bhi.y, bhi.z, 0.f)))) {
       const float before = vis.bound();
       vis.st_scan += 1;
+      vis.prof_mark(0);
       stage_points<V>(L, p);
+      vis.prof_mark(1);
       vis.process(L, (base + cur) * kLeafSize);
+      vis.prof_mark(2);
       improved |= __any(vis.bound() < before);
     }
   }
@@ -404,6 +409,10 @@ __device__ __forceinline__ void traverse(const CloudDev& c, V& vis, WaveLds* L) 
 
 struct VisitStats {
   unsigned st_blocks = 0, st_box = 0, st_exact = 0, st_scan = 0, st_splits = 0;
+  // developer timing hook (k_covariances2's -DDDLO_COV_PROF build): 0 before a
+  // leaf's points are staged, 1 after, 2 after its scan; 3 / 4 around a leaf
+  // block's box tests
+  __device__ __forceinline__ void prof_mark(int) {}
 };
 
 // ---------------------------------------------------------------------------

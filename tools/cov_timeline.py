@@ -20,6 +20,8 @@ frames = scene.loop_sequence(64, 2048, 0, nf, device=0)[0]
 L = P.load()
 L.ddlo_dev_cov_prof.restype = C.c_int
 buf = np.zeros((8192, 4), np.uint64)
+buf2 = np.zeros((8192, 4), np.uint64)   # s_memtime cycles: point wait, leaf scans, box tests; leaf blocks
+has2 = hasattr(L, "ddlo_dev_cov_prof2")
 c = P.Context(0)
 c.set_params(P.default_params(k_correspondences=10))
 c.set_tie_order(False)
@@ -31,6 +33,9 @@ for fi, f in enumerate(frames):
     c.synchronize()
     assert L.ddlo_dev_cov_prof(buf.ctypes.data_as(C.c_void_p)) == 0
     ng = (len(f) + 31) // 32
+    if has2:
+        assert L.ddlo_dev_cov_prof2(buf2.ctypes.data_as(C.c_void_p)) == 0
+        b2 = buf2[:ng][buf[:ng, 1] != 0].astype(np.float64)
     b = buf[:ng]
     t0 = b[:, 0].astype(np.int64)
     t1 = b[:, 1].astype(np.int64)
@@ -55,6 +60,17 @@ for fi, f in enumerate(frames):
     q = [float(np.mean(fin <= span * x)) for x in (0.25, 0.5, 0.75, 0.9)]
     print(f"   corr(dur, scanned) {cc:.2f}; groups finished by 25/50/75/90 % of the span: "
           + ", ".join(f"{v:.3f}" for v in q), flush=True)
+    if has2:
+        cyc = b2[:, 0] + b2[:, 1] + b2[:, 2]
+        sc = np.maximum(scan, 1)
+        print(f"   cycles per scanned leaf (median): wait {np.median(b2[:, 0] / sc):.0f}, scan {np.median(b2[:, 1] / sc):.0f}; "
+              f"box tests per block {np.median(b2[:, 2] / np.maximum(b2[:, 3], 1)):.0f} over {np.median(b2[:, 3]):.0f} blocks; "
+              f"share of the three in wait / scan / box (median) {np.median(b2[:, 0] / np.maximum(cyc, 1)):.2f} / "
+              f"{np.median(b2[:, 1] / np.maximum(cyc, 1)):.2f} / {np.median(b2[:, 2] / np.maximum(cyc, 1)):.2f}; "
+              f"their cycles per us of the group (median) {np.median(cyc / np.maximum(dur, 1e-3)):.0f}", flush=True)
+        for g in order[:4]:
+            print(f"      slow group {g}: wait {b2[g, 0]:.0f} scan {b2[g, 1]:.0f} box {b2[g, 2]:.0f} cycles over "
+                  f"{b2[g, 3]:.0f} blocks, {scan[g]} leaves, {dur[g]:.1f} us", flush=True)
     # per-scan-count cost: us per leaf scanned (median of groups with >= 8 leaves)
     m = scan >= 8
     if m.any():
