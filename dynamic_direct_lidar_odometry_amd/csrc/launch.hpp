@@ -111,12 +111,13 @@ void launch_cov_remap(hipStream_t s, const double* old_cov6, const int* old_inv_
 // preprocess.hip (odometry driver): see the kernels there for the reference
 // filters they restate.  Scratch sizes: *_tmp_bytes (hipcub temporaries).
 void launch_pack4(hipStream_t s, const unsigned char* raw, size_t stride, int n, float4* out);
+// pin: pinned host ints for the count read-back (crop_box 2, voxel_grid 16)
 int crop_box(hipStream_t s, const float4* in, int n, float size, float4* out, int* keep, int* pos, void* tmp,
-             size_t tmp_bytes, int* count_host);
+             size_t tmp_bytes, int* count_host, int* pin);
 size_t crop_box_tmp_bytes(int n);
 // crop > 0: the crop box (points inside [-crop, crop]^3 removed) folded into the same pass
 int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, int* scratch, void* tmp, size_t tmp_bytes,
-               int* count_host, float crop);
+               int* count_host, float crop, int* pin);
 size_t voxel_tmp_bytes(int n);
 constexpr size_t voxel_scratch_ints(int n) { return 7 * (size_t)n + 16 + 6 * 64; }
 void median_range_async(hipStream_t s, const float4* in, int n, float* d, float* result, void* tmp, size_t tmp_bytes,

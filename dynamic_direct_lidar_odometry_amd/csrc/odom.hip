@@ -458,8 +458,14 @@ struct ddlo_odom {
   gicp_ctx* s2m = nullptr;
   hipStream_t s = nullptr;
   // scratch (device)
-  DevBuf up, a, b, keep, pos, vscratch, cubtmp, rng, rng_sorted, cat_pts, cat_cov;
-  float* median_pin = nullptr;   // pinned: the median range of the current scan
+  DevBuf up, a, b, keep, pos, vscratch, cubtmp, medtmp, rng, rng_sorted, cat_pts, cat_cov;
+  // pinned host memory: [0] the median range of the current scan, [4..19] the
+  // voxel / crop count read-back (int)
+  float* median_pin = nullptr;
+  int* count_pin = nullptr;
+  // the median range runs on the S2M stream (it is read after the S2S align),
+  // beside the scan's index build: med_in = the voxel output is ready, med_done
+  hipEvent_t med_in = nullptr, med_done = nullptr;
   // DDLO_ODOM_TIMING=1: host wall time per phase, printed at destroy (development)
   bool timing = false;
   double t_phase[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // [8] device drain before a frame, [9] H2D call
@@ -487,8 +493,9 @@ struct ddlo_odom {
 namespace {
 
 gicp_status ensure_tmp(ddlo_odom* o, int n) {
-  const size_t t = std::max({crop_box_tmp_bytes(n), voxel_tmp_bytes(n), median_tmp_bytes(n)});
+  const size_t t = std::max(crop_box_tmp_bytes(n), voxel_tmp_bytes(n));
   HIP_TRY(o->cubtmp.ensure(t));
+  HIP_TRY(o->medtmp.ensure(median_tmp_bytes(n)));
   return GICP_OK;
 }
 
@@ -506,7 +513,7 @@ gicp_status preprocess(ddlo_odom* o, int n, bool crop, double crop_size, bool vo
     // bbox, their input order), one count read-back instead of two
     int c = 0;
     if (voxel_grid(o->s, o->a.as<float4>(), m, (float)leaf, o->b.as<float4>(), o->vscratch.as<int>(), o->cubtmp.p,
-                   o->cubtmp.bytes, &c, (float)crop_size))
+                   o->cubtmp.bytes, &c, (float)crop_size, o->count_pin))
       return fail(GICP_EHIP, "voxel filter scratch too small");
     if (c >= 0) {
       *nout = c;
@@ -520,7 +527,7 @@ gicp_status preprocess(ddlo_odom* o, int n, bool crop, double crop_size, bool vo
   }
   if (crop && m > 0) {
     if (crop_box(o->s, o->a.as<float4>(), m, (float)crop_size, o->b.as<float4>(), o->keep.as<int>(), o->pos.as<int>(),
-                 o->cubtmp.p, o->cubtmp.bytes, &m))
+                 o->cubtmp.p, o->cubtmp.bytes, &m, o->count_pin))
       return fail(GICP_EHIP, "crop box scratch too small");
     std::swap(o->a.p, o->b.p);
     std::swap(o->a.bytes, o->b.bytes);
@@ -528,7 +535,7 @@ gicp_status preprocess(ddlo_odom* o, int n, bool crop, double crop_size, bool vo
   if (vox && m > 0) {
     int c = 0;
     if (voxel_grid(o->s, o->a.as<float4>(), m, (float)leaf, o->b.as<float4>(), o->vscratch.as<int>(), o->cubtmp.p,
-                   o->cubtmp.bytes, &c, 0.f))
+                   o->cubtmp.bytes, &c, 0.f, o->count_pin))
       return fail(GICP_EHIP, "voxel filter scratch too small");
     if (c >= 0) {  // -1: grid overflow, the reference keeps the cloud unchanged
       m = c;
@@ -721,11 +728,17 @@ gicp_status ddlo_odom_create(int device, const ddlo_odom_params* p, ddlo_odom** 
   }
   o->s = o->s2s->stream;  // one stream: the driver's work is one dependent chain
   o->timing = dev_getenv("DDLO_ODOM_TIMING") != nullptr;
-  if (hipHostMalloc((void**)&o->median_pin, sizeof(float), hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc((void**)&o->median_pin, sizeof(float) * 20, hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&o->med_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&o->med_done, hipEventDisableTiming) != hipSuccess) {
+    if (o->median_pin) (void)hipHostFree(o->median_pin);
+    if (o->med_in) (void)hipEventDestroy(o->med_in);
     gicp_ctx_destroy(o->s2s);
     gicp_ctx_destroy(o->s2m);
     return fail(GICP_EHIP, "pinned allocation failed");
   }
+  *o->median_pin = 0.f;
+  o->count_pin = reinterpret_cast<int*>(o->median_pin + 4);
   mat4_identity(o->T);
   mat4_identity(o->T_s2s);
   mat4_identity(o->T_s2s_prev);
@@ -748,6 +761,8 @@ gicp_status ddlo_odom_destroy(ddlo_odom* o) {
   }
   o->keyframes.clear();
   if (o->median_pin) (void)hipHostFree(o->median_pin);
+  if (o->med_in) (void)hipEventDestroy(o->med_in);
+  if (o->med_done) (void)hipEventDestroy(o->med_done);
   gicp_ctx_destroy(o->s2m);
   gicp_ctx_destroy(o->s2s);
   delete o;
@@ -808,19 +823,28 @@ gicp_status ddlo_odom_process(ddlo_odom* o, const float* xyz, size_t n, size_t s
   if (st) return st;
   res->scan_points = m;
   mark(1);
-  // computeSpaciousness (odom.cc:981-1001): the median range is sorted on the
-  // device and copied to pinned memory; it is read after the next wait on
-  // the stream (nothing before scan matching uses it)
+  // computeSpaciousness (odom.cc:981-1001): the median range is selected on
+  // the device and copied to pinned memory, on the S2M context's stream (idle
+  // until the submap build) beside the scan's index build and the S2S align;
+  // metrics() waits for it (nothing before scan matching uses it).  The scan
+  // (o->a) is not written again before that wait.
   HIP_TRY(o->rng.ensure(sizeof(float) * (size_t)std::max(m, 1)));
   HIP_TRY(o->rng_sorted.ensure(sizeof(float) * (size_t)std::max(m, 1)));
-  if (m > 0)
-    median_range_async(o->s, o->a.as<float4>(), m, o->rng.as<float>(), o->rng_sorted.as<float>(), o->cubtmp.p,
-                       o->cubtmp.bytes, o->median_pin);
-  else
-    *o->median_pin = 0.f;
+  {
+    hipStream_t sm = o->s2m->stream;
+    HIP_TRY(hipEventRecord(o->med_in, o->s));
+    HIP_TRY(hipStreamWaitEvent(sm, o->med_in, 0));
+    if (m > 0)
+      median_range_async(sm, o->a.as<float4>(), m, o->rng.as<float>(), o->rng_sorted.as<float>(), o->medtmp.p,
+                         o->medtmp.bytes, o->median_pin);
+    else
+      *o->median_pin = 0.f;
+    HIP_TRY(hipEventRecord(o->med_done, sm));
+  }
   // computeMetrics + setAdaptiveParams (odom.cc:981-1001, 1156-1178), once
   // the median has arrived
   auto metrics = [&]() {
+    (void)hipEventSynchronize(o->med_done);
     const float median_curr = *o->median_pin;
     if (!o->have_median) {  // static float median_prev = median_curr (first call)
       o->median_prev = median_curr;

@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void k_gather_cov6(const double* __restrict__ 
 // host launchers
 // ============================================================================
 int crop_box(hipStream_t s, const float4* in, int n, float size, float4* out, int* keep, int* pos, void* tmp,
-             size_t tmp_bytes, int* count_host) {
+             size_t tmp_bytes, int* count_host, int* pin) {
   if (n <= 0) {
     *count_host = 0;
     return 0;
@@ -238,11 +238,10 @@ int crop_box(hipStream_t s, const float4* in, int n, float size, float4* out, in
   if (need > tmp_bytes) return -1;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, need, keep, pos, n, s);
   k_compact<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, keep, pos, out);
-  int last_pos = 0, last_keep = 0;
-  (void)hipMemcpyAsync(&last_pos, pos + n - 1, sizeof(int), hipMemcpyDeviceToHost, s);
-  (void)hipMemcpyAsync(&last_keep, keep + n - 1, sizeof(int), hipMemcpyDeviceToHost, s);
+  (void)hipMemcpyAsync(pin, pos + n - 1, sizeof(int), hipMemcpyDeviceToHost, s);
+  (void)hipMemcpyAsync(pin + 1, keep + n - 1, sizeof(int), hipMemcpyDeviceToHost, s);
   (void)hipStreamSynchronize(s);
-  *count_host = last_pos + last_keep;
+  *count_host = pin[0] + pin[1];
   return 0;
 }
 size_t crop_box_tmp_bytes(int n) {
@@ -265,8 +264,10 @@ size_t voxel_tmp_bytes(int n) {
 // keys_sorted[n], idx[n], order[n], uniq[n], counts[n], offsets[n], small[16],
 // part[6 * 64] floats.  Returns the output count in *count_host (-1 if the
 // grid overflows: the caller copies the input, as the reference does).
+// pin: 16 ints of pinned host memory (the read-back of small).  small needs
+// no clearing: every slot the host reads ([5], [6], [8], [9]) is written.
 int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, int* scratch, void* tmp, size_t tmp_bytes,
-               int* count_host, float crop) {
+               int* count_host, float crop, int* pin) {
   *count_host = 0;
   if (n <= 0) return 0;
   unsigned* keys = reinterpret_cast<unsigned*>(scratch);
@@ -280,7 +281,6 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   float* part = reinterpret_cast<float*>(small + 16);
   // inverse_leaf_size_ = 1 / leaf_size_ (float)
   const float inv = 1.0f / leaf;
-  (void)hipMemsetAsync(small, 0, 16 * sizeof(int), s);
   k_minmax_partial<<<kVoxParts, 256, 0, s>>>(in, n, crop, part);
   k_voxel_keys<<<cdiv_l(n, 256), 256, 0, s>>>(in, n, inv, inv, inv, crop, part, small, keys, idx);
   size_t need = voxel_tmp_bytes(n);
@@ -292,8 +292,8 @@ int voxel_grid(hipStream_t s, const float4* in, int n, float leaf, float4* out, 
   k_voxel_tail<<<1, 64, 0, s>>>(uniq, n, small);
   t = tmp_bytes;
   (void)hipcub::DeviceScan::ExclusiveSum(tmp, t, counts, offsets, n, s);
-  int h[16];
-  (void)hipMemcpyAsync(h, small, sizeof(h), hipMemcpyDeviceToHost, s);
+  int* const h = pin;
+  (void)hipMemcpyAsync(h, small, 16 * sizeof(int), hipMemcpyDeviceToHost, s);
   (void)hipStreamSynchronize(s);
   if (h[6]) return 0;            // no (finite, uncropped) point
   if (h[5]) {                    // grid overflow: the reference leaves the cloud as it is

@@ -522,7 +522,7 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(grow(c->raw_pts, sizeof(float4) * n, s));
   HIP_TRY(grow(c->partial, sizeof(float) * 6 * nb, s));
   HIP_TRY(grow(c->nonfinite, sizeof(int), s));
-  HIP_TRY(hipMemsetAsync(c->nonfinite.p, 0, sizeof(int), s));
+  if (check_finite) HIP_TRY(hipMemsetAsync(c->nonfinite.p, 0, sizeof(int), s));   // (else never read)
   HIP_TRY(cd->quant.ensure(sizeof(float) * 8));
   launch_pack_bbox(s, raw, stride, N, c->raw_pts.as<float4>(), c->partial.as<float>(),
                    c->nonfinite.as<int>(), nb);
