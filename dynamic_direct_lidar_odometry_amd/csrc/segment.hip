@@ -117,6 +117,13 @@ __global__ __launch_bounds__(256) void k_seg_pixels(SegPixelArgs a) {
 
 inline int cdiv_s(long a, long b) { return (int)((a + b - 1) / b); }
 
+// The labelling's queues, kept across scans (a ddlo_seg keeps one): a fresh
+// set per scan cost four zero-filled allocations of the image size.
+struct LabelWork {
+  std::vector<int> qy, qx, py, px, rows_hit;
+  std::vector<char> line_flag;   // all zero between components
+};
+
 // cloudSegmentation + labelComponents (detection.cpp:510-724) over host images.
 struct Labeller {
   const ddlo_seg_params& p;
@@ -125,14 +132,26 @@ struct Labeller {
   const float* resid;     // H x W or nullptr (icp_residuals_set_ false)
   int* label;             // H x W, in: -1 / 0
   float sin_x, cos_x, sin_y, cos_y, sensor_z;
+  // the angle test without atan2 away from the threshold: atan is monotonic,
+  // so for x > 0 the float atan2f(y, x) (within 1 ulp of atan(y / x)) is
+  // above theta when y / x > tan(theta (1 + 1e-6)) and not above it when
+  // y / x < tan(theta (1 - 1e-6)); in between (and for x <= 0) the
+  // reference's atan2 decides.  Same decisions, one division per edge.
+  double tan_lo = 0.0, tan_hi = 0.0;
+  bool tan_ok = false;
   int label_count = 1;
   std::vector<double>& avg_residual;   // by label
-  std::vector<int> qy, qx, py, px, rows_hit;
-  std::vector<char> line_flag;
+  std::vector<int>& qy;
+  std::vector<int>& qx;
+  std::vector<int>& py;
+  std::vector<int>& px;
+  std::vector<int>& rows_hit;
+  std::vector<char>& line_flag;
 
   Labeller(const ddlo_seg_params& p_, const float* range_, const float* z_, const float* resid_, int* label_,
-           float sensor_z_, std::vector<double>& avg)
-      : p(p_), range(range_), z(z_), resid(resid_), label(label_), sensor_z(sensor_z_), avg_residual(avg) {
+           float sensor_z_, std::vector<double>& avg, LabelWork& w)
+      : p(p_), range(range_), z(z_), resid(resid_), label(label_), sensor_z(sensor_z_), avg_residual(avg), qy(w.qy),
+        qx(w.qx), py(w.py), px(w.px), rows_hit(w.rows_hit), line_flag(w.line_flag) {
     const int H = p.rows, W = p.cols;
     // loadParams :82-83,108-111: ang_res_x_ = 360.0 / float(W_) (double, stored
     // as float), ang_res_y_ = 2 * ang_bottom_ / float(H_ - 1) (float); double sin/cos
@@ -142,12 +161,21 @@ struct Labeller {
     cos_x = (float)std::cos(ang_res_x / 180.0 * M_PI);
     sin_y = (float)std::sin(ang_res_y / 180.0 * M_PI);
     cos_y = (float)std::cos(ang_res_y / 180.0 * M_PI);
+    const double th = (double)p.theta;
+    tan_ok = th > 1e-3 && th < 1.5;   // a threshold well inside (0, pi / 2): both bounds finite and ordered
+    if (tan_ok) {
+      tan_lo = std::tan(th * (1.0 - 1e-6));
+      tan_hi = std::tan(th * (1.0 + 1e-6));
+    }
     const size_t n = (size_t)H * W;
-    qy.resize(n);
-    qx.resize(n);
-    py.resize(n);
-    px.resize(n);
-    line_flag.assign(H, 0);
+    if (qy.size() < n) {   // (grown once; every slot is written before it is read)
+      qy.resize(n);
+      qx.resize(n);
+      py.resize(n);
+      px.resize(n);
+    }
+    if (line_flag.size() != (size_t)H) line_flag.assign(H, 0);
+    rows_hit.clear();
     rows_hit.reserve(H);
     avg_residual.assign(1, 0.0);
   }
@@ -190,8 +218,13 @@ struct Labeller {
         const float d1 = std::max(range[f], range[t]);
         const float d2 = std::min(range[f], range[t]);
         const float sa = dr[k] == 0 ? sin_x : sin_y, ca = dr[k] == 0 ? cos_x : cos_y;
-        const float angle = std::atan2(d2 * sa, d1 - d2 * ca);
-        if (angle > p.theta) {
+        const float y = d2 * sa, x = d1 - d2 * ca;
+        bool pass;
+        const double ratio = x > 0.f ? (double)y / (double)x : 0.0;
+        if (tan_ok && x > 0.f && ratio > tan_hi) pass = true;
+        else if (tan_ok && x > 0.f && ratio < tan_lo) pass = false;
+        else pass = std::atan2(y, x) > p.theta;
+        if (pass) {
           const double zz = z[t];
           if (zz < min_z && zz != 0) min_z = (float)zz;
           else if (zz > max_z) max_z = (float)zz;
@@ -261,10 +294,14 @@ struct ddlo_seg {
   float* pin = nullptr;               // range | label | ground, pinned
   size_t pin_bytes = 0;
   std::vector<float> z;
-  std::vector<float> h_range;
-  std::vector<signed char> h_ground;
-  std::vector<int> h_label;
+  // the last scan's images: the pinned read-back buffers themselves (the
+  // labelling rewrites h_label in place)
+  const float* h_range = nullptr;
+  const signed char* h_ground = nullptr;
+  int* h_label = nullptr;
+  size_t hn = 0;
   std::vector<double> avg;
+  LabelWork work;
   bool have = false;
   ddlo_seg_result last{};
 };
@@ -373,10 +410,11 @@ gicp_status ddlo_seg_process(ddlo_seg* o, const float* xyz_t, size_t stride, con
   const unsigned char* b = reinterpret_cast<const unsigned char*>(xyz_t);
   for (size_t i = 0; i < n; ++i) std::memcpy(&o->z[i], b + i * stride + 8, sizeof(float));
   HIP_TRY(hipStreamSynchronize(o->s));
-  o->h_range.assign(pin_range, pin_range + n);
-  o->h_ground.assign(pin_ground, pin_ground + n);
-  o->h_label.assign(pin_label, pin_label + n);
-  Labeller lb(p, o->h_range.data(), o->z.data(), residual, o->h_label.data(), T[11], o->avg);
+  o->h_range = pin_range;
+  o->h_ground = pin_ground;
+  o->h_label = pin_label;
+  o->hn = n;
+  Labeller lb(p, o->h_range, o->z.data(), residual, o->h_label, T[11], o->avg, o->work);
   lb.run();
   ddlo_seg_result r{};
   r.segments = lb.label_count - 1;
@@ -394,10 +432,10 @@ gicp_status ddlo_seg_process(ddlo_seg* o, const float* xyz_t, size_t stride, con
 gicp_status ddlo_seg_images(ddlo_seg* o, float* range, int8_t* ground, int32_t* label) {
   if (!o) return fail(GICP_EINVAL, "null handle");
   if (!o->have) return fail(GICP_EINVAL, "no processed scan");
-  const size_t n = o->h_range.size();
-  if (range) std::memcpy(range, o->h_range.data(), sizeof(float) * n);
-  if (ground) std::memcpy(ground, o->h_ground.data(), n);
-  if (label) std::memcpy(label, o->h_label.data(), sizeof(int) * n);
+  const size_t n = o->hn;
+  if (range) std::memcpy(range, o->h_range, sizeof(float) * n);
+  if (ground) std::memcpy(ground, o->h_ground, n);
+  if (label) std::memcpy(label, o->h_label, sizeof(int) * n);
   return GICP_OK;
 }
 
@@ -433,7 +471,7 @@ gicp_status ddlo_seg_label_indices(ddlo_seg* o, int32_t* offsets, size_t offsets
   const int L = o->last.segments;
   if (offsets && offsets_cap < (size_t)L + 2) return fail(GICP_EINVAL, "offsets needs segments + 2 entries");
   std::vector<int32_t> cnt(L + 2, 0);
-  const size_t n = o->h_label.size();
+  const size_t n = o->hn;
   for (size_t i = 0; i < n; ++i) {
     const int l = o->h_label[i];
     if (l > 0 && l != kRejected) ++cnt[l + 1];
@@ -458,7 +496,8 @@ gicp_status ddlo_seg_label(const ddlo_seg_params* p, const float* range, const f
   if (gicp_status st = check_params(p)) return st;
   if (!range || !z || !label || (!avg_residual && avg_cap)) return fail(GICP_EINVAL, "invalid argument");
   std::vector<double> avg;
-  Labeller lb(*p, range, z, residual, label, sensor_z, avg);
+  LabelWork work;
+  Labeller lb(*p, range, z, residual, label, sensor_z, avg, work);
   lb.run();
   for (size_t l = 0; l < avg_cap; ++l) avg_residual[l] = l < avg.size() ? avg[l] : 0.0;
   if (segments) *segments = lb.label_count - 1;
