@@ -304,13 +304,23 @@ __device__ __forceinline__ void leaf_block(const CloudDev& c, int base, int cnt,
   vis.st_box += __popcll(mask);
   unsigned long long ex = 0ull;
   const float before = vis.bound();
+  // two leaves per step: both boxes read from LDS together (one LDS round
+  // trip per pair), then tested in leaf order as before
   while (mask) {
     const int b = __builtin_ctzll(mask);
     mask &= mask - 1;
+    const int b2 = mask ? __builtin_ctzll(mask) : b;
+    if (mask) mask &= mask - 1;
     const f4v blo = L->blo[b], bhi = L->bhi[b];
+    const f4v blo2 = L->blo[b2], bhi2 = L->bhi[b2];
     vis.note_leaf(blo, bhi, base + b);   // a visitor may tighten its bound from the box alone
     if (__any(vis.active && vis.need(make_float4(blo.x, blo.y, blo.z, 0.f), make_float4(bhi.x, bhi.y, bhi.z, 0.f))))
       ex |= 1ull << b;
+    if (b2 != b) {
+      vis.note_leaf(blo2, bhi2, base + b2);
+      if (__any(vis.active && vis.need(make_float4(blo2.x, blo2.y, blo2.z, 0.f), make_float4(bhi2.x, bhi2.y, bhi2.z, 0.f))))
+        ex |= 1ull << b2;
+    }
   }
   vis.st_exact += __popcll(ex);
   bool shrink = __any(vis.bound() < before);   // tightened by a box: later blocks see the smaller wave box
