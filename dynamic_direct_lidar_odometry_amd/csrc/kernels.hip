@@ -210,31 +210,29 @@ __global__ __launch_bounds__(256) void k_key_fine(const unsigned long long* __re
   fine[((size_t)slot << kFineBits) + lane] = (unsigned short)(a - lo);
 }
 
-// Per-leaf SoA copy of the sorted points: leaf l = x[32], y[32], z[32], so
+// Per-leaf SoA copy of the sorted points (leaf l = x[32], y[32], z[32], so
 // that a lane's 8 consecutive coordinates are two 16-B loads per axis and
-// pairs of them feed the packed-math distance directly (k_nn_scan).
-__global__ __launch_bounds__(256) void k_leaf_soa(const float4* __restrict__ pts, int npad, float* __restrict__ soa) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npad) return;
-  const float4 p = pts[i];
-  const int l = i / kLeafSize, t = i % kLeafSize;
-  float* o = soa + (size_t)l * 3 * kLeafSize;
-  o[t] = p.x;
-  o[kLeafSize + t] = p.y;
-  o[2 * kLeafSize + t] = p.z;
-}
-
-__global__ __launch_bounds__(256) void k_leaf_boxes(const float4* __restrict__ pts, int n, int nleaves,
-                                                    float4* __restrict__ lo, float4* __restrict__ hi) {
+// pairs of them feed the packed-math distance directly, k_nn_scan) and each
+// leaf's box over its real points, in one pass: thread = sorted position,
+// 32 threads per leaf (8 leaves per block).
+__global__ __launch_bounds__(256) void k_leaf_soa_boxes(const float4* __restrict__ pts, int n, int nleaves,
+                                                        float* __restrict__ soa, float4* __restrict__ lo,
+                                                        float4* __restrict__ hi) {
   const int leaf = blockIdx.x * 8 + (threadIdx.x >> 5);
   const int sub = threadIdx.x & 31;
   const int p = leaf * kLeafSize + sub;
   float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  if (leaf < nleaves && p < n) {
+  if (leaf < nleaves) {   // the sentinel-padded positions of the last leaf are copied too
     const float4 q = pts[p];
-    v[0] = v[3] = q.x;
-    v[1] = v[4] = q.y;
-    v[2] = v[5] = q.z;
+    float* o = soa + (size_t)leaf * 3 * kLeafSize;
+    o[sub] = q.x;
+    o[kLeafSize + sub] = q.y;
+    o[2 * kLeafSize + sub] = q.z;
+    if (p < n) {
+      v[0] = v[3] = q.x;
+      v[1] = v[4] = q.y;
+      v[2] = v[5] = q.z;
+    }
   }
 #pragma unroll
   for (int m = 16; m >= 1; m >>= 1) {
@@ -3150,11 +3148,8 @@ void launch_key_dir(hipStream_t s, const unsigned long long* keys, int n, int* d
   const long max_slots = (long)n / (kFineMin + 1) + 1;   // (fine_dir_ints)
   k_key_fine<<<cdiv(max_slots, 4), 256, 0, s>>>(keys, dir);
 }
-void launch_leaf_soa(hipStream_t s, const float4* pts, int npad, float* soa) {
-  k_leaf_soa<<<cdiv(npad, 256), 256, 0, s>>>(pts, npad, soa);
-}
-void launch_leaf_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float4* lo, float4* hi) {
-  k_leaf_boxes<<<cdiv(nleaves, 8), 256, 0, s>>>(pts, n, nleaves, lo, hi);
+void launch_leaf_soa_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float* soa, float4* lo, float4* hi) {
+  k_leaf_soa_boxes<<<cdiv(nleaves, 8), 256, 0, s>>>(pts, n, nleaves, soa, lo, hi);
 }
 void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int nchild, int nparent, float4* plo,
                         float4* phi) {

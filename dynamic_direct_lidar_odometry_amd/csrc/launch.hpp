@@ -13,8 +13,8 @@ void launch_bbox_final(hipStream_t s, const float* partial, int nparts, float* q
 void launch_morton(hipStream_t s, const float4* pts, int n, const float* quant, unsigned long long* keys, int* vals);
 void launch_gather(hipStream_t s, const float4* raw, const int* perm, int n, int npad, float4* sorted, int* inv_perm);
 void launch_key_dir(hipStream_t s, const unsigned long long* keys, int n, int* dir);
-void launch_leaf_soa(hipStream_t s, const float4* pts, int npad, float* soa);
-void launch_leaf_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float4* lo, float4* hi);
+// the sorted points' per-leaf SoA copy (nleaves whole leaves) and the leaves' boxes (real points only)
+void launch_leaf_soa_boxes(hipStream_t s, const float4* pts, int n, int nleaves, float* soa, float4* lo, float4* hi);
 void launch_level_boxes(hipStream_t s, const float4* clo, const float4* chi, int nchild, int nparent, float4* plo,
                         float4* phi);
 // returns false if k is unsupported (> 64)

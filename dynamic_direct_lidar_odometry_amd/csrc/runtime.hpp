@@ -556,10 +556,10 @@ inline gicp_status build_cloud(gicp_ctx* c, const float* xyz, size_t n, size_t s
   HIP_TRY(cd->dir.ensure(sizeof(int) * (size_t)fine_dir_ints(N)));
   launch_key_dir(s, cd->keys.as<unsigned long long>(), N, cd->dir.as<int>());
   HIP_TRY(cd->soa.ensure(sizeof(float) * 3 * (size_t)npad));
-  launch_leaf_soa(s, cd->pts.as<float4>(), npad, cd->soa.as<float>());
   HIP_TRY(cd->box_lo.ensure(sizeof(float4) * total_boxes));
   HIP_TRY(cd->box_hi.ensure(sizeof(float4) * total_boxes));
-  launch_leaf_boxes(s, cd->pts.as<float4>(), N, cd->lvl_cnt[0], cd->box_lo.as<float4>(), cd->box_hi.as<float4>());
+  launch_leaf_soa_boxes(s, cd->pts.as<float4>(), N, cd->lvl_cnt[0], cd->soa.as<float>(), cd->box_lo.as<float4>(),
+                        cd->box_hi.as<float4>());
   for (int l = 1; l < cd->nlevels; ++l)
     launch_level_boxes(s, cd->box_lo.as<float4>() + cd->lvl_off[l - 1], cd->box_hi.as<float4>() + cd->lvl_off[l - 1],
                        cd->lvl_cnt[l - 1], cd->lvl_cnt[l], cd->box_lo.as<float4>() + cd->lvl_off[l],
