@@ -1,7 +1,7 @@
 // kernels.hip — hand-written gfx950 kernels of the GICP hot path.
 //
 //   K1 index build      k_pack_bbox, k_bbox_final, k_morton, k_gather,
-//                       k_leaf_boxes, k_level_boxes   (radix sort: hipcub, capi.hip)
+//                       k_leaf_soa_boxes, k_level_boxes   (radix sort: hipcub, capi.hip)
 //   K2 kNN-k covariance k_covariances<KCAP,EXACT>        calculate_covariances
 //                                                       nano_gicp_impl.hpp:373-441
 //   K3 correspondences  k_cell_lookup (candidate cells,  update_correspondences
